@@ -1,0 +1,441 @@
+"""ORACLE — test infrastructure only.
+
+CPU restatement (numpy float32, + plain C for the serial point ops in ``pointops.c``) of the
+reference's pose-candidate path. Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the checker /
+CPU baseline. The product path (``genpose2_amd``) never imports it.
+
+Each function cites the reference lines it restates. Parity of this restatement against
+the reference itself is pinned by ``tests/golden/*.npz`` (generated here by importing the
+reference read-only: ``tests/golden/make_golden.py``) and checked in
+``tests/test_oracle_golden.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from genpose2_amd import arch, weights
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+F32 = np.float32
+
+
+# ============================================================ native point ops (pointops.c)
+def _lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "build", "liboracle_pointops.so")
+        if not os.path.exists(path):
+            subprocess.run(["make", "-s", "-C", _HERE], check=True)
+        lib = ctypes.CDLL(path)
+        fp, ip = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)
+        lib.oracle_fps.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip]
+        lib.oracle_ball_query.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                          ctypes.c_int, fp, fp, ip]
+        lib.oracle_fps_block_size.argtypes = [ctypes.c_int]
+        lib.oracle_fps_block_size.restype = ctypes.c_int
+        _LIB = lib
+    return _LIB
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _ip(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def furthest_point_sample(xyz: np.ndarray, npoint: int) -> np.ndarray:
+    """``FurthestPointSampling.forward`` (pointnet2_utils.py:14-44 -> sampling_gpu.cu:94-209)."""
+    xyz = np.ascontiguousarray(xyz, dtype=F32)
+    B, N, _ = xyz.shape
+    idx = np.zeros((B, npoint), dtype=np.int32)
+    _lib().oracle_fps(_fp(xyz), B, N, npoint, _ip(idx))
+    return idx
+
+
+def ball_query(radius: float, nsample: int, xyz: np.ndarray, new_xyz: np.ndarray) -> np.ndarray:
+    """``BallQuery.forward`` (pointnet2_utils.py:226-256 -> ball_query_gpu.cu:9-45)."""
+    xyz = np.ascontiguousarray(xyz, dtype=F32)
+    new_xyz = np.ascontiguousarray(new_xyz, dtype=F32)
+    B, N, _ = xyz.shape
+    M = new_xyz.shape[1]
+    idx = np.zeros((B, M, nsample), dtype=np.int32)
+    _lib().oracle_ball_query(B, N, M, F32(radius), nsample, _fp(new_xyz), _fp(xyz), _ip(idx))
+    return idx
+
+
+def grouping_operation(features: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """(B,C,N),(B,M,ns) -> (B,C,M,ns) (group_points_gpu.cu:47-66)."""
+    B = features.shape[0]
+    return np.stack([features[b][:, idx[b]] for b in range(B)]).astype(F32)
+
+
+def gather_operation(features: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """(B,C,N),(B,M) -> (B,C,M) (sampling_gpu.cu:8-24)."""
+    B = features.shape[0]
+    return np.stack([features[b][:, idx[b]] for b in range(B)]).astype(F32)
+
+
+# ============================================================ encoder (Pointnet2ClsMSG)
+def _conv_bn_relu(x: np.ndarray, sd, prefix: str) -> np.ndarray:
+    """Conv2d 1x1 (no bias) -> BatchNorm2d(eval) -> ReLU (pytorch_utils.py:58-106)."""
+    w = sd[f"{prefix}.conv.weight"][:, :, 0, 0].astype(F32)
+    y = np.einsum("oc,bcms->boms", w, x, optimize=True).astype(F32)
+    g = sd[f"{prefix}.bn.bn.weight"].astype(F32)[:, None, None]
+    b = sd[f"{prefix}.bn.bn.bias"].astype(F32)[:, None, None]
+    mu = sd[f"{prefix}.bn.bn.running_mean"].astype(F32)[:, None, None]
+    var = sd[f"{prefix}.bn.bn.running_var"].astype(F32)[:, None, None]
+    y = (y - mu) / np.sqrt(var + F32(arch.BN_EPS)) * g + b
+    return np.maximum(y, F32(0)).astype(F32)
+
+
+def encoder_forward(sd, pts: np.ndarray, return_levels: bool = False):
+    """``Pointnet2ClsMSG.forward`` (pointnet2.py:244-252) over ``_PointnetSAModuleBase.forward``
+    (pointnet2_modules.py:19-74), QueryAndGroup/GroupAll (pointnet2_utils.py:259-328).
+
+    pts: (B, N, 3) un-centred camera-frame points. Returns (B, 1024)."""
+    xyz = np.ascontiguousarray(pts[..., :3], dtype=F32)
+    feats = None  # (B, C, N)
+    levels = []
+    for lv, branches in enumerate(arch.sa_branches()):
+        npoint = arch.NPOINTS[lv]
+        if npoint is not None:
+            fidx = furthest_point_sample(xyz, npoint)
+            new_xyz = gather_operation(xyz.transpose(0, 2, 1), fidx).transpose(0, 2, 1).copy()
+        else:
+            fidx, new_xyz = None, None
+        outs, bq = [], []
+        for br in branches:
+            if npoint is not None:
+                idx = ball_query(br.radius, br.nsample, xyz, new_xyz)
+                bq.append(idx)
+                gx = grouping_operation(xyz.transpose(0, 2, 1), idx)
+                gx = gx - new_xyz.transpose(0, 2, 1)[..., None]
+                grouped = gx if feats is None else np.concatenate(
+                    [gx, grouping_operation(feats, idx)], axis=1)
+            else:  # GroupAll: raw xyz + features, (B, 3+C, 1, N)
+                gx = xyz.transpose(0, 2, 1)[:, :, None, :]
+                grouped = gx if feats is None else np.concatenate([gx, feats[:, :, None, :]], axis=1)
+            h = grouped.astype(F32)
+            for i in range(len(br.widths) - 1):
+                h = _conv_bn_relu(h, sd, f"pts_encoder.SA_modules.{lv}.mlps.{br.branch}.layer{i}")
+            outs.append(h.max(axis=3))  # max_pool2d over nsample
+        feats = np.concatenate(outs, axis=1).astype(F32)  # (B, C_out, npoint or 1)
+        levels.append(dict(fps_idx=fidx, new_xyz=new_xyz, ball_idx=bq, features=feats))
+        if new_xyz is not None:
+            xyz = new_xyz
+    out = feats[:, :, 0]
+    return (out, levels) if return_levels else out
+
+
+# ============================================================ SDE helpers (sde.py:15-35)
+def ve_sigma(t):
+    """sigma_min * (sigma_max/sigma_min) ** t, in the dtype of ``t`` (sde.py:15-18)."""
+    t = np.asarray(t)
+    dt = t.dtype if t.dtype in (np.float32, np.float64) else np.float64
+    return (dt.type(arch.SIGMA_MIN) * np.power(dt.type(arch.SIGMA_MAX / arch.SIGMA_MIN), t)).astype(dt)
+
+
+def ve_diffusion(t):
+    """sigma(t) * sqrt(2 (ln sigma_max - ln sigma_min)) (sde.py:21-27)."""
+    s = ve_sigma(t)
+    return (s * s.dtype.type(arch.DIFFUSION_SCALE)).astype(s.dtype)
+
+
+def gram_schmidt(rot6: np.ndarray) -> np.ndarray:
+    """``normalize_rotation(.., 'rot_matrix')`` (misc.py:327-344) via rotation_6d_to_matrix
+    (rotation_conversions.py:556-577): b1 = n(a1), b2 = n(a2 - (b1.a2) b1)."""
+    a1, a2 = rot6[:, :3], rot6[:, 3:6]
+    dt = rot6.dtype.type
+    b1 = a1 / np.maximum(np.linalg.norm(a1, axis=-1, keepdims=True), dt(1e-12))
+    b2 = a2 - (b1 * a2).sum(-1, keepdims=True) * b1
+    b2 = b2 / np.maximum(np.linalg.norm(b2, axis=-1, keepdims=True), dt(1e-12))
+    return np.concatenate([b1, b2], axis=-1).astype(rot6.dtype)
+
+
+# ============================================================ score / energy MLP
+def _lin(x, w, b):
+    return (x @ w.T.astype(F32) + b.astype(F32)).astype(F32)
+
+
+def head_features(sd, pts_feat, pose, t):
+    """Shared trunk of PoseScoreNet.forward (scorenet.py:236-249) / PoseEnergyNet.get_energy
+    (energynet.py:152-157): returns (f (R,9) before the sigma division, std (R,1))."""
+    n = "pose_score_net"
+    t = np.asarray(t, dtype=F32).reshape(-1, 1)
+    W = sd[f"{n}.t_encoder.0.W"].astype(F32)
+    x_proj = (t[:, 0][:, None] * W[None, :]) * F32(2) * F32(np.pi)   # scorenet.py:87
+    t_emb = np.concatenate([np.sin(x_proj), np.cos(x_proj)], axis=-1).astype(F32)
+    t_feat = np.maximum(_lin(t_emb, sd[f"{n}.t_encoder.1.weight"], sd[f"{n}.t_encoder.1.bias"]), 0)
+    h = np.maximum(_lin(pose.astype(F32), sd[f"{n}.pose_encoder.0.weight"], sd[f"{n}.pose_encoder.0.bias"]), 0)
+    pose_feat = np.maximum(_lin(h, sd[f"{n}.pose_encoder.2.weight"], sd[f"{n}.pose_encoder.2.bias"]), 0)
+    total = np.concatenate([pts_feat.astype(F32), t_feat, pose_feat], axis=-1)
+    outs = []
+    for hn in arch.HEAD_NAMES:
+        u = np.maximum(_lin(total, sd[f"{n}.{hn}.0.weight"], sd[f"{n}.{hn}.0.bias"]), 0)
+        outs.append(_lin(u, sd[f"{n}.{hn}.2.weight"], sd[f"{n}.{hn}.2.bias"]))
+    return np.concatenate(outs, axis=-1).astype(F32), ve_sigma(t)
+
+
+def score_forward(sd, pts_feat, pose, t):
+    """PoseScoreNet.forward with Rx_Ry_and_T heads (scorenet.py:215-275)."""
+    f, std = head_features(sd, pts_feat, pose, t)
+    return (f / (std + F32(1e-7))).astype(F32)
+
+
+def energy_forward(sd, pts_feat, pose, t):
+    """PoseEnergyNet.get_energy, energy_mode IP, s_theta score, norm identical, decoupled_rt
+    (energynet.py:151-208) -> (R, 2) [rot, trans]."""
+    f, std = head_features(sd, pts_feat, pose, t)
+    s = (f / std).astype(F32)
+    pose = pose.astype(F32)
+    return np.stack([(pose[:, :6] * s[:, :6]).sum(-1), (pose[:, 6:] * s[:, 6:]).sum(-1)], -1).astype(F32)
+
+
+# ============================================================ samplers
+def time_grid(num_steps: int, eps: float = arch.SAMPLING_EPS) -> np.ndarray:
+    """``torch.linspace(1.0, eps, num_steps)`` (samplers.py:129) as float32."""
+    import torch
+    return torch.linspace(1.0, eps, num_steps).numpy().astype(F32)
+
+
+def pc_sample(score_fn: Callable, x0: np.ndarray, pts_center_rows: np.ndarray, num_steps: int,
+              z1: np.ndarray, z2: np.ndarray, snr: float = arch.SNR):
+    """``cond_pc_sampler`` (samplers.py:113-177) with injected noise.
+
+    x0: (R,9) initial state (prior sample or init_x); z1/z2: (T,R,9) the two randn_like draws
+    per step (Langevin :148, predictor :166). Returns (xs (R,T,9), mean_x (R,9))."""
+    ts = time_grid(num_steps)
+    step_size = F32(ts[0] - ts[1])
+    x = x0.astype(F32).copy()
+    R = x.shape[0]
+    xs = []
+    ls_coef = F32(snr * np.sqrt(arch.POSE_DIM))
+    mean_x = x
+    for k, t in enumerate(ts):
+        grad = score_fn(x, np.full((R, 1), t, dtype=F32)).astype(F32)
+        grad_norm = F32(np.linalg.norm(grad, axis=-1).astype(F32).mean(dtype=F32))
+        ls = F32(2) * (ls_coef / grad_norm) ** 2
+        x = (x + ls * grad + np.sqrt(F32(2) * ls) * z1[k]).astype(F32)
+        x[:, :3] /= np.linalg.norm(x[:, :3], axis=-1, keepdims=True)
+        x[:, 3:6] /= np.linalg.norm(x[:, 3:6], axis=-1, keepdims=True)
+        g = ve_diffusion(np.full((R, 1), t, dtype=F32))
+        drift = -(g ** 2) * grad
+        mean_x = (x + drift * step_size).astype(F32)
+        x = (mean_x + g * np.sqrt(step_size) * z2[k]).astype(F32)
+        x[:, :6] = gram_schmidt(x[:, :6])
+        xs.append(x.copy())
+    xs = np.stack(xs, axis=0)
+    xs[:, :, 6:] += pts_center_rows[None].astype(F32)
+    mean_x = mean_x.copy()
+    mean_x[:, 6:] += pts_center_rows.astype(F32)
+    mean_x[:, :6] = gram_schmidt(mean_x[:, :6])
+    return xs.transpose(1, 0, 2), mean_x
+
+
+def ode_sample(score_fn: Callable, x0: np.ndarray, pts_center_rows: np.ndarray, T0: float,
+               num_steps: Optional[int], eps: float = arch.SAMPLING_EPS,
+               atol: float = 1e-5, rtol: float = 1e-5, denoise: bool = True):
+    """``cond_ode_sampler`` (samplers.py:180-258): probability-flow ODE through scipy RK45
+    (the reference's own integrator, scipy/integrate/_ivp/rk.py), float64 state.
+
+    x0: (R,9) float32 initial state (prior(T0) [+ init_x]). Returns (xs, x) float64, nfev."""
+    from scipy import integrate
+    R = x0.shape[0]
+
+    def ode_func(t, y):
+        x = y.reshape(-1, arch.POSE_DIM).astype(F32)
+        tt = np.full((R, 1), F32(t), dtype=F32)   # ones(bs).unsqueeze(-1) * t (float32)
+        s = score_fn(x, tt).astype(F32).reshape(-1)
+        g = ve_diffusion(np.float64(t))            # sde_coeff(torch.tensor(t)) is float64
+        return 0.0 - 0.5 * (g ** 2) * s.astype(np.float64)
+
+    t_eval = None if num_steps is None else np.linspace(T0, eps, num_steps)
+    res = integrate.solve_ivp(ode_func, (T0, eps), x0.reshape(-1).astype(np.float64),
+                              rtol=rtol, atol=atol, method="RK45", t_eval=t_eval)
+    xs = res.y.T.reshape(-1, R, arch.POSE_DIM).copy()
+    x = res.y[:, -1].reshape(R, arch.POSE_DIM).copy()
+    if denoise:
+        ve = np.full((R, 1), F32(eps), dtype=F32)
+        g = ve_diffusion(ve)
+        grad = score_fn(x.astype(F32), ve).astype(F32)
+        drift = (F32(0) - g ** 2 * grad).astype(F32)
+        x = x + drift.astype(np.float64) * ((1 - eps) / (1000 if num_steps is None else num_steps))
+    n_t = xs.shape[0]
+    flat = xs.reshape(n_t * R, -1)
+    flat[:, :6] = gram_schmidt(flat[:, :6])
+    xs = flat.reshape(n_t, R, -1)
+    xs[:, :, 6:] += pts_center_rows[None].astype(F32).astype(np.float64)
+    x[:, :6] = gram_schmidt(x[:, :6])
+    x[:, 6:] += pts_center_rows.astype(F32).astype(np.float64)
+    return xs.transpose(1, 0, 2), x, int(res.nfev)
+
+
+# ============================================================ rotations (rotation_conversions.py)
+def rot6_to_matrix(rot6: np.ndarray) -> np.ndarray:
+    """get_rot_matrix(.., 'rot_matrix') = rotation_6d_to_matrix(x).permute(0,2,1): columns
+    b1, b2, b3 (misc.py:152-153, rotation_conversions.py:556-577)."""
+    g = gram_schmidt(rot6)
+    b1, b2 = g[:, :3], g[:, 3:6]
+    b3 = np.cross(b1, b2)
+    return np.stack([b1, b2, b3], axis=-1).astype(rot6.dtype)
+
+
+def matrix_to_quaternion(m: np.ndarray) -> np.ndarray:
+    """rotation_conversions.py:102-161 (no sign standardisation), wxyz."""
+    m = np.asarray(m)
+    dt = m.dtype.type
+    m00, m01, m02 = m[..., 0, 0], m[..., 0, 1], m[..., 0, 2]
+    m10, m11, m12 = m[..., 1, 0], m[..., 1, 1], m[..., 1, 2]
+    m20, m21, m22 = m[..., 2, 0], m[..., 2, 1], m[..., 2, 2]
+    qa = np.stack([dt(1) + m00 + m11 + m22, dt(1) + m00 - m11 - m22,
+                   dt(1) - m00 + m11 - m22, dt(1) - m00 - m11 + m22], -1)
+    q_abs = np.where(qa > 0, np.sqrt(np.maximum(qa, 0)), dt(0)).astype(m.dtype)
+    cand = np.stack([
+        np.stack([q_abs[..., 0] ** 2, m21 - m12, m02 - m20, m10 - m01], -1),
+        np.stack([m21 - m12, q_abs[..., 1] ** 2, m10 + m01, m02 + m20], -1),
+        np.stack([m02 - m20, m10 + m01, q_abs[..., 2] ** 2, m12 + m21], -1),
+        np.stack([m10 - m01, m20 + m02, m21 + m12, q_abs[..., 3] ** 2], -1)], -2)
+    cand = cand / (dt(2) * np.maximum(q_abs[..., None], dt(0.1)))
+    sel = q_abs.argmax(-1)
+    return np.take_along_axis(cand, sel[..., None, None].repeat(4, -1), -2)[..., 0, :].astype(m.dtype)
+
+
+def quaternion_to_matrix(q: np.ndarray) -> np.ndarray:
+    """rotation_conversions.py:41-70."""
+    r, i, j, k = q[..., 0], q[..., 1], q[..., 2], q[..., 3]
+    two_s = 2.0 / (q * q).sum(-1)
+    o = np.stack([1 - two_s * (j * j + k * k), two_s * (i * j - k * r), two_s * (i * k + j * r),
+                  two_s * (i * j + k * r), 1 - two_s * (i * i + k * k), two_s * (j * k - i * r),
+                  two_s * (i * k - j * r), two_s * (j * k + i * r), 1 - two_s * (i * i + j * j)], -1)
+    return o.reshape(q.shape[:-1] + (3, 3)).astype(q.dtype)
+
+
+def pose_to_quat_rows(res: np.ndarray) -> np.ndarray:
+    """pred_func tail (posenet_agent.py:554-556): [quat_wxyz(GS(res[:, :6])), res[:, 6:]]."""
+    q = matrix_to_quaternion(rot6_to_matrix(res[:, :6]))
+    return np.concatenate([q, res[:, 6:]], -1)
+
+
+def average_quaternion_batch(Q: np.ndarray) -> np.ndarray:
+    """misc.py:295-317 (uniform weights)."""
+    n = Q.shape[1]
+    w = np.full((Q.shape[0], n), 1.0 / n, dtype=Q.dtype)
+    oq = ((Q[:, :, 0:1] > 0).astype(Q.dtype) - Q.dtype.type(0.5)) * 2 * Q
+    A = np.einsum("abi,abk->abik", oq, oq)
+    A = (A * w[:, :, None, None]).sum(1) / w.sum(-1)[:, None, None]
+    _, vec = np.linalg.eigh(A)
+    q = vec[:, :, -1]
+    return (((q[:, 0:1] > 0).astype(Q.dtype) - Q.dtype.type(0.5)) * 2 * q).astype(Q.dtype)
+
+
+# ============================================================ ranking / aggregation
+def sort_poses_by_energy(poses: np.ndarray, energy: np.ndarray):
+    """reward.py:131-155: rotation part ordered by energy[...,0] desc, translation part by
+    energy[...,1] desc."""
+    o_rot = np.argsort(-energy[..., 0], axis=1, kind="stable")
+    o_tr = np.argsort(-energy[..., 1], axis=1, kind="stable")
+    sp = np.take_along_axis(poses, o_rot[..., None], 1).copy()
+    sp[..., 6:] = np.take_along_axis(poses, o_tr[..., None], 1)[..., 6:]
+    se = np.stack([np.take_along_axis(energy[..., 0], o_rot, 1),
+                   np.take_along_axis(energy[..., 1], o_tr, 1)], -1)
+    return sp, se, o_rot, o_tr
+
+
+def aggregate_pose(pred_pose: np.ndarray, pred_energy: np.ndarray, retain_ratio=0.4,
+                   clustering=1, clustering_eps=0.05, clustering_minpts=0.1667):
+    """evaluation_single.py:160-219 for one batch -> (B,4,4) float32."""
+    from sklearn.cluster import DBSCAN
+    bs, K = pred_pose.shape[:2]
+    sp, _, _, _ = sort_poses_by_energy(pred_pose, pred_energy)
+    keep = int(K * retain_ratio)
+    good = sp[:, :keep]
+    R = rot6_to_matrix(good[:, :, :6].reshape(bs * keep, -1))
+    q = matrix_to_quaternion(R).reshape(bs, keep, 4)
+    qa = average_quaternion_batch(q)
+    if clustering:
+        for j in range(bs):
+            D = 1 - (q[j][None] * q[j][:, None]).sum(2) ** 2
+            labels = DBSCAN(eps=clustering_eps, min_samples=int(clustering_minpts * keep)).fit(
+                D.astype(np.float32)).labels_
+            if np.any(labels >= 0):
+                best = np.argmax(np.bincount(labels[labels >= 0]))
+                qa[j] = average_quaternion_batch(q[j, labels == best][None])[0]
+    out = np.zeros((bs, 4, 4), dtype=np.float32)
+    out[:, 3, 3] = 1
+    out[:, :3, :3] = quaternion_to_matrix(qa)
+    out[:, :3, 3] = good[:, :, 6:].mean(1)
+    return out
+
+
+# ============================================================ ScaleNet
+def encode_axes(axes: np.ndarray, dim: int) -> np.ndarray:
+    """genpose_utils.py:8-18."""
+    bs = axes.shape[0]
+    a = axes.reshape(bs, -1, 1).astype(F32)
+    e = (2.0 ** np.arange(dim, dtype=F32)).reshape(1, 1, -1)
+    return np.concatenate([np.sin(e * a).reshape(bs, -1), np.cos(e * a).reshape(bs, -1)], -1).astype(F32)
+
+
+def scale_forward(sd, pts_feat: np.ndarray, axes: np.ndarray) -> np.ndarray:
+    """ScaleNet.forward (scalenet.py:33-49) -> (B,3)."""
+    emb = encode_axes(axes, arch.SCALE_EMB // 18)
+    h = np.maximum(_lin(emb, sd["axes_encoder.0.weight"], sd["axes_encoder.0.bias"]), 0)
+    h = np.maximum(_lin(h, sd["axes_encoder.2.weight"], sd["axes_encoder.2.bias"]), 0)
+    tot = np.concatenate([pts_feat.astype(F32), h], -1)
+    u = np.maximum(_lin(tot, sd["fusion_tail_length.0.weight"], sd["fusion_tail_length.0.bias"]), 0)
+    return _lin(u, sd["fusion_tail_length.2.weight"], sd["fusion_tail_length.2.bias"])
+
+
+# ============================================================ whole pred_func (PC / ODE)
+def pred_func(sd, pts: np.ndarray, pts_center: np.ndarray, repeat_num: int, num_steps: int,
+              sampler: str, prior: np.ndarray, z1=None, z2=None, T0: Optional[float] = None,
+              init_x: Optional[np.ndarray] = None):
+    """``PoseNet.pred_func`` (posenet_agent.py:490-584) with injected noise.
+
+    prior: (B*K, 9) standard-normal draw (scaled here by sigma(T)). Returns
+    (pred_pose (B,K,9), pred_q (B,K,7), pts_feat (B,1024), extra)."""
+    B = pts.shape[0]
+    K = repeat_num
+    feat = encoder_forward(sd, pts)
+    feat_rows = np.repeat(feat, K, axis=0)
+    center_rows = np.repeat(pts_center.astype(F32), K, axis=0)
+
+    def score_fn(x, t):
+        return score_forward(sd, feat_rows, x, t)
+
+    if sampler == "pc":
+        sig = F32(arch.SIGMA_MIN * (arch.SIGMA_MAX / arch.SIGMA_MIN) ** 1.0)
+        x0 = (prior.astype(F32) * sig).astype(F32) if init_x is None else np.repeat(init_x, K, 0)
+        xs, res = pc_sample(score_fn, x0, center_rows, num_steps, z1, z2)
+        extra = dict(xs=xs)
+    elif sampler == "ode":
+        T0 = arch.SDE_T if T0 is None else T0
+        sig = F32(arch.SIGMA_MIN * (arch.SIGMA_MAX / arch.SIGMA_MIN) ** T0)
+        x0 = (prior.astype(F32) * sig).astype(F32)
+        if init_x is not None:
+            x0 = (np.repeat(init_x, K, 0).astype(F32) + x0).astype(F32)
+        xs, res, nfev = ode_sample(score_fn, x0, center_rows, T0, num_steps)
+        extra = dict(xs=xs, nfev=nfev)
+    else:
+        raise NotImplementedError(sampler)
+    q = pose_to_quat_rows(res)
+    return res.reshape(B, K, -1), q.reshape(B, K, -1), feat, extra
+
+
+def get_energy(sd, pts: np.ndarray, pts_center: np.ndarray, pose_samples: np.ndarray, T: float):
+    """``PoseNet.get_energy(mode='test', extract_feature=True)`` (posenet_agent.py:608-705)."""
+    B, K = pose_samples.shape[:2]
+    feat = encoder_forward(sd, pts)
+    rows = pose_samples.reshape(B * K, -1).astype(F32).copy()
+    rows[:, 6:] -= np.repeat(pts_center.astype(F32), K, axis=0)
+    t = np.full((B * K, 1), F32(T), dtype=F32)
+    return energy_forward(sd, np.repeat(feat, K, 0), rows, t).reshape(B, K, 2)

@@ -1,0 +1,92 @@
+"""Pin the oracle (CPU restatement) to outputs of the reference itself.
+
+Fixtures: tests/golden/*.npz, produced by tests/golden/make_golden.py from the imported
+reference with recorded noise and seeded synthetic weights. Tolerances:
+  * index outputs (FPS, ball query, sort orders, DBSCAN labels): exact;
+  * fp32 network outputs: |a-b| <= 1e-5 * max|b| (different but valid fp32 summation orders);
+  * PC sampler: rotation |a-b| <= 1e-4 (north_star), translation relative to max |t| 1e-5;
+  * ODE sampler (scipy RK45, adaptive): T0=0.55 within 1e-5; T0=1.0 the step-size controller
+    may take a different accept/reject path, so the bound is the integrator tolerance scale
+    (5e-4 abs rotation, 1e-4 relative translation).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import oracle
+
+
+def rel(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+@pytest.mark.parametrize("tag", ["n1024", "n2048"])
+def test_encoder_levels(tag, score_sd):
+    g = golden("encoder")
+    feat, levels = oracle.encoder_forward(score_sd, g[f"{tag}_pts"], return_levels=True)
+    for lv in range(4):
+        assert np.array_equal(levels[lv]["fps_idx"], g[f"{tag}_l{lv}_fps"])
+        np.testing.assert_array_equal(levels[lv]["new_xyz"], g[f"{tag}_l{lv}_new_xyz"])
+        for b in range(2):
+            assert np.array_equal(levels[lv]["ball_idx"][b], g[f"{tag}_l{lv}_ball{b}"])
+    for lv in range(5):
+        assert rel(levels[lv]["features"][0], g[f"{tag}_l{lv}_feat0"]) < 1e-5
+    assert rel(feat, g[f"{tag}_feat"]) < 1e-5
+
+
+def test_score_and_energy_heads(score_sd, energy_sd):
+    g = golden("heads")
+    s = oracle.score_forward(score_sd, g["pts_feat"], g["pose"], g["t"])
+    # per-row scale: sigma(t) spans 0.01..50 across rows
+    err = np.abs(s - g["score"]).max(1) / np.abs(g["score"]).max(1)
+    assert err.max() < 1e-5
+    e = oracle.energy_forward(energy_sd, g["pts_feat"], g["pose"], g["t"])
+    err = np.abs(e - g["energy"]).max(1) / np.abs(g["energy"]).max(1)
+    assert err.max() < 1e-5
+
+
+@pytest.mark.parametrize("name", ["pc_k10_t100", "pc_k50_t20"])
+def test_pc_pred_func(name, score_sd):
+    g = golden(name)
+    K, T = int(g["K"]), int(g["T"])
+    pose, q, feat, ex = oracle.pred_func(score_sd, g["pts"], g["pts_center"], K, T, "pc",
+                                         g["prior"], g["z1"], g["z2"])
+    assert rel(feat, g["pts_feat"]) < 1e-5
+    assert np.abs(pose[..., :6] - g["pred_pose"][..., :6]).max() < 1e-4
+    assert rel(pose[..., 6:], g["pred_pose"][..., 6:]) < 1e-5
+    assert np.abs(q[..., :4] - g["pred_q"][..., :4]).max() < 1e-4
+    if "xs" in g.files:
+        xs = ex["xs"].reshape(g["xs"].shape)
+        assert np.abs(xs[..., :6] - g["xs"][..., :6]).max() < 1e-4
+
+
+@pytest.mark.parametrize("tag,rot_tol,tr_rel", [("t055_s20", 1e-5, 1e-5), ("t1_none", 5e-4, 1e-4)])
+def test_ode_pred_func(tag, rot_tol, tr_rel, score_sd):
+    g = golden("ode")
+    steps = int(g[f"{tag}_steps"])
+    steps = None if steps < 0 else steps
+    pose, q, feat, ex = oracle.pred_func(score_sd, g[f"{tag}_pts"], g[f"{tag}_pts_center"], 5, steps,
+                                         "ode", g[f"{tag}_prior"], T0=float(g[f"{tag}_T0"]))
+    gp = g[f"{tag}_pred_pose"]
+    assert pose.dtype == np.float64  # ODE path returns float64
+    assert np.abs(pose[..., :6] - gp[..., :6]).max() < rot_tol
+    assert rel(pose[..., 6:], gp[..., 6:]) < tr_rel
+    if steps is not None:
+        assert ex["nfev"] == int(g[f"{tag}_nfev"])
+        xs = ex["xs"].reshape(g[f"{tag}_xs"].shape)
+        assert np.abs(xs - g[f"{tag}_xs"]).max() < 1e-5 * np.abs(g[f"{tag}_xs"]).max()
+
+
+def test_energy_sort_aggregate_scale(energy_sd, scale_sd):
+    g = golden("pipeline")
+    e = oracle.get_energy(energy_sd, g["pts"], g["pts_center"], g["pred_pose"], 1e-5)
+    assert rel(e, g["energy"]) < 1e-5
+    sp, se, _, _ = oracle.sort_poses_by_energy(g["pred_pose"], g["energy"])
+    assert np.array_equal(sp, g["sorted_pose"]) and np.array_equal(se, g["sorted_energy"])
+    for c in (0, 1):
+        a = oracle.aggregate_pose(g["pred_pose"], g["energy"], clustering=c)
+        assert np.abs(a - g[f"aggregated_c{c}"]).max() < 1e-4
+    a = oracle.aggregate_pose(g["cl_pose"], g["cl_energy"], clustering=1)
+    assert np.abs(a - g["cl_aggregated"]).max() < 1e-4
+    L = oracle.scale_forward(scale_sd, g["pts_feat"], g["scale_axes"])
+    assert rel(L, g["scale_length"]) < 1e-5
