@@ -1,0 +1,214 @@
+"""Benchmark: pose candidates/s (B objects x K candidates x T denoise steps) on MI355X.
+
+One "step" = one PoseNet.pred_func call (PointNet++ encoder + T-step PC sampler) over one batch of
+synthetic objects resident in HBM, i.e. the reference's inference_score stage per batch
+(runners/evaluation_single.py:98-104). Config (BASELINE.json configs[1]): B=64 objects/GPU,
+N=1024 points, K=50 candidates, T=500 steps, ScoreNet only. --config 3 adds EnergyNet + ranking +
+aggregation, --config 5 is the B=256, N=2048, K=100, T=1000 + ScaleNet stress case.
+
+Multi-GPU: one process per GPU (torchrun), objects sharded (weak scaling: B objects per GPU),
+packed weights broadcast once from rank 0 over RCCL, no collective on the timed data path.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    2: dict(B=64, N=1024, K=50, T=500, energy=False, scale=False),
+    3: dict(B=64, N=1024, K=50, T=500, energy=True, scale=False),
+    4: dict(B=256, N=1024, K=50, T=500, energy=True, scale=False),   # per GPU of the 8-GPU B=2048 case
+    5: dict(B=256, N=2048, K=100, T=1000, energy=False, scale=True),
+}
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (and vector) peak
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def broadcast_weights(agent, ws):
+    """RCCL broadcast of the packed weight buffers from rank 0."""
+    if ws > 1:
+        from genpose2_amd import shard
+        shard.broadcast_tensors(shard.model_tensors(agent), src=0)
+
+
+def cpu_baseline(cfg, threads):
+    """Oracle ("port") timing on a bounded sample of the same workload: the encoder on 2 objects
+    and the PC sampler at the full R = B*K rows for a few steps, extrapolated to B objects and T
+    steps (per-object and per-step costs are independent of B and T)."""
+    from genpose2_amd import synthetic, weights
+    from oracle import oracle
+    torch.set_num_threads(threads)
+    B, N, K, T = cfg["B"], cfg["N"], cfg["K"], cfg["T"]
+    sd = weights.synthetic_state_dict("score")
+    pts, center = synthetic.make_batch(77, 2, N)
+    oracle.encoder_forward(sd, pts[:1])
+    t0 = time.perf_counter()
+    feat = oracle.encoder_forward(sd, pts)
+    t_enc_obj = (time.perf_counter() - t0) / 2
+    R = B * K
+    feat_rows = np.repeat(np.resize(feat, (B, feat.shape[1])), K, axis=0)
+    rng = np.random.default_rng(0)
+    ts_sample = 6
+    z = rng.standard_normal((ts_sample, R, 9)).astype(np.float32)
+    x0 = (rng.standard_normal((R, 9)) * 50).astype(np.float32)
+    t0 = time.perf_counter()
+    oracle.pc_sample(lambda x, t: oracle.score_forward(sd, feat_rows, x, t), x0,
+                     np.zeros((R, 3), np.float32), ts_sample, z, z)
+    t_step = (time.perf_counter() - t0) / ts_sample
+    total = t_enc_obj * B + t_step * T
+    return {"value": B * K * T / total, "unit": "pose-candidate-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (numpy fp32, reference unhoisted score form) encoder on 2 objects "
+                      f"({t_enc_obj*1e3:.0f} ms/object) + PC sampler at R={R} rows for {ts_sample} steps "
+                      f"({t_step*1e3:.0f} ms/step), extrapolated to B={B}, T={T}"}
+
+
+def load_traffic():
+    """HBM bytes per pc_step launch from a committed PMC pass (profiles/*pmc*.json), or None."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_pc_step*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfgd = CONFIGS[args.config]
+    ws, rank, local = dist_env()
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from genpose2_amd import aggregate, arch, synthetic
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+
+    B, N, K, T = cfgd["B"], cfgd["N"], cfgd["K"], cfgd["T"]
+    cfg = GenPoseConfig(device=str(dev), sampling_steps=T, eval_repeat_num=K, noise_seed=1234 + rank)
+    score = PoseNet(cfg).eval()
+    broadcast_weights(score, ws)
+    energy = PoseNet(cfg.copy(agent_type="energy")).eval() if cfgd["energy"] else None
+    scale = PoseNet(cfg.copy(agent_type="scale")).eval() if cfgd["scale"] else None
+    for a in (energy, scale):
+        if a is not None:
+            broadcast_weights(a, ws)
+    pts, center = synthetic.make_batch(args.config, B, N, first_object=rank * B)
+    data0 = {"pts": torch.from_numpy(pts).to(dev), "pts_center": torch.from_numpy(center).to(dev)}
+
+    stream = torch.cuda.current_stream(dev)
+    samp_ev = []
+
+    def one_step(record=False):
+        data = dict(data0)
+        if record:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            # bracket only the PC sampler launches (pc_step_kernel x (T+1)) on the launch stream
+            orig = score.heads.pc_sample
+
+            def timed(*a, **k):
+                e0.record(stream)
+                out = orig(*a, **k)
+                e1.record(stream)
+                return out
+            score.heads.pc_sample = timed
+        pose, _ = score.pred_func(data, repeat_num=K)
+        if record:
+            score.heads.pc_sample = orig
+            samp_ev.append((e0, e1))
+        if energy is not None:
+            e = energy.get_energy({"pts": data0["pts"], "pts_center": data0["pts_center"]}, pose, T=1e-5)
+            agg = aggregate.aggregate_pose(pose, e)
+            if scale is not None:
+                scale.pred_scale_func({"pts_feat": data["pts_feat"], "axes": agg[:, :3, :3].contiguous()})
+        elif scale is not None:
+            axes = torch.eye(3, device=dev).expand(B, 3, 3).contiguous()
+            scale.pred_scale_func({"pts_feat": data["pts_feat"], "axes": axes})
+        return pose
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step(record=True)
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    units = B * K * T * ws * args.steps
+    samp_ms = float(np.mean([a.elapsed_time(b) for a, b in samp_ev]))
+    per_launch_s = samp_ms / 1e3 / (T + 1)
+    flop_launch = B * K * arch.score_flops_per_candidate_step()
+    achieved = flop_launch / per_launch_s / 1e12
+    if rank == 0:
+        out = {
+            "metric": "pose candidates/sec (B objs x K cands x T denoise steps)",
+            "value": units / elapsed,
+            "unit": "pose-candidate-steps/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded point clouds, seeded synthetic weights; no checkpoint exists for dino=none)",
+            "config": {"workload": f"config{args.config}: B={B} objects/GPU, N={N} pts, K={K} candidates, T={T} PC "
+                                   f"steps, {'ScoreNet+EnergyNet+ranking/aggregation' if cfgd['energy'] else 'ScoreNet'}"
+                                   f"{' + ScaleNet' if cfgd['scale'] else ''} (encoder + sampler per step)",
+                       "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": load_traffic(),
+                         "kernel": "pc_step_kernel", "flop_per_launch": flop_launch,
+                         "avg_launch_us": per_launch_s * 1e6, "sampler_ms_per_step": samp_ms},
+        }
+        if not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(cfgd, threads) if ws == 1 else None
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

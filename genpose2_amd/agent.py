@@ -1,0 +1,236 @@
+"""``PoseNet``-compatible inference agent (networks/posenet_agent.py:52) on the MI355X path.
+
+Drop-in for the inference members the evaluation runner uses
+(runners/evaluation_single.py:83-104, 129-152, 258-280): ``__init__(cfg)``, ``load_ckpt``,
+``eval``, ``pred_func``, ``get_energy``, ``pred_scale_func`` -- same signatures, argument
+meaning, return shapes/dtypes and data-dict side effects. Training members are out of scope.
+
+Every computation runs in libgenpose_hip.so; this class only moves tensors and scalars.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import aggregate, arch, device as dev, sde, weights
+from .config import GenPoseConfig
+from .ode import rk45_solve
+
+
+def _as_config(cfg) -> GenPoseConfig:
+    if isinstance(cfg, GenPoseConfig):
+        return cfg
+    base = GenPoseConfig()
+    kw = {f: getattr(cfg, f) for f in base.__dataclass_fields__ if hasattr(cfg, f)}
+    return base.copy(**kw)
+
+
+class NoiseFeed:
+    """Injected standard-normal draws for parity runs: ``prior`` (R,9) replaces the prior
+    ``torch.randn`` (sde.py:34); ``z1``/``z2`` (T,R,9) replace the two ``randn_like`` per PC step
+    (samplers.py:148,166)."""
+
+    def __init__(self, prior: torch.Tensor, z1: Optional[torch.Tensor] = None, z2: Optional[torch.Tensor] = None):
+        self.prior, self.z1, self.z2 = prior, z1, z2
+
+
+class PoseNet:
+    def __init__(self, cfg):
+        self.cfg = _as_config(cfg)
+        self.cfg.validate()
+        self.device = torch.device(self.cfg.device)
+        if self.device.type != "cuda":
+            raise ValueError("genpose2_amd runs on a HIP device only (cfg.device must be 'cuda[:i]')")
+        self.is_testing = False
+        self.pts_feature = False
+        self.noise_feed: Optional[NoiseFeed] = None
+        self._calls = 0
+        self._gen = torch.Generator(device=self.device)
+        self._gen.manual_seed(self.cfg.noise_seed)
+        self.weights_source = f"synthetic(seed={self.cfg.seed})"
+        self._build(weights.synthetic_state_dict(self.cfg.agent_type, seed=self.cfg.seed))
+
+    # ------------------------------------------------------------------ model construction
+    def _build(self, sd: weights.StateDict) -> None:
+        weights.check_keys(sd, self.cfg.agent_type)
+        self.state_dict = sd
+        if self.cfg.agent_type in ("score", "energy"):
+            self.encoder = dev.EncoderModel(sd, self.device)
+            self.heads = dev.HeadModel(sd, self.device)
+            self.scale = None
+        else:
+            self.encoder = self.heads = None
+            self.scale = dev.ScaleModel(sd, self.device)
+
+    def load_ckpt(self, name=None, model_dir=None, model_path=False, load_model_only=False):
+        """posenet_agent.py:171-203 path resolution; loads with torch.load(weights_only=True)."""
+        if not model_path:
+            if name not in ("latest", "best"):
+                name = "ckpt_epoch{}".format(name)
+            load_path = os.path.join(model_dir if model_dir is not None else "./results/ckpts/debug",
+                                     "{}.pth".format(name))
+        else:
+            load_path = model_dir
+        sd = weights.load_checkpoint(load_path)
+        self._build(sd)
+        self.weights_source = load_path
+
+    def eval(self):
+        self.is_testing = True
+        return self
+
+    def train(self, mode: bool = True):
+        raise NotImplementedError("training is out of scope for the MI355X inference path")
+
+    # ------------------------------------------------------------------ helpers
+    def _draw_prior(self, R: int) -> torch.Tensor:
+        if self.noise_feed is not None:
+            return self.noise_feed.prior.to(self.device, torch.float32).reshape(R, arch.POSE_DIM)
+        return torch.randn((R, arch.POSE_DIM), generator=self._gen, device=self.device, dtype=torch.float32)
+
+    def _encode(self, data) -> torch.Tensor:
+        return self.encoder.forward(data["pts"])
+
+    @staticmethod
+    def _time_row_and_sigma(heads: dev.HeadModel, t: float):
+        t32 = torch.tensor([t], dtype=torch.float32)
+        sig = float(sde.sigma(t32)[0])
+        return heads.time_proj(t32.to(heads.device)), sig
+
+    # ------------------------------------------------------------------ pred_func
+    @torch.no_grad()
+    def pred_func(self, data, repeat_num, save_path="./visualization_results", return_average_res=False,
+                  init_x: torch.Tensor = None, T0=None, return_process=False):
+        """posenet_agent.py:490-584."""
+        if self.cfg.agent_type != "score":
+            raise NotImplementedError("pred_func needs agent_type='score'")
+        self.is_testing = True
+        feat = self._encode(data)
+        data["pts_feat"] = feat
+        data["rgb_feat"] = None                    # dino none (posenet.py:316-318)
+        bs = data["pts"].shape[0]
+        K = int(repeat_num)
+        R = bs * K
+        self.pts_feature = True
+        center = dev.require_device_tensor(data["pts_center"], "pts_center")
+        pobj = self.heads.object_proj(feat)
+        rep_init = None if init_x is None else init_x.to(self.device).unsqueeze(1).repeat(1, K, 1).view(R, -1)
+        mode = self.cfg.sampler_mode[0]
+        self._calls += 1
+        if mode == "pc":
+            T = int(self.cfg.sampling_steps)
+            tab = sde.pc_step_table(T)
+            tproj = self.heads.time_proj(torch.from_numpy(tab[:, 0]).to(self.device))
+            if rep_init is None:   # prior((R,9)) at T=1 (sde.py:30-34); init_x used as-is (samplers.py:128)
+                x = (self._draw_prior(R) * sde.prior_sigma(arch.SDE_T)).contiguous()
+            else:
+                x = rep_init.to(torch.float32).contiguous().clone()
+            z1 = z2 = None
+            if self.noise_feed is not None and self.noise_feed.z1 is not None:
+                z1 = self.noise_feed.z1.to(self.device, torch.float32).contiguous()
+                z2 = self.noise_feed.z2.to(self.device, torch.float32).contiguous()
+            seed = (self.cfg.noise_seed * 1000003 + self._calls) & 0xFFFFFFFFFFFF
+            want_xs = bool(return_process or self.cfg.save_video)
+            res, q, xs = self.heads.pc_sample(pobj, tproj, tab, x, K, center, z1, z2, seed=seed, want_xs=want_xs)
+            pred_pose = res.view(bs, K, -1)
+            pred_q = q.view(bs, K, -1)
+            in_process = xs.view(bs, K, T, -1) if xs is not None else None
+        elif mode == "ode":
+            pred_pose, pred_q, in_process = self._ode(pobj, center, bs, K, rep_init, T0)
+        else:
+            raise NotImplementedError(mode)
+        self.pts_feature = False
+        if return_average_res:
+            avg = torch.zeros((bs, 7), dtype=pred_q.dtype, device=self.device)
+            avg[:, :4] = aggregate.average_quaternion_batch(pred_q[:, :, :4])
+            avg[:, 4:] = torch.mean(pred_q[:, :, 4:], dim=1)
+            if return_process:
+                return pred_pose, pred_q, avg, in_process
+            return pred_pose, pred_q, avg
+        if return_process:
+            return [pred_pose, in_process]
+        return pred_pose, pred_q
+
+    def _ode(self, pobj, center, bs, K, rep_init, T0):
+        """cond_ode_sampler (samplers.py:180-258) on device."""
+        R = bs * K
+        T0 = arch.SDE_T if T0 is None else float(T0)
+        eps = arch.SAMPLING_EPS
+        steps = self.cfg.sampling_steps
+        x0 = self._draw_prior(R) * sde.prior_sigma(T0)
+        if rep_init is not None:
+            x0 = rep_init.to(torch.float32) + x0
+        cache = {}
+        buf = torch.empty((R, arch.POSE_DIM), dtype=torch.float32, device=self.device)
+
+        def fun(t: float, y: torch.Tensor) -> torch.Tensor:
+            t32 = float(np.float32(t))
+            if t32 not in cache:
+                cache.clear()
+                cache[t32] = self._time_row_and_sigma(self.heads, t32)
+            trow, sig32 = cache[t32]
+            s = self.heads.score(pobj, trow, sig32, y.view(R, -1).to(torch.float32), K, out=buf)
+            g = float(sde.diffusion(torch.tensor(t, dtype=torch.float64)))
+            return -((0.5 * g * g) * s.to(torch.float64)).view(-1)
+
+        t_eval = None if steps is None else np.linspace(T0, eps, steps)
+        _, ys, nfev = rk45_solve(fun, T0, x0.reshape(-1).to(torch.float64), eps, t_eval=t_eval)
+        self.last_nfev = nfev
+        n_t = ys.shape[0]
+        x = ys[-1].view(R, -1).clone()
+        # denoise with the PC predictor step (samplers.py:240-249)
+        trow, sig32 = self._time_row_and_sigma(self.heads, eps)
+        vec_eps = torch.full((1,), eps, dtype=torch.float32)
+        g32 = sde.diffusion(vec_eps).to(self.device)
+        grad = self.heads.score(pobj, trow, sig32, x.to(torch.float32).contiguous(), K)
+        drift = 0 - g32 ** 2 * grad
+        x = x + drift * ((1 - eps) / (1000 if steps is None else steps))
+        xs = ys.view(n_t * R, -1).clone()
+        xs, _ = dev.pose_epilogue_f64(xs, K, center.repeat(n_t, 1))  # row r -> object (r % R) // K
+        x, q = dev.pose_epilogue_f64(x.contiguous(), K, center)
+        in_process = xs.view(n_t, R, -1).permute(1, 0, 2).reshape(bs, K, n_t, -1)
+        return x.view(bs, K, -1), q.view(bs, K, -1), in_process
+
+    # ------------------------------------------------------------------ get_energy
+    @torch.no_grad()
+    def get_energy(self, data, pose_samples, T=None, mode="test", extract_feature=True):
+        """posenet_agent.py:608-705 (mode='test')."""
+        if mode == "train":
+            raise NotImplementedError("training is out of scope for the MI355X inference path")
+        if mode != "test":
+            raise NotImplementedError
+        if self.cfg.agent_type != "energy":
+            raise NotImplementedError("get_energy needs agent_type='energy'")
+        self.is_testing = True
+        bs, K = pose_samples.shape[0], pose_samples.shape[1]
+        R = bs * K
+        feat = self._encode(data) if extract_feature else dev.require_device_tensor(data["pts_feat"], "pts_feat")
+        self.pts_feature = True
+        pobj = self.heads.object_proj(feat)
+        pose = pose_samples.to(self.device).reshape(R, -1).to(torch.float32).clone()
+        center = dev.require_device_tensor(data["pts_center"], "pts_center")
+        pose[:, -3:] -= center.unsqueeze(1).repeat(1, K, 1).view(R, -1)
+        if T is not None:
+            trow, sig = self._time_row_and_sigma(self.heads, float(np.float32(T)))
+            energy = self.heads.energy(pobj, trow, sig, pose, K)
+        else:  # per-object t ~ randint([1e-5, 1e-4)) (posenet_agent.py:677-687)
+            ts = torch.randint(1, 10, (bs,), generator=torch.Generator().manual_seed(self._calls)).float() / 1e5
+            energy = torch.empty((R, 2), dtype=torch.float32, device=self.device)
+            for b in range(bs):
+                trow, sig = self._time_row_and_sigma(self.heads, float(ts[b]))
+                energy[b * K:(b + 1) * K] = self.heads.energy(pobj[b:b + 1], trow, sig, pose[b * K:(b + 1) * K], K)
+        self._calls += 1
+        return energy.view(bs, K, -1)
+
+    # ------------------------------------------------------------------ pred_scale_func
+    @torch.no_grad()
+    def pred_scale_func(self, data):
+        """posenet_agent.py:586-606 -> (axes, length (B,3))."""
+        if self.cfg.agent_type != "scale":
+            raise NotImplementedError("pred_scale_func needs agent_type='scale'")
+        self.is_testing = True
+        length = self.scale.forward(data["axes"], data["pts_feat"])
+        return data["axes"], length

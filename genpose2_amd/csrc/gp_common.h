@@ -1,0 +1,87 @@
+// Shared device helpers for the GenPose++ MI355X kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/genpose_hip.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define GP_WAVE 64
+
+// --------------------------------------------------------------- error plumbing (host)
+void gp_set_error(const char* fmt, ...);
+int gp_check_launch(const char* what);
+
+#define GP_REQUIRE(cond, ...)                   \
+    do {                                        \
+        if (!(cond)) {                          \
+            gp_set_error(__VA_ARGS__);          \
+            return GP_ERR_INVALID;              \
+        }                                       \
+    } while (0)
+
+// --------------------------------------------------------------- MFMA (exact f32)
+// D = A(16x4) * B(4x16) + C.  Lane l supplies A[l&15][l>>4] and B[l>>4][l&15]; C/D lane l
+// holds rows 4*(l>>4)+j, column l&15 (j = register 0..3).
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// One 16-deep k-group: 4 MFMAs with the lane's A float4 / B float4 (k = 16g + 4q + j).
+__device__ __forceinline__ f32x4 mfma_kgroup(const f32x4 a, const f32x4 b, f32x4 c) {
+    c = mfma4(a.x, b.x, c);
+    c = mfma4(a.y, b.y, c);
+    c = mfma4(a.z, b.z, c);
+    c = mfma4(a.w, b.w, c);
+    return c;
+}
+
+__device__ __forceinline__ f32x4 relu4(f32x4 v) {
+    return f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// Non-contracted fp32 arithmetic (mirrors the reference's separately rounded torch ops).
+__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
+__device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+
+// Squared distance exactly as the reference CUDA text writes it: (dx*dx + dy*dy) + dz*dz
+// with every operation rounded separately (no FMA contraction).
+__device__ __forceinline__ float dist2_ref(float ax, float ay, float az, float bx, float by, float bz) {
+    const float dx = fsub(ax, bx), dy = fsub(ay, by), dz = fsub(az, bz);
+    return fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
+}
+
+// --------------------------------------------------------------- Philox4x32-10 + Box-Muller
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * ctr.x;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * ctr.z;
+        ctr = u32x4{(uint32_t)(p1 >> 32) ^ ctr.y ^ k0, (uint32_t)p1,
+                    (uint32_t)(p0 >> 32) ^ ctr.w ^ k1, (uint32_t)p0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return ctr;
+}
+
+__device__ __forceinline__ float u01(uint32_t v) {  // (0,1]
+    return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+// 4 standard normals for (seed, stream, row, block).
+__device__ __forceinline__ f32x4 philox_normal4(uint64_t seed, uint32_t stream, uint32_t row,
+                                                uint32_t blk) {
+    u32x4 r = philox4x32_10(u32x4{row, blk, stream, 0x5EEDu}, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float r0 = sqrtf(-2.0f * logf(u01(r.x))), r1 = sqrtf(-2.0f * logf(u01(r.z)));
+    const float a0 = 6.2831853071795864f * u01(r.y), a1 = 6.2831853071795864f * u01(r.w);
+    return f32x4{r0 * cosf(a0), r0 * sinf(a0), r1 * cosf(a1), r1 * sinf(a1)};
+}

@@ -1,0 +1,318 @@
+// PointNet++ MSG set-abstraction encoder for gfx950 (Pointnet2ClsMSG(0), Light config:
+// networks/pts_encoder/pointnet2.py:77-89, 211-252; SA module pointnet2_modules.py:19-124).
+//
+// The reference materialises every grouped tensor (B, 3+C, M, ns) in HBM (group_points_gpu.cu)
+// and runs each 1x1 conv + BN + ReLU as a separate cuDNN call, then max-pools. Here one kernel
+// per (level, branch) does gather -> 2-3 BN-folded layers -> ReLU -> max-pool with the grouped
+// tile never leaving the CU:
+//   * grouped rows are MFMA columns (16 per column tile), output channels are MFMA rows, so
+//     the weights are the streamed A operand (packed once by genpose2_amd/pack.py into the
+//     exact per-lane fragment order: one 1 KiB coalesced load feeds 4 MFMAs per column tile);
+//   * layer-0 B fragments are gathered straight from the previous level's point-major
+//     features (one float4 = 4 channels of one neighbour per lane) with the relative xyz as the
+//     last k-group (input channels are permuted [feats | xyz | pad] so feature float4s align);
+//   * inter-layer activations live in LDS in the MFMA accumulator's native layout, so a layer
+//     writes and the next reads 1 KiB per wave-instruction, linear and conflict-free;
+//   * the max over nsample is taken on the accumulators with 16-lane shuffles.
+// Exact f32 MFMA (v_mfma_f32_16x16x4_f32): no precision is traded.
+#include "gp_common.h"
+
+int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const int* m, int* const* idx,
+                        float* const* nxyz, hipStream_t st);
+int gp_launch_ball_query2(int b, int n, int m, float ra, float rb, int nsa, int nsb, const float* new_xyz,
+                          const float* xyz, int* idxa, int* idxb, hipStream_t st);
+
+struct SAArgs {
+    int n_prev, c_prev, m, ns, cols;  // cols = columns per object (m*ns, or n_prev for group-all)
+    const float* xyz_prev;            // (B, n_prev, 3)
+    const float* feat_prev;           // (B, n_prev, c_prev) or null
+    const float* cent;                // (B, m, 3) or null (group-all: raw xyz)
+    const int* nbr;                   // (B, m, ns) or null (group-all)
+    int nlayers;
+    const float* w[3];
+    const float* bias[3];
+    int kg[3];                        // k-groups (k_pad / 16)
+    int nt[3];                        // output tiles (n_pad / 16)
+    float* out;                       // (B, m, c_out_total)
+    int c_out_total, out_off;
+    int buf1_off;                     // float4 offset of the second LDS buffer
+};
+
+constexpr int SA_THREADS = 256;
+
+template <int CT, int TC, int SPAN>
+__global__ __launch_bounds__(SA_THREADS) void sa_branch_kernel(SAArgs a) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int q = lane >> 4, nn = lane & 15;
+    const int b = blockIdx.y;
+    const int col0 = blockIdx.x * CT * 16;
+    const int tpc = a.ns >> 4;  // column tiles per centroid
+
+    // per-lane gathered point of each column tile + the xyz k-group fragment
+    int pi[CT];
+    bool valid[CT];
+    f32x4 bx[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        const int col = col0 + ct * 16 + nn;
+        valid[ct] = col < a.cols;
+        const int m = col / a.ns, s = col - m * a.ns;
+        int p = 0;
+        if (valid[ct]) p = a.nbr ? a.nbr[((size_t)b * a.m + m) * a.ns + s] : s;
+        pi[ct] = p;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (valid[ct] && q == 0) {
+            const float* px = a.xyz_prev + ((size_t)b * a.n_prev + p) * 3;
+            if (a.cent) {  // grouped_xyz -= new_xyz (pointnet2_utils.py:281-282)
+                const float* c = a.cent + ((size_t)b * a.m + m) * 3;
+                v = f32x4{fsub(px[0], c[0]), fsub(px[1], c[1]), fsub(px[2], c[2]), 0.f};
+            } else {       // GroupAll keeps raw xyz (pointnet2_utils.py:316-324)
+                v = f32x4{px[0], px[1], px[2], 0.f};
+            }
+        }
+        bx[ct] = v;
+    }
+    const int feat_groups = a.c_prev >> 4;
+
+    for (int L = 0; L < a.nlayers; ++L) {
+        const int KG = a.kg[L], NT = a.nt[L];
+        const float* __restrict__ W = a.w[L];
+        const f32x4* in_lds = (L == 1) ? lds : lds + a.buf1_off;   // L>=1 reads buffer (L-1)&1
+        f32x4* out_lds = (L == 0) ? lds : lds + a.buf1_off;         // L<last writes buffer L&1
+        const bool last = (L == a.nlayers - 1);
+        for (int T0 = wid * TC; T0 < NT; T0 += 4 * TC) {
+            f32x4 acc[TC][CT];
+#pragma unroll
+            for (int t = 0; t < TC; ++t)
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int g = 0; g < KG; ++g) {
+                f32x4 bf[CT];
+                if (L == 0) {
+                    if (g < feat_groups) {
+#pragma unroll
+                        for (int ct = 0; ct < CT; ++ct)
+                            bf[ct] = valid[ct] ? ld4(a.feat_prev + ((size_t)b * a.n_prev + pi[ct]) * a.c_prev +
+                                                     16 * g + 4 * q)
+                                               : f32x4{0.f, 0.f, 0.f, 0.f};
+                    } else {
+#pragma unroll
+                        for (int ct = 0; ct < CT; ++ct) bf[ct] = bx[ct];
+                    }
+                } else {
+#pragma unroll
+                    for (int ct = 0; ct < CT; ++ct) bf[ct] = in_lds[(g * CT + ct) * 64 + lane];
+                }
+#pragma unroll
+                for (int t = 0; t < TC; ++t) {
+                    const int T = T0 + t;
+                    if (T < NT) {
+                        const f32x4 af = ld4(W + ((size_t)(T * KG + g) * 64 + lane) * 4);
+#pragma unroll
+                        for (int ct = 0; ct < CT; ++ct) acc[t][ct] = mfma_kgroup(af, bf[ct], acc[t][ct]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < TC; ++t) {
+                const int T = T0 + t;
+                if (T >= NT) continue;
+                const f32x4 bias = ld4(a.bias[L] + 16 * T + 4 * q);
+                if (!last) {
+#pragma unroll
+                    for (int ct = 0; ct < CT; ++ct) out_lds[(T * CT + ct) * 64 + lane] = relu4(acc[t][ct] + bias);
+                } else {
+                    // max over nsample: across the centroid's SPAN column tiles, then 16 lanes
+#pragma unroll
+                    for (int cb = 0; cb < CT; cb += SPAN) {
+                        f32x4 v = relu4(acc[t][cb] + bias);
+#pragma unroll
+                        for (int u = 1; u < SPAN; ++u) {
+                            const f32x4 w2 = relu4(acc[t][cb + u] + bias);
+                            v = f32x4{fmaxf(v.x, w2.x), fmaxf(v.y, w2.y), fmaxf(v.z, w2.z), fmaxf(v.w, w2.w)};
+                        }
+#pragma unroll
+                        for (int off = 8; off >= 1; off >>= 1) {
+                            v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
+                            v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
+                            v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
+                            v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
+                        }
+                        const int colc = col0 + cb * 16;
+                        if (nn == 0 && colc < a.cols) {
+                            const int m = colc / a.ns;
+                            float* o = a.out + ((size_t)b * a.m + m) * a.c_out_total + a.out_off + 16 * T + 4 * q;
+                            if (tpc <= CT) {
+                                st4(o, v);
+                            } else {  // centroid split over workgroups: post-ReLU values are >= 0
+                                unsigned int* u = reinterpret_cast<unsigned int*>(o);
+                                atomicMax(u + 0, __float_as_uint(v.x));
+                                atomicMax(u + 1, __float_as_uint(v.y));
+                                atomicMax(u + 2, __float_as_uint(v.z));
+                                atomicMax(u + 3, __float_as_uint(v.w));
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ============================================================================ host side
+static const int kNpoint[4] = {512, 256, 128, 64};
+static const int kNs[2] = {16, 32};
+static const float kRadius[4][2] = {{0.01f, 0.02f}, {0.02f, 0.04f}, {0.04f, 0.08f}, {0.08f, 0.16f}};
+static const int kWidths[5][2][4] = {
+    {{3, 16, 16, 32}, {3, 32, 32, 64}},
+    {{99, 64, 64, 128}, {99, 64, 96, 128}},
+    {{259, 128, 196, 256}, {259, 128, 196, 256}},
+    {{515, 256, 256, 512}, {515, 256, 384, 512}},
+    {{1027, 512, 512, 0}, {1027, 512, 512, 0}}};
+static const int kCout[5] = {96, 256, 512, 1024, 1024};
+
+static inline int pad16(int v) { return (v + 15) & ~15; }
+
+struct EncLayout {
+    size_t fps[4], nxyz[4], ball[4][2], feat[5], total;
+};
+
+static EncLayout enc_layout(int B, int N) {
+    EncLayout L;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    for (int l = 0; l < 4; ++l) {
+        const size_t M = kNpoint[l];
+        L.fps[l] = take(sizeof(int) * B * M);
+        L.nxyz[l] = take(sizeof(float) * B * M * 3);
+        L.ball[l][0] = take(sizeof(int) * B * M * kNs[0]);
+        L.ball[l][1] = take(sizeof(int) * B * M * kNs[1]);
+    }
+    for (int l = 0; l < 5; ++l) L.feat[l] = take(sizeof(float) * B * (l < 4 ? kNpoint[l] : 1) * kCout[l]);
+    L.total = off;
+    (void)N;
+    return L;
+}
+
+extern "C" size_t gp_encoder_workspace_size(int b, int n) { return enc_layout(b, n).total; }
+
+extern "C" int gp_encoder_workspace_layout(int b, int n, int64_t* offsets) {
+    GP_REQUIRE(offsets, "encoder_workspace_layout: null offsets");
+    const EncLayout L = enc_layout(b, n);
+    for (int l = 0; l < 5; ++l) {
+        offsets[l * 5 + 0] = l < 4 ? (int64_t)L.fps[l] : -1;
+        offsets[l * 5 + 1] = l < 4 ? (int64_t)L.nxyz[l] : -1;
+        offsets[l * 5 + 2] = l < 4 ? (int64_t)L.ball[l][0] : -1;
+        offsets[l * 5 + 3] = l < 4 ? (int64_t)L.ball[l][1] : -1;
+        offsets[l * 5 + 4] = (int64_t)L.feat[l];
+    }
+    return GP_OK;
+}
+
+template <int CT>
+static int launch_sa(const SAArgs& a, int B, hipStream_t st) {
+    size_t buf0 = 0, buf1 = 0;
+    if (a.nlayers >= 2) buf0 = (size_t)CT * 16 * a.nt[0] * 16;                 // floats
+    if (a.nlayers >= 3) buf1 = (size_t)CT * 16 * a.nt[1] * 16;
+    SAArgs args = a;
+    args.buf1_off = (int)(buf0 / 4);
+    const size_t lds = (buf0 + buf1) * sizeof(float);
+    if (lds > 160 * 1024) {
+        gp_set_error("sa_branch_kernel: LDS %zu bytes exceeds 160 KiB", lds);
+        return GP_ERR_UNSUPPORTED;
+    }
+    const int blocks = (a.cols + CT * 16 - 1) / (CT * 16);
+    const int tpc = a.ns / 16;
+    const int span = tpc < CT ? tpc : CT;
+    if (span == 1)
+        hipLaunchKernelGGL((sa_branch_kernel<CT, 4, 1>), dim3(blocks, B), dim3(SA_THREADS), lds, st, args);
+    else if (span == 2)
+        hipLaunchKernelGGL((sa_branch_kernel<CT, 4, 2>), dim3(blocks, B), dim3(SA_THREADS), lds, st, args);
+    else if (span == 4 && CT >= 4)
+        hipLaunchKernelGGL((sa_branch_kernel<(CT >= 4 ? CT : 4), 4, 4>), dim3(blocks, B), dim3(SA_THREADS), lds, st,
+                           args);
+    else {
+        gp_set_error("sa_branch_kernel: unsupported span %d", span);
+        return GP_ERR_UNSUPPORTED;
+    }
+    return gp_check_launch("sa_branch_kernel");
+}
+
+extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N,
+                                  void* workspace, size_t workspace_bytes, float* feat, hipStream_t st) {
+    GP_REQUIRE(wbuf && layer_off && pts && workspace && feat, "encoder_forward: null pointer");
+    GP_REQUIRE(B >= 1 && N >= kNpoint[0] && N <= 8192, "encoder_forward: need 1<=b and 512<=n<=8192 (b=%d n=%d)",
+               B, N);
+    const EncLayout L = enc_layout(B, N);
+    GP_REQUIRE(workspace_bytes >= L.total, "encoder_forward: workspace %zu < %zu", workspace_bytes, L.total);
+    char* ws = static_cast<char*>(workspace);
+    int* fidx[4];
+    float* nxyz[4];
+    int nin[4], mout[4];
+    for (int l = 0; l < 4; ++l) {
+        fidx[l] = reinterpret_cast<int*>(ws + L.fps[l]);
+        nxyz[l] = reinterpret_cast<float*>(ws + L.nxyz[l]);
+        nin[l] = l == 0 ? N : kNpoint[l - 1];
+        mout[l] = kNpoint[l];
+    }
+    int rc = gp_launch_fps_chain(pts, B, 4, nin, mout, fidx, nxyz, st);
+    if (rc) return rc;
+    for (int l = 0; l < 5; ++l) {
+        const float* xyz_prev = l == 0 ? pts : nxyz[l - 1];
+        const int n_prev = l == 0 ? N : kNpoint[l - 1];
+        int* b0 = nullptr;
+        int* b1 = nullptr;
+        if (l < 4) {
+            b0 = reinterpret_cast<int*>(ws + L.ball[l][0]);
+            b1 = reinterpret_cast<int*>(ws + L.ball[l][1]);
+            rc = gp_launch_ball_query2(B, n_prev, kNpoint[l], kRadius[l][0], kRadius[l][1], kNs[0], kNs[1], nxyz[l],
+                                       xyz_prev, b0, b1, st);
+            if (rc) return rc;
+        }
+        float* out = l < 4 ? reinterpret_cast<float*>(ws + L.feat[l]) : feat;
+        if (l == 4) {  // group-all pools with atomicMax when a centroid spans workgroups
+            if (hipMemsetAsync(out, 0, sizeof(float) * B * kCout[4], st) != hipSuccess)
+                return gp_check_launch("encoder memset");
+        }
+        int out_off = 0;
+        for (int br = 0; br < 2; ++br) {
+            SAArgs a = {};
+            a.n_prev = n_prev;
+            a.c_prev = l == 0 ? 0 : kCout[l - 1];
+            a.m = l < 4 ? kNpoint[l] : 1;
+            a.ns = l < 4 ? kNs[br] : n_prev;
+            a.cols = a.m * a.ns;
+            a.xyz_prev = xyz_prev;
+            a.feat_prev = l == 0 ? nullptr : reinterpret_cast<const float*>(ws + L.feat[l - 1]);
+            a.cent = l < 4 ? nxyz[l] : nullptr;
+            a.nbr = l < 4 ? (br == 0 ? b0 : b1) : nullptr;
+            a.nlayers = l < 4 ? 3 : 2;
+            for (int i = 0; i < a.nlayers; ++i) {
+                const int64_t* o = layer_off + ((l * 2 + br) * 3 + i) * 2;
+                GP_REQUIRE(o[0] >= 0 && o[1] >= 0, "encoder_forward: missing layer %d/%d/%d", l, br, i);
+                a.w[i] = wbuf + o[0];
+                a.bias[i] = wbuf + o[1];
+                const int kin = i == 0 ? a.c_prev + 16 : pad16(kWidths[l][br][i]);
+                a.kg[i] = kin / 16;
+                a.nt[i] = pad16(kWidths[l][br][i + 1]) / 16;
+            }
+            a.out = out;
+            a.c_out_total = kCout[l];
+            a.out_off = out_off;
+            out_off += kWidths[l][br][a.nlayers];
+            if (a.ns % 16 != 0) {
+                gp_set_error("encoder_forward: nsample %d not a multiple of 16", a.ns);
+                return GP_ERR_UNSUPPORTED;
+            }
+            rc = (l == 3) ? launch_sa<2>(a, B, st) : launch_sa<4>(a, B, st);
+            if (rc) return rc;
+        }
+    }
+    return GP_OK;
+}

@@ -1,0 +1,353 @@
+// Point-cloud geometry kernels for gfx950: farthest-point sampling, ball query, gather/group.
+//
+// Semantics follow the reference CUDA text (networks/pts_encoder/pointnet2_utils/pointnet2/
+// src/sampling_gpu.cu, ball_query_gpu.cu, group_points_gpu.cu); the execution design does not.
+//
+// FPS: the reference runs min(2^floor(log2 n),1024) threads, keeps the running min-distance in
+// GLOBAL memory and reduces through a 10-level shared-memory tree with a barrier per level.
+// Here one 256-thread workgroup per object keeps min-distances in VGPRs and the point set in
+// LDS, and picks the farthest point with a single 64-bit max (distance bits | tie key) through
+// wave shuffles + one LDS exchange per iteration. The tie key reproduces the reference winner
+// exactly: the reference prefers, among equal distances, the first point in a thread's strided
+// scan (strict >) and then the lower shared-memory slot at every tree level, i.e. the thread
+// whose index is smallest in bit-reversed order. key = bitrev(k mod bs) << jbits | k / bs.
+//
+// Ball query: one wave per centroid scans 64 points per step with two ballots (both radii of
+// an MSG level at once) and writes the hits in index order with mbcnt ranks; early exit when
+// every list is full.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "gp_common.h"
+
+// ============================================================================ error plumbing
+static thread_local char g_err[512];
+
+void gp_set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int gp_check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gp_set_error("%s: %s", what, hipGetErrorString(e));
+        return GP_ERR_LAUNCH;
+    }
+    return GP_OK;
+}
+
+extern "C" const char* gp_last_error(void) { return g_err; }
+extern "C" int gp_abi_version(void) { return GP_ABI_VERSION; }
+
+// ============================================================================ FPS
+static int fps_block_log2(int n) {  // cuda_utils.h:9-13 (opt_n_threads), exact for n>=1
+    int p = 0;
+    while ((2 << p) <= n && p < 10) ++p;
+    return p;
+}
+
+struct FpsGeom {
+    int nb;      // log2 of the reference block size
+    int jbits;   // bits for k / bs
+};
+
+static FpsGeom fps_geom(int n) {
+    FpsGeom g;
+    g.nb = fps_block_log2(n);
+    const int jmax = (n - 1) >> g.nb;
+    g.jbits = 0;
+    while ((1 << g.jbits) <= jmax) ++g.jbits;
+    return g;
+}
+
+__device__ __forceinline__ uint32_t fps_key(int k, int nb, int jbits) {
+    const uint32_t t = (uint32_t)k & ((1u << nb) - 1u);
+    const uint32_t rt = nb ? (__brev(t) >> (32 - nb)) : 0u;
+    return (rt << jbits) | ((uint32_t)k >> nb);
+}
+
+__device__ __forceinline__ int fps_key_to_k(uint32_t key, int nb, int jbits) {
+    const uint32_t rt = key >> jbits;
+    const uint32_t t = nb ? (__brev(rt) >> (32 - nb)) : 0u;
+    return (int)(t + ((key & ((1u << jbits) - 1u)) << nb));
+}
+
+__device__ __forceinline__ unsigned long long fps_pack(float d2, uint32_t key) {
+    return ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned long long)(0xFFFFFFFFu - key);
+}
+
+constexpr int FPS_THREADS = 256;
+
+// One FPS run over `n` points held in LDS (s_xyz, xyz interleaved). Writes m indices to
+// out_idx (global, may be null) and the selected coordinates to s_out (LDS, may be null) and
+// out_xyz (global, may be null). All 256 threads must call it.
+template <int PMAX>
+__device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits,
+                        unsigned long long* s_red /* [2][4] */, int* out_idx, float* s_out,
+                        float* out_xyz) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    float px[PMAX], py[PMAX], pz[PMAX], tmin[PMAX];
+    uint32_t key[PMAX];
+#pragma unroll
+    for (int p = 0; p < PMAX; ++p) {
+        const int k = tid + p * FPS_THREADS;
+        const bool ok = k < n;
+        px[p] = ok ? s_xyz[3 * k + 0] : 0.f;
+        py[p] = ok ? s_xyz[3 * k + 1] : 0.f;
+        pz[p] = ok ? s_xyz[3 * k + 2] : 0.f;
+        tmin[p] = 1e10f;                        // pointnet2_utils.py:32-34
+        key[p] = ok ? fps_key(k, nb, jbits) : 0u;
+    }
+    int old = 0;
+    if (m <= 0) return;
+    if (tid == 0) {
+        if (out_idx) out_idx[0] = 0;
+    }
+    if (tid < 3) {
+        if (s_out) s_out[tid] = s_xyz[tid];
+        if (out_xyz) out_xyz[tid] = s_xyz[tid];
+    }
+    for (int j = 1; j < m; ++j) {
+        const float x1 = s_xyz[3 * old + 0], y1 = s_xyz[3 * old + 1], z1 = s_xyz[3 * old + 2];
+        unsigned long long best = 0ull;
+#pragma unroll
+        for (int p = 0; p < PMAX; ++p) {
+            const int k = tid + p * FPS_THREADS;
+            if (k < n) {
+                const float d = dist2_ref(px[p], py[p], pz[p], x1, y1, z1);
+                const float d2 = fminf(d, tmin[p]);
+                tmin[p] = d2;
+                const unsigned long long c = fps_pack(d2, key[p]);
+                best = c > best ? c : best;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned long long o = __shfl_xor(best, off, 64);
+            best = o > best ? o : best;
+        }
+        unsigned long long* red = s_red + (j & 1) * 4;
+        if (lane == 0) red[wid] = best;
+        __syncthreads();
+        unsigned long long b = red[0];
+#pragma unroll
+        for (int w = 1; w < FPS_THREADS / 64; ++w) b = red[w] > b ? red[w] : b;
+        old = fps_key_to_k(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull), nb, jbits);
+        if (tid == 0 && out_idx) out_idx[j] = old;
+        if (tid < 3) {
+            const float v = s_xyz[3 * old + tid];
+            if (s_out) s_out[3 * j + tid] = v;
+            if (out_xyz) out_xyz[3 * j + tid] = v;
+        }
+    }
+}
+
+template <int PMAX>
+__global__ __launch_bounds__(FPS_THREADS) void fps_kernel(const float* __restrict__ xyz, int n, int m,
+                                                          int nb, int jbits, int* __restrict__ idx) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(smem);
+    float* s_xyz = reinterpret_cast<float*>(smem + 64);
+    const int b = blockIdx.x;
+    const float* src = xyz + (size_t)b * n * 3;
+    for (int i = threadIdx.x; i < 3 * n; i += FPS_THREADS) s_xyz[i] = src[i];
+    __syncthreads();
+    fps_run<PMAX>(s_xyz, n, m, nb, jbits, s_red, idx + (size_t)b * m, nullptr, nullptr);
+}
+
+static int launch_fps(const float* xyz, int b, int n, int m, int* idx, hipStream_t st) {
+    const FpsGeom g = fps_geom(n);
+    const size_t lds = 64 + sizeof(float) * 3 * (size_t)n;
+    const int p = (n + FPS_THREADS - 1) / FPS_THREADS;
+#define GP_FPS_CASE(PM)                                                                      \
+    if (p <= PM) {                                                                           \
+        hipLaunchKernelGGL(fps_kernel<PM>, dim3(b), dim3(FPS_THREADS), lds, st, xyz, n, m, g.nb, \
+                           g.jbits, idx);                                                    \
+        return gp_check_launch("fps_kernel");                                                \
+    }
+    GP_FPS_CASE(1) GP_FPS_CASE(2) GP_FPS_CASE(4) GP_FPS_CASE(8) GP_FPS_CASE(16) GP_FPS_CASE(32)
+#undef GP_FPS_CASE
+    gp_set_error("furthest_point_sampling: n=%d exceeds 8192", n);
+    return GP_ERR_UNSUPPORTED;
+}
+
+extern "C" int gp_furthest_point_sampling(int b, int n, int m, const float* xyz, float* temp,
+                                          int* idx, hipStream_t stream) {
+    (void)temp;
+    GP_REQUIRE(b >= 0 && n >= 1 && m >= 0, "furthest_point_sampling: bad sizes b=%d n=%d m=%d", b, n, m);
+    GP_REQUIRE(xyz && idx, "furthest_point_sampling: null pointer");
+    if (b == 0 || m == 0) return GP_OK;
+    return launch_fps(xyz, b, n, m, idx, stream);
+}
+
+// ---------------------------------------------------------------------------- FPS chain
+// All SA levels' FPS for one object in one workgroup: level l samples M_l points from the
+// M_{l-1} points chosen by level l-1 (pointnet2_modules.py:39-47 applied level after level).
+struct ChainArgs {
+    int nlev;
+    int n[4];      // input size per level
+    int m[4];      // samples per level
+    int nb[4];
+    int jbits[4];
+    int* idx[4];   // (B, m_l)
+    float* nxyz[4];  // (B, m_l, 3)
+};
+
+template <int PMAX>
+__global__ __launch_bounds__(FPS_THREADS) void fps_chain_kernel(const float* __restrict__ xyz, ChainArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(smem);
+    float* bufA = reinterpret_cast<float*>(smem + 64);
+    float* bufB = bufA + 3 * a.n[0];
+    const int b = blockIdx.x;
+    const float* src = xyz + (size_t)b * a.n[0] * 3;
+    for (int i = threadIdx.x; i < 3 * a.n[0]; i += FPS_THREADS) bufA[i] = src[i];
+    __syncthreads();
+    float* cur = bufA;
+    float* nxt = bufB;
+    for (int l = 0; l < a.nlev; ++l) {
+        fps_run<PMAX>(cur, a.n[l], a.m[l], a.nb[l], a.jbits[l], s_red, a.idx[l] + (size_t)b * a.m[l],
+                      nxt, a.nxyz[l] + (size_t)b * a.m[l] * 3);
+        __syncthreads();
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+}
+
+int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const int* m, int* const* idx,
+                        float* const* nxyz, hipStream_t st) {
+    ChainArgs a;
+    a.nlev = nlev;
+    for (int l = 0; l < nlev; ++l) {
+        a.n[l] = n[l];
+        a.m[l] = m[l];
+        const FpsGeom g = fps_geom(n[l]);
+        a.nb[l] = g.nb;
+        a.jbits[l] = g.jbits;
+        a.idx[l] = idx[l];
+        a.nxyz[l] = nxyz[l];
+    }
+    const size_t lds = 64 + sizeof(float) * 3 * ((size_t)n[0] + (size_t)m[0]);
+    const int p = (n[0] + FPS_THREADS - 1) / FPS_THREADS;
+#define GP_CHAIN_CASE(PM)                                                                       \
+    if (p <= PM) {                                                                              \
+        hipLaunchKernelGGL(fps_chain_kernel<PM>, dim3(b), dim3(FPS_THREADS), lds, st, xyz, a);  \
+        return gp_check_launch("fps_chain_kernel");                                             \
+    }
+    GP_CHAIN_CASE(4) GP_CHAIN_CASE(8) GP_CHAIN_CASE(16) GP_CHAIN_CASE(32)
+#undef GP_CHAIN_CASE
+    gp_set_error("encoder: n=%d exceeds 8192", n[0]);
+    return GP_ERR_UNSUPPORTED;
+}
+
+// ============================================================================ ball query
+// One wave per centroid, NR radii (1 or 2) answered by the same scan.
+template <int NR>
+__global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const float* __restrict__ new_xyz,
+                                                         const float* __restrict__ xyz, float r2a,
+                                                         float r2b, int nsa, int nsb,
+                                                         int* __restrict__ idxa,
+                                                         int* __restrict__ idxb) {
+    const int lane = threadIdx.x & 63;
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    if (p >= m) return;  // wave-uniform
+    const float* c = new_xyz + ((size_t)b * m + p) * 3;
+    const float cx = c[0], cy = c[1], cz = c[2];
+    const float* pts = xyz + (size_t)b * n * 3;
+    int* oa = idxa + ((size_t)b * m + p) * nsa;
+    int* ob = NR > 1 ? idxb + ((size_t)b * m + p) * nsb : nullptr;
+    int cnta = 0, cntb = 0, firsta = -1, firstb = -1;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int base = 0; base < n; base += 64) {
+        const int k = base + lane;
+        float d2 = 3.0e38f;
+        if (k < n) d2 = dist2_ref(cx, cy, cz, pts[3 * k + 0], pts[3 * k + 1], pts[3 * k + 2]);
+        const bool ha = (k < n) && d2 < r2a;
+        const unsigned long long ma = __ballot(ha);
+        if (cnta < nsa && ma) {
+            const int rank = cnta + __popcll(ma & lt);
+            if (ha && rank < nsa) oa[rank] = k;
+            if (firsta < 0) firsta = base + __ffsll((long long)ma) - 1;
+            cnta += __popcll(ma);
+        }
+        if (NR > 1) {
+            const bool hb = (k < n) && d2 < r2b;
+            const unsigned long long mb = __ballot(hb);
+            if (cntb < nsb && mb) {
+                const int rank = cntb + __popcll(mb & lt);
+                if (hb && rank < nsb) ob[rank] = k;
+                if (firstb < 0) firstb = base + __ffsll((long long)mb) - 1;
+                cntb += __popcll(mb);
+            }
+        }
+        if (cnta >= nsa && (NR == 1 || cntb >= nsb)) break;
+    }
+    // pad with the first hit (ball_query_gpu.cu:35-40); no hit -> 0 (zero-initialised output)
+    for (int s = (cnta < nsa ? cnta : nsa) + lane; s < nsa; s += 64) oa[s] = firsta < 0 ? 0 : firsta;
+    if (NR > 1)
+        for (int s = (cntb < nsb ? cntb : nsb) + lane; s < nsb; s += 64) ob[s] = firstb < 0 ? 0 : firstb;
+}
+
+int gp_launch_ball_query2(int b, int n, int m, float ra, float rb, int nsa, int nsb,
+                          const float* new_xyz, const float* xyz, int* idxa, int* idxb,
+                          hipStream_t st) {
+    const float r2a = ra * ra, r2b = rb * rb;  // radius2 = radius * radius in fp32
+    dim3 grid((m + 3) / 4, b);
+    if (idxb)
+        hipLaunchKernelGGL(ball_query_kernel<2>, grid, dim3(256), 0, st, n, m, new_xyz, xyz, r2a, r2b,
+                           nsa, nsb, idxa, idxb);
+    else
+        hipLaunchKernelGGL(ball_query_kernel<1>, grid, dim3(256), 0, st, n, m, new_xyz, xyz, r2a, 0.f,
+                           nsa, 0, idxa, nullptr);
+    return gp_check_launch("ball_query_kernel");
+}
+
+extern "C" int gp_ball_query(int b, int n, int m, float radius, int nsample, const float* new_xyz,
+                             const float* xyz, int* idx, hipStream_t stream) {
+    GP_REQUIRE(b >= 0 && n >= 0 && m >= 0 && nsample >= 1, "ball_query: bad sizes");
+    GP_REQUIRE(new_xyz && xyz && idx, "ball_query: null pointer");
+    if (b == 0 || m == 0) return GP_OK;
+    return gp_launch_ball_query2(b, n, m, radius, 0.f, nsample, 0, new_xyz, xyz, idx, nullptr, stream);
+}
+
+// ============================================================================ gather / group
+__global__ void gather_points_kernel(int c, int n, int m, const float* __restrict__ pts,
+                                     const int* __restrict__ idx, float* __restrict__ out) {
+    const int b = blockIdx.z, ch = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    out[((size_t)b * c + ch) * m + i] = pts[((size_t)b * c + ch) * n + idx[(size_t)b * m + i]];
+}
+
+extern "C" int gp_gather_points(int b, int c, int n, int npoints, const float* points, const int* idx,
+                                float* out, hipStream_t stream) {
+    GP_REQUIRE(b >= 0 && c >= 0 && n >= 0 && npoints >= 0, "gather_points: bad sizes");
+    GP_REQUIRE(points && idx && out, "gather_points: null pointer");
+    if (!b || !c || !npoints) return GP_OK;
+    hipLaunchKernelGGL(gather_points_kernel, dim3((npoints + 255) / 256, c, b), dim3(256), 0, stream, c, n,
+                       npoints, points, idx, out);
+    return gp_check_launch("gather_points_kernel");
+}
+
+__global__ void group_points_kernel(int c, int n, int m, int ns, const float* __restrict__ pts,
+                                    const int* __restrict__ idx, float* __restrict__ out) {
+    const int b = blockIdx.z, ch = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m * ns) return;
+    out[((size_t)b * c + ch) * m * ns + i] = pts[((size_t)b * c + ch) * n + idx[(size_t)b * m * ns + i]];
+}
+
+extern "C" int gp_group_points(int b, int c, int n, int npoints, int nsample, const float* points,
+                               const int* idx, float* out, hipStream_t stream) {
+    GP_REQUIRE(b >= 0 && c >= 0 && n >= 0 && npoints >= 0 && nsample >= 1, "group_points: bad sizes");
+    GP_REQUIRE(points && idx && out, "group_points: null pointer");
+    if (!b || !c || !npoints) return GP_OK;
+    hipLaunchKernelGGL(group_points_kernel, dim3((npoints * nsample + 255) / 256, c, b), dim3(256), 0,
+                       stream, c, n, npoints, nsample, points, idx, out);
+    return gp_check_launch("group_points_kernel");
+}

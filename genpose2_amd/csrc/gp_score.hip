@@ -1,0 +1,583 @@
+// Score / energy heads and the fused PC sampling step for gfx950.
+//
+// Reference: PoseScoreNet.forward (networks/gf_algorithms/scorenet.py:215-275), PoseEnergyNet.get_energy
+// (energynet.py:151-208), cond_pc_sampler (samplers.py:113-177), VE SDE (sde.py:15-35).
+//
+// Hoisting. The first head layer Linear(1408 -> 3x256) sees [pts_feat | t_feat | pose_feat]. The pts
+// block is constant per object and the t block is constant per step, so they are computed once
+// (gp_head_object_proj: B x 1024 x 768, gp_head_time_proj: T x 128 x 768) and enter the per-candidate
+// GEMM as the accumulator's initial value. Per candidate-step only pose 9->256->256 -> 3x256 and the
+// block-diagonal 3x(256->3) remain: 0.5335 MFLOP instead of the reference's 2.336 MFLOP.
+//
+// Tiling. A workgroup (4 waves) owns 16 candidates. Candidates are MFMA columns, output channels are
+// MFMA rows, so weights are the streamed A operand (packed per lane by pack.py: one coalesced 1 KiB
+// load per 4 MFMAs) and activations stay in the accumulator-native LDS layout between layers.
+// Exact f32 MFMA (v_mfma_f32_16x16x4_f32).
+//
+// PC step fusion. The Langevin step size uses the mean score norm over ALL rows of the call
+// (samplers.py:143), a grid-wide dependency. Launch i therefore (a) finishes step i-1 for its own
+// rows -- reading the per-tile norm partials every tile wrote in launch i-1, summed in one fixed
+// order so every workgroup derives the identical grad_norm -- and (b) evaluates the score at step i
+// and publishes its tile's partial. The kernel boundary is the only grid-wide synchronisation.
+#include "gp_common.h"
+
+constexpr int HT = 256;          // threads per workgroup
+constexpr int HID = 256;         // pose/head hidden width
+constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
+
+// ============================================================================ shared head trunk
+struct HeadSmem {
+    float xin[16 * 16];            // input poses, [col][16] (9 used)
+    f32x4 act1[KG_HID * 64];       // pose_encoder.0 output (accumulator-native layout)
+    f32x4 act2[KG_HID * 64];       // pose_encoder.2 output
+    float red[4][9][16];           // per-wave head-layer-2 partials
+    float f[16][9];                // head output before the sigma division
+    float scratch[HT];
+};
+
+// Computes f (16 cols x 9) = heads(x) into sm.f for the 16 candidates of this tile.
+// `obj` maps column -> object row of pobj; `tproj` is the 768-vector of this time value.
+__device__ void head_trunk(const gp_head_weights& w, const float* __restrict__ pobj,
+                           const float* __restrict__ tproj, const int* obj_of_col, HeadSmem& sm) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int q = lane >> 4, n = lane & 15;
+    // ---- pose_encoder.0 (9 -> 256), one k-group
+    {
+        const f32x4 bf = ld4(&sm.xin[n * 16 + 4 * q]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int T = wid * 4 + t;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            acc = mfma_kgroup(ld4(w.pe0_w + ((size_t)T * 64 + lane) * 4), bf, acc);
+            sm.act1[T * 64 + lane] = relu4(acc + ld4(w.pe0_b + 16 * T + 4 * q));
+        }
+    }
+    __syncthreads();
+    // ---- pose_encoder.2 (256 -> 256)
+    {
+        f32x4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int g = 0; g < KG_HID; ++g) {
+            const f32x4 bf = sm.act1[g * 64 + lane];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int T = wid * 4 + t;
+                acc[t] = mfma_kgroup(ld4(w.pe2_w + ((size_t)(T * KG_HID + g) * 64 + lane) * 4), bf, acc[t]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int T = wid * 4 + t;
+            sm.act2[T * 64 + lane] = relu4(acc[t] + ld4(w.pe2_b + 16 * T + 4 * q));
+        }
+    }
+    __syncthreads();
+    // ---- head layer 1 (pose block 256 -> 3x256) + hoisted pts/t blocks, ReLU, head layer 2 partials
+    const int ob = obj_of_col[n];
+    f32x4 acc[3][4];
+#pragma unroll
+    for (int h = 0; h < 3; ++h)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int ch = h * HID + 16 * (wid * 4 + t) + 4 * q;
+            acc[h][t] = ld4(pobj + (size_t)ob * (3 * HID) + ch) + ld4(tproj + ch);
+        }
+    for (int g = 0; g < KG_HID; ++g) {
+        const f32x4 bf = sm.act2[g * 64 + lane];
+#pragma unroll
+        for (int h = 0; h < 3; ++h)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int T = h * 16 + wid * 4 + t;
+                acc[h][t] = mfma_kgroup(ld4(w.h1p_w + ((size_t)(T * KG_HID + g) * 64 + lane) * 4), bf, acc[h][t]);
+            }
+    }
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+        float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const f32x4 u = relu4(acc[h][t]);
+            const int ch = 16 * (wid * 4 + t) + 4 * q;
+            const f32x4 w0 = ld4(w.h2_w + (h * 3 + 0) * HID + ch);
+            const f32x4 w1 = ld4(w.h2_w + (h * 3 + 1) * HID + ch);
+            const f32x4 w2 = ld4(w.h2_w + (h * 3 + 2) * HID + ch);
+            p0 += u.x * w0.x + u.y * w0.y + u.z * w0.z + u.w * w0.w;
+            p1 += u.x * w1.x + u.y * w1.y + u.z * w1.z + u.w * w1.w;
+            p2 += u.x * w2.x + u.y * w2.y + u.z * w2.z + u.w * w2.w;
+        }
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {
+            p0 += __shfl_xor(p0, off, 64);
+            p1 += __shfl_xor(p1, off, 64);
+            p2 += __shfl_xor(p2, off, 64);
+        }
+        if (q == 0) {
+            sm.red[wid][h * 3 + 0][n] = p0;
+            sm.red[wid][h * 3 + 1][n] = p1;
+            sm.red[wid][h * 3 + 2][n] = p2;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 16 * 9) {
+        const int c = threadIdx.x / 9, o = threadIdx.x - c * 9;
+        sm.f[c][o] = w.h2_b[o] + ((sm.red[0][o][c] + sm.red[1][o][c]) + (sm.red[2][o][c] + sm.red[3][o][c]));
+    }
+    __syncthreads();
+}
+
+// ============================================================================ pose helpers
+template <typename T>
+__device__ __forceinline__ T tsqrt(T v);
+template <>
+__device__ __forceinline__ float tsqrt<float>(float v) { return sqrtf(v); }
+template <>
+__device__ __forceinline__ double tsqrt<double>(double v) { return sqrt(v); }
+
+// normalize_rotation(.., 'rot_matrix') (misc.py:327-344): rotation_6d_to_matrix GS with
+// F.normalize's eps 1e-12 (rotation_conversions.py:571-575).
+template <typename T>
+__device__ __forceinline__ void gram_schmidt6(T* v) {
+#pragma clang fp contract(off)
+    T n1 = tsqrt<T>((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+    n1 = n1 > (T)1e-12 ? n1 : (T)1e-12;
+    const T b0 = v[0] / n1, b1 = v[1] / n1, b2 = v[2] / n1;
+    const T d = (b0 * v[3] + b1 * v[4]) + b2 * v[5];
+    T c0 = v[3] - d * b0, c1 = v[4] - d * b1, c2 = v[5] - d * b2;
+    T n2 = tsqrt<T>((c0 * c0 + c1 * c1) + c2 * c2);
+    n2 = n2 > (T)1e-12 ? n2 : (T)1e-12;
+    v[0] = b0;
+    v[1] = b1;
+    v[2] = b2;
+    v[3] = c0 / n2;
+    v[4] = c1 / n2;
+    v[5] = c2 / n2;
+}
+
+// matrix_to_quaternion (rotation_conversions.py:102-161) of R = [b1 b2 b1xb2] (columns), input
+// already Gram-Schmidt'ed; returns wxyz.
+template <typename T>
+__device__ __forceinline__ void quat_from_gs(const T* v, T* qo) {
+#pragma clang fp contract(off)
+    // second GS pass as get_rot_matrix applies rotation_6d_to_matrix again (posenet_agent.py:554)
+    T g[6] = {v[0], v[1], v[2], v[3], v[4], v[5]};
+    gram_schmidt6<T>(g);
+    const T b3x = g[1] * g[5] - g[2] * g[4];
+    const T b3y = g[2] * g[3] - g[0] * g[5];
+    const T b3z = g[0] * g[4] - g[1] * g[3];
+    const T m00 = g[0], m01 = g[3], m02 = b3x;
+    const T m10 = g[1], m11 = g[4], m12 = b3y;
+    const T m20 = g[2], m21 = g[5], m22 = b3z;
+    const T one = (T)1;
+    T qa[4] = {((one + m00) + m11) + m22, ((one + m00) - m11) - m22, ((one - m00) + m11) - m22,
+               ((one - m00) - m11) + m22};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qa[i] = qa[i] > (T)0 ? tsqrt<T>(qa[i]) : (T)0;
+    int best = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+        if (qa[i] > qa[best]) best = i;
+    T c[4];
+    if (best == 0) {
+        c[0] = qa[0] * qa[0]; c[1] = m21 - m12; c[2] = m02 - m20; c[3] = m10 - m01;
+    } else if (best == 1) {
+        c[0] = m21 - m12; c[1] = qa[1] * qa[1]; c[2] = m10 + m01; c[3] = m02 + m20;
+    } else if (best == 2) {
+        c[0] = m02 - m20; c[1] = m10 + m01; c[2] = qa[2] * qa[2]; c[3] = m12 + m21;
+    } else {
+        c[0] = m10 - m01; c[1] = m20 + m02; c[2] = m21 + m12; c[3] = qa[3] * qa[3];
+    }
+    const T den = (T)2 * (qa[best] > (T)0.1 ? qa[best] : (T)0.1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qo[i] = c[i] / den;
+}
+
+// ============================================================================ hoist kernels
+__global__ __launch_bounds__(HT) void object_proj_kernel(gp_head_weights w, const float* __restrict__ feat,
+                                                         float* __restrict__ pobj) {
+    __shared__ float sf[1024];
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < 1024; i += HT) sf[i] = feat[(size_t)b * 1024 + i];
+    __syncthreads();
+    const int o = blockIdx.x * HT + threadIdx.x;  // 0..767
+    float acc = 0.f;
+    for (int c = 0; c < 1024; ++c) acc += w.h1pts_t[(size_t)c * 768 + o] * sf[c];
+    pobj[(size_t)b * 768 + o] = acc + w.h1_b[o];
+}
+
+extern "C" int gp_head_object_proj(const gp_head_weights* w, const float* pts_feat, int b, float* pobj,
+                                   hipStream_t stream) {
+    GP_REQUIRE(w && pts_feat && pobj && b >= 0, "head_object_proj: bad arguments");
+    if (!b) return GP_OK;
+    hipLaunchKernelGGL(object_proj_kernel, dim3(3, b), dim3(HT), 0, stream, *w, pts_feat, pobj);
+    return gp_check_launch("object_proj_kernel");
+}
+
+__global__ __launch_bounds__(HT) void time_proj_kernel(gp_head_weights w, const float* __restrict__ tv,
+                                                       float* __restrict__ tproj) {
+    __shared__ float emb[128];
+    __shared__ float tf[128];
+    const int k = blockIdx.x;
+    const float t = tv[k];
+    const int i = threadIdx.x;
+    if (i < 64) {  // x_proj = x[:, None] * W[None, :] * 2 * np.pi (scorenet.py:87)
+        const float a = fmul(fmul(fmul(t, w.gfp_w[i]), 2.0f), 3.14159265358979323846f);
+        emb[i] = sinf(a);
+        emb[64 + i] = cosf(a);
+    }
+    __syncthreads();
+    if (i < 128) {
+        float acc = 0.f;
+        for (int c = 0; c < 128; ++c) acc += w.te_w_t[c * 128 + i] * emb[c];
+        tf[i] = fmaxf(acc + w.te_b[i], 0.f);
+    }
+    __syncthreads();
+    for (int o = i; o < 768; o += HT) {
+        float acc = 0.f;
+        for (int c = 0; c < 128; ++c) acc += w.h1t_t[c * 768 + o] * tf[c];
+        tproj[(size_t)k * 768 + o] = acc;
+    }
+}
+
+extern "C" int gp_head_time_proj(const gp_head_weights* w, const float* t, int nt, float* tproj,
+                                 hipStream_t stream) {
+    GP_REQUIRE(w && t && tproj && nt >= 0, "head_time_proj: bad arguments");
+    if (!nt) return GP_OK;
+    hipLaunchKernelGGL(time_proj_kernel, dim3(nt), dim3(HT), 0, stream, *w, t, tproj);
+    return gp_check_launch("time_proj_kernel");
+}
+
+// ============================================================================ score / energy eval
+template <int MODE>  // 0: score f/(sigma+1e-7), 1: energy (IP, decoupled)
+__global__ __launch_bounds__(HT) void head_eval_kernel(gp_head_weights w, const float* __restrict__ pobj,
+                                                       const float* __restrict__ tproj, float sigma,
+                                                       const float* __restrict__ x, int rows, int kper,
+                                                       float* __restrict__ out) {
+    __shared__ HeadSmem sm;
+    __shared__ int obj[16];
+    const int r0 = blockIdx.x * 16;
+    for (int i = threadIdx.x; i < 256; i += HT) {
+        const int c = i >> 4, j = i & 15;
+        const int r = r0 + c;
+        sm.xin[i] = (r < rows && j < 9) ? x[(size_t)r * 9 + j] : 0.f;
+    }
+    if (threadIdx.x < 16) {
+        const int r = r0 + threadIdx.x;
+        obj[threadIdx.x] = (r < rows ? r : rows - 1) / kper;
+    }
+    __syncthreads();
+    head_trunk(w, pobj, tproj, obj, sm);
+    if (MODE == 0) {
+        if (threadIdx.x < 144) {
+            const int c = threadIdx.x / 9, o = threadIdx.x - c * 9;
+            if (r0 + c < rows) out[(size_t)(r0 + c) * 9 + o] = fdiv(sm.f[c][o], fadd(sigma, 1e-7f));
+        }
+    } else {
+        if (threadIdx.x < 32) {
+            const int c = threadIdx.x >> 1, part = threadIdx.x & 1;
+            if (r0 + c < rows) {
+                const int lo = part ? 6 : 0, hi = part ? 9 : 6;
+                float e = 0.f;
+                for (int o = lo; o < hi; ++o) e += sm.xin[c * 16 + o] * fdiv(sm.f[c][o], sigma);
+                out[(size_t)(r0 + c) * 2 + part] = e;
+            }
+        }
+    }
+}
+
+extern "C" int gp_score_eval(const gp_head_weights* w, const float* pobj, const float* tproj_row, float sigma,
+                             const float* x, int rows, int k, float* score, hipStream_t stream) {
+    GP_REQUIRE(w && pobj && tproj_row && x && score && rows >= 0 && k >= 1, "score_eval: bad arguments");
+    if (!rows) return GP_OK;
+    hipLaunchKernelGGL(head_eval_kernel<0>, dim3((rows + 15) / 16), dim3(HT), 0, stream, *w, pobj, tproj_row,
+                       sigma, x, rows, k, score);
+    return gp_check_launch("head_eval_kernel<score>");
+}
+
+extern "C" int gp_energy_eval(const gp_head_weights* w, const float* pobj, const float* tproj_row, float sigma,
+                              const float* pose, int rows, int k, float* energy, hipStream_t stream) {
+    GP_REQUIRE(w && pobj && tproj_row && pose && energy && rows >= 0 && k >= 1, "energy_eval: bad arguments");
+    if (!rows) return GP_OK;
+    hipLaunchKernelGGL(head_eval_kernel<1>, dim3((rows + 15) / 16), dim3(HT), 0, stream, *w, pobj, tproj_row,
+                       sigma, pose, rows, k, energy);
+    return gp_check_launch("head_eval_kernel<energy>");
+}
+
+// ============================================================================ PC sampler
+struct PCStep {       // one row of step_tab: {t, sigma, g, dt, sqrt_dt}
+    float t, sigma, g, dt, sqrt_dt;
+};
+
+struct PCArgs {
+    gp_head_weights w;
+    const float* pobj;
+    const float* tproj;   // (T, 768)
+    float* x;             // (R, 9) state
+    float* s;             // (R, 9) score of the previous step
+    float* part;          // (2, ntiles) per-tile sums of row score norms
+    const float* z1;      // (T, R, 9) or null -> Philox
+    const float* z2;
+    uint64_t seed;
+    const float* center;  // (B, 3)
+    float* res;           // (R, 9)
+    float* q;             // (R, 7)
+    float* xs;            // (R, T, 9) or null
+    int rows, kper, steps, ntiles;
+    float ls_coef;        // snr * sqrt(pose_dim)
+};
+
+__device__ __forceinline__ float noise_at(const float* z, uint64_t seed, int stream, int step, int rows, int r,
+                                          int j) {
+    if (z) return z[((size_t)step * rows + r) * 9 + j];
+    const f32x4 v = philox_normal4(seed, (uint32_t)(stream + 2 * step), (uint32_t)r, (uint32_t)(j >> 2));
+    const int c = j & 3;
+    return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+}
+
+// Launch i in [0, steps]: finish step i-1 (if i > 0), then score at step i (if i < steps).
+__global__ __launch_bounds__(HT) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
+    __shared__ HeadSmem sm;
+    __shared__ int obj[16];
+    __shared__ float s_gn;
+    const int tid = threadIdx.x;
+    const int tile = blockIdx.x;
+    const int r0 = tile * 16;
+    if (tid < 16) {
+        const int r = r0 + tid;
+        obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
+    }
+    if (i == 0) {
+        for (int e = tid; e < 256; e += HT) {
+            const int c = e >> 4, j = e & 15;
+            const int r = r0 + c;
+            sm.xin[e] = (r < a.rows && j < 9) ? a.x[(size_t)r * 9 + j] : 0.f;
+        }
+    } else {
+        // ---- grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143), fixed order
+        const float* part = a.part + (size_t)((i - 1) & 1) * a.ntiles;
+        float acc = 0.f;
+        for (int t = tid; t < a.ntiles; t += HT) acc += part[t];
+        sm.scratch[tid] = acc;
+        __syncthreads();
+        if (tid < 64) {
+            float v = (sm.scratch[tid] + sm.scratch[tid + 64]) + (sm.scratch[tid + 128] + sm.scratch[tid + 192]);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+            if (tid == 0) s_gn = v / (float)a.rows;
+        }
+        __syncthreads();
+        if (tid < 16) {
+#pragma clang fp contract(off)
+            const int r = r0 + tid;
+            float xv[9];
+            if (r < a.rows) {
+                const float gn = s_gn;
+                const float ratio = a.ls_coef / gn;
+                const float ls = 2.0f * (ratio * ratio);
+                const float sq2ls = sqrtf(2.0f * ls);
+                const float* sp = a.s + (size_t)r * 9;
+                float sv[9];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) {
+                    sv[j] = sp[j];
+                    const float z = noise_at(a.z1, a.seed, 0, i - 1, a.rows, r, j);
+                    xv[j] = (a.x[(size_t)r * 9 + j] + ls * sv[j]) + sq2ls * z;
+                }
+                // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
+                const float na = sqrtf((xv[0] * xv[0] + xv[1] * xv[1]) + xv[2] * xv[2]);
+                const float nb = sqrtf((xv[3] * xv[3] + xv[4] * xv[4]) + xv[5] * xv[5]);
+                xv[0] /= na; xv[1] /= na; xv[2] /= na;
+                xv[3] /= nb; xv[4] /= nb; xv[5] /= nb;
+                // reverse-SDE Euler-Maruyama predictor (samplers.py:163-166; sign as in the reference)
+                const float g2 = prev.g * prev.g;
+                const float gs = prev.g * prev.sqrt_dt;
+                float mean[9];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) {
+                    const float drift = 0.0f - g2 * sv[j];
+                    mean[j] = xv[j] + drift * prev.dt;
+                    const float z = noise_at(a.z2, a.seed, 1, i - 1, a.rows, r, j);
+                    xv[j] = mean[j] + gs * z;
+                }
+                gram_schmidt6<float>(xv);
+                const float* cen = a.center + (size_t)obj[tid] * 3;
+                if (a.xs) {
+                    float* o = a.xs + ((size_t)r * a.steps + (i - 1)) * 9;
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) o[j] = xv[j];
+                    o[6] = xv[6] + cen[0];
+                    o[7] = xv[7] + cen[1];
+                    o[8] = xv[8] + cen[2];
+                }
+                if (i == a.steps) {  // res = mean_x of the last step (+centre, GS), samplers.py:174-177
+                    mean[6] += cen[0];
+                    mean[7] += cen[1];
+                    mean[8] += cen[2];
+                    gram_schmidt6<float>(mean);
+                    float qq[4];
+                    quat_from_gs<float>(mean, qq);
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) a.res[(size_t)r * 9 + j] = mean[j];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) a.q[(size_t)r * 7 + j] = qq[j];
+                    a.q[(size_t)r * 7 + 4] = mean[6];
+                    a.q[(size_t)r * 7 + 5] = mean[7];
+                    a.q[(size_t)r * 7 + 6] = mean[8];
+                }
+#pragma unroll
+                for (int j = 0; j < 9; ++j) a.x[(size_t)r * 9 + j] = xv[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 9; ++j) xv[j] = 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) sm.xin[tid * 16 + j] = j < 9 ? xv[j] : 0.f;
+        }
+    }
+    if (i == a.steps) return;  // finalize launch: no score evaluation
+    __syncthreads();
+    head_trunk(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm);
+    // ---- s = f / (sigma + 1e-7); tile partial of sum_r ||s_r||
+    if (tid < 16) {
+        const int r = r0 + tid;
+        float nrm = 0.f;
+        if (r < a.rows) {
+            const float den = fadd(cur.sigma, 1e-7f);
+            float ss = 0.f;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                const float v = fdiv(sm.f[tid][j], den);
+                a.s[(size_t)r * 9 + j] = v;
+                ss = fadd(ss, fmul(v, v));
+            }
+            nrm = sqrtf(ss);
+        }
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) nrm += __shfl_xor(nrm, off, 16);
+        if (tid == 0) a.part[(size_t)(i & 1) * a.ntiles + tile] = nrm;
+    }
+}
+
+extern "C" size_t gp_pc_workspace_size(int rows) {
+    const size_t ntiles = ((size_t)rows + 15) / 16;
+    return sizeof(float) * ((size_t)rows * 9 + 2 * ntiles) + 256;
+}
+
+extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const float* tproj, const float* step_tab,
+                            int steps, float* x, int rows, int k, const float* pts_center, const float* z1,
+                            const float* z2, uint64_t seed, float snr, float* res, float* q, float* xs,
+                            void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    GP_REQUIRE(w && pobj && tproj && step_tab && x && pts_center && res && q && workspace,
+               "pc_sample: null pointer");
+    GP_REQUIRE(steps >= 2 && rows >= 1 && k >= 1, "pc_sample: need steps>=2, rows>=1, k>=1");
+    GP_REQUIRE((z1 == nullptr) == (z2 == nullptr), "pc_sample: z1/z2 must both be given or both null");
+    GP_REQUIRE(workspace_bytes >= gp_pc_workspace_size(rows), "pc_sample: workspace too small");
+    PCArgs a;
+    a.w = *w;
+    a.pobj = pobj;
+    a.tproj = tproj;
+    a.x = x;
+    a.s = static_cast<float*>(workspace);
+    a.part = a.s + (size_t)rows * 9;
+    a.z1 = z1;
+    a.z2 = z2;
+    a.seed = seed;
+    a.center = pts_center;
+    a.res = res;
+    a.q = q;
+    a.xs = xs;
+    a.rows = rows;
+    a.kper = k;
+    a.steps = steps;
+    a.ntiles = (rows + 15) / 16;
+    a.ls_coef = snr * 3.0f;  // snr * sqrt(pose_dim=9) in fp32 (0.48 rounds identically)
+    const dim3 grid(a.ntiles);
+    for (int i = 0; i <= steps; ++i) {
+        PCStep cur = {}, prev = {};
+        if (i < steps) cur = PCStep{step_tab[5 * i], step_tab[5 * i + 1], step_tab[5 * i + 2], step_tab[5 * i + 3],
+                                    step_tab[5 * i + 4]};
+        if (i > 0) prev = PCStep{step_tab[5 * (i - 1)], step_tab[5 * (i - 1) + 1], step_tab[5 * (i - 1) + 2],
+                                 step_tab[5 * (i - 1) + 3], step_tab[5 * (i - 1) + 4]};
+        hipLaunchKernelGGL(pc_step_kernel, grid, dim3(HT), 0, stream, a, i, cur, prev);
+    }
+    return gp_check_launch("pc_step_kernel");
+}
+
+// ============================================================================ ODE epilogue (fp64)
+__global__ void pose_epilogue_f64_kernel(double* pose, int rows, int kper, const float* center, double* q) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    double v[9];
+    for (int j = 0; j < 9; ++j) v[j] = pose[(size_t)r * 9 + j];
+    gram_schmidt6<double>(v);
+    const float* c = center + (size_t)(r / kper) * 3;
+    v[6] += (double)c[0];
+    v[7] += (double)c[1];
+    v[8] += (double)c[2];
+    double qq[4];
+    quat_from_gs<double>(v, qq);
+    for (int j = 0; j < 9; ++j) pose[(size_t)r * 9 + j] = v[j];
+    for (int j = 0; j < 4; ++j) q[(size_t)r * 7 + j] = qq[j];
+    for (int j = 0; j < 3; ++j) q[(size_t)r * 7 + 4 + j] = v[6 + j];
+}
+
+extern "C" int gp_pose_epilogue_f64(double* pose, int rows, int k, const float* pts_center, double* q,
+                                    hipStream_t stream) {
+    GP_REQUIRE(pose && pts_center && q && rows >= 0 && k >= 1, "pose_epilogue_f64: bad arguments");
+    if (!rows) return GP_OK;
+    hipLaunchKernelGGL(pose_epilogue_f64_kernel, dim3((rows + 255) / 256), dim3(256), 0, stream, pose, rows, k,
+                       pts_center, q);
+    return gp_check_launch("pose_epilogue_f64_kernel");
+}
+
+// ============================================================================ ScaleNet
+// ScaleNet.forward (scalenet.py:33-49) with encode_axes (genpose_utils.py:8-18). 0.88 MFLOP per
+// object: one workgroup per object, VALU dot products.
+__global__ __launch_bounds__(HT) void scale_kernel(gp_scale_weights w, const float* __restrict__ axes,
+                                                   const float* __restrict__ feat, float* __restrict__ len) {
+    __shared__ float emb[180];
+    __shared__ float h1[256];
+    __shared__ float tot[1280];
+    __shared__ float u[256];
+    const int b = blockIdx.x, i = threadIdx.x;
+    if (i < 90) {  // embedding[(fn, a, e)] = fn(2^e * axes[a]), a<9, e<10
+        const int a = i / 10, e = i - a * 10;
+        const float v = fmul((float)(1 << e), axes[(size_t)b * 9 + a]);
+        emb[i] = sinf(v);
+        emb[90 + i] = cosf(v);
+    }
+    for (int c = i; c < 1024; c += HT) tot[c] = feat[(size_t)b * 1024 + c];
+    __syncthreads();
+    {
+        float acc = 0.f;
+        for (int c = 0; c < 180; ++c) acc += w.ae0_w[i * 180 + c] * emb[c];
+        h1[i] = fmaxf(acc + w.ae0_b[i], 0.f);
+    }
+    __syncthreads();
+    {
+        float acc = 0.f;
+        for (int c = 0; c < 256; ++c) acc += w.ae2_w[i * 256 + c] * h1[c];
+        tot[1024 + i] = fmaxf(acc + w.ae2_b[i], 0.f);
+    }
+    __syncthreads();
+    {
+        float acc = 0.f;
+        for (int c = 0; c < 1280; ++c) acc += w.ft0_w[(size_t)i * 1280 + c] * tot[c];
+        u[i] = fmaxf(acc + w.ft0_b[i], 0.f);
+    }
+    __syncthreads();
+    if (i < 3) {
+        float acc = 0.f;
+        for (int c = 0; c < 256; ++c) acc += w.ft2_w[i * 256 + c] * u[c];
+        len[(size_t)b * 3 + i] = acc + w.ft2_b[i];
+    }
+}
+
+extern "C" int gp_scale_forward(const gp_scale_weights* w, const float* axes, const float* pts_feat, int b,
+                                float* length, hipStream_t stream) {
+    GP_REQUIRE(w && axes && pts_feat && length && b >= 0, "scale_forward: bad arguments");
+    if (!b) return GP_OK;
+    hipLaunchKernelGGL(scale_kernel, dim3(b), dim3(HT), 0, stream, *w, axes, pts_feat, length);
+    return gp_check_launch("scale_kernel");
+}

@@ -1,0 +1,189 @@
+"""Device-resident models: packed weights in HBM + thin calls into libgenpose_hip.so.
+
+PyTorch is used only for device memory, the current HIP stream and host<->device copies; every
+computation on the path is a call into the HIP library.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _lib, arch, pack, weights
+from ._lib import check
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device_tensor(t: torch.Tensor, name: str, dtype=torch.float32) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must live on a HIP device (got {t.device}); the path has no CPU fallback")
+    return t.to(dtype).contiguous()
+
+
+class _Uploaded:
+    def __init__(self, arrays: Dict[str, np.ndarray], device: torch.device):
+        self.t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in arrays.items()}
+
+    def ptr(self, k: str) -> int:
+        return self.t[k].data_ptr()
+
+
+class EncoderModel:
+    """Pointnet2ClsMSG(0), Light cfg, on device (gp_encoder_forward)."""
+
+    def __init__(self, sd: weights.StateDict, device: torch.device):
+        self.lib = _lib.load()
+        self.device = device
+        buf, offs = pack.pack_encoder(sd)
+        self.wbuf = torch.from_numpy(buf).to(device)
+        self.offsets = np.ascontiguousarray(offs.reshape(-1), np.int64)
+        self._ws: Optional[torch.Tensor] = None
+
+    def workspace(self, b: int, n: int) -> torch.Tensor:
+        need = int(self.lib.gp_encoder_workspace_size(b, n))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def forward(self, pts: torch.Tensor, return_workspace: bool = False):
+        pts = require_device_tensor(pts, "pts")
+        B, N, C = pts.shape
+        if C < 3:
+            raise ValueError("pts must be (B, N, 3+)")
+        if C != 3:
+            pts = pts[..., :3].contiguous()
+        feat = torch.empty((B, arch.PTS_FEAT_DIM), dtype=torch.float32, device=self.device)
+        ws = self.workspace(B, N)
+        check(self.lib.gp_encoder_forward(
+            ctypes.c_void_p(self.wbuf.data_ptr()), self.offsets.ctypes.data_as(_lib.c_int64_p),
+            ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+            ctypes.c_void_p(feat.data_ptr()), ctypes.c_void_p(stream_handle(self.device))), "encoder_forward")
+        return (feat, ws) if return_workspace else feat
+
+    def levels(self, b: int, n: int, ws: torch.Tensor):
+        """Views of the per-level intermediates in the workspace (for parity tests)."""
+        off = np.zeros(25, np.int64)
+        check(self.lib.gp_encoder_workspace_layout(b, n, off.ctypes.data_as(_lib.c_int64_p)))
+        out = []
+        couts = [arch.level_out_channels(lv) for lv in range(5)]
+        for lv in range(5):
+            m = arch.NPOINTS[lv] if lv < 4 else 1
+            d = {}
+            if lv < 4:
+                d["fps_idx"] = ws[off[lv * 5]:].view(torch.int32)[: b * m].view(b, m)
+                d["new_xyz"] = ws[off[lv * 5 + 1]:].view(torch.float32)[: b * m * 3].view(b, m, 3)
+                d["ball_idx"] = [ws[off[lv * 5 + 2 + i]:].view(torch.int32)[: b * m * ns].view(b, m, ns)
+                                 for i, ns in enumerate(arch.NSAMPLES[lv])]
+            if lv < 4:
+                d["features"] = ws[off[lv * 5 + 4]:].view(torch.float32)[: b * m * couts[lv]].view(b, m, couts[lv])
+            out.append(d)
+        return out
+
+
+class HeadModel:
+    """PoseScoreNet / PoseEnergyNet heads (Rx_Ry_and_T) on device."""
+
+    def __init__(self, sd: weights.StateDict, device: torch.device):
+        self.lib = _lib.load()
+        self.device = device
+        self.up = _Uploaded(pack.pack_heads(sd), device)
+        self.w = _lib.HeadWeights(**{k: self.up.ptr(k) for k in pack.HEAD_FIELDS})
+        self._pc_ws: Optional[torch.Tensor] = None
+
+    def _s(self):
+        return ctypes.c_void_p(stream_handle(self.device))
+
+    def object_proj(self, feat: torch.Tensor) -> torch.Tensor:
+        feat = require_device_tensor(feat, "pts_feat")
+        B = feat.shape[0]
+        pobj = torch.empty((B, 3 * arch.HEAD_HID), dtype=torch.float32, device=self.device)
+        check(self.lib.gp_head_object_proj(ctypes.byref(self.w), ctypes.c_void_p(feat.data_ptr()), B,
+                                           ctypes.c_void_p(pobj.data_ptr()), self._s()), "head_object_proj")
+        return pobj
+
+    def time_proj(self, t: torch.Tensor) -> torch.Tensor:
+        t = require_device_tensor(t.reshape(-1), "t")
+        out = torch.empty((t.numel(), 3 * arch.HEAD_HID), dtype=torch.float32, device=self.device)
+        check(self.lib.gp_head_time_proj(ctypes.byref(self.w), ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                         ctypes.c_void_p(out.data_ptr()), self._s()), "head_time_proj")
+        return out
+
+    def score(self, pobj, tproj_row, sigma: float, x: torch.Tensor, k: int, out=None) -> torch.Tensor:
+        x = require_device_tensor(x, "x")
+        R = x.shape[0]
+        out = torch.empty((R, arch.POSE_DIM), dtype=torch.float32, device=self.device) if out is None else out
+        check(self.lib.gp_score_eval(ctypes.byref(self.w), ctypes.c_void_p(pobj.data_ptr()),
+                                     ctypes.c_void_p(tproj_row.data_ptr()), ctypes.c_float(sigma),
+                                     ctypes.c_void_p(x.data_ptr()), R, k, ctypes.c_void_p(out.data_ptr()),
+                                     self._s()), "score_eval")
+        return out
+
+    def energy(self, pobj, tproj_row, sigma: float, pose: torch.Tensor, k: int) -> torch.Tensor:
+        pose = require_device_tensor(pose, "pose")
+        R = pose.shape[0]
+        out = torch.empty((R, 2), dtype=torch.float32, device=self.device)
+        check(self.lib.gp_energy_eval(ctypes.byref(self.w), ctypes.c_void_p(pobj.data_ptr()),
+                                      ctypes.c_void_p(tproj_row.data_ptr()), ctypes.c_float(sigma),
+                                      ctypes.c_void_p(pose.data_ptr()), R, k, ctypes.c_void_p(out.data_ptr()),
+                                      self._s()), "energy_eval")
+        return out
+
+    def pc_sample(self, pobj, tproj, step_tab: np.ndarray, x: torch.Tensor, k: int, pts_center: torch.Tensor,
+                  z1=None, z2=None, seed: int = 0, snr: float = arch.SNR, want_xs: bool = False):
+        R = x.shape[0]
+        T = step_tab.shape[0]
+        need = int(self.lib.gp_pc_workspace_size(R))
+        if self._pc_ws is None or self._pc_ws.numel() < need:
+            self._pc_ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        res = torch.empty((R, 9), dtype=torch.float32, device=self.device)
+        q = torch.empty((R, 7), dtype=torch.float32, device=self.device)
+        xs = torch.empty((R, T, 9), dtype=torch.float32, device=self.device) if want_xs else None
+        tab = np.ascontiguousarray(step_tab, np.float32)
+        check(self.lib.gp_pc_sample(
+            ctypes.byref(self.w), ctypes.c_void_p(pobj.data_ptr()), ctypes.c_void_p(tproj.data_ptr()),
+            tab.ctypes.data_as(ctypes.c_void_p), T, ctypes.c_void_p(x.data_ptr()), R, k,
+            ctypes.c_void_p(pts_center.data_ptr()), ctypes.c_void_p(_ptr(z1)), ctypes.c_void_p(_ptr(z2)),
+            ctypes.c_uint64(seed), ctypes.c_float(snr), ctypes.c_void_p(res.data_ptr()),
+            ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(_ptr(xs)), ctypes.c_void_p(self._pc_ws.data_ptr()),
+            self._pc_ws.numel(), self._s()), "pc_sample")
+        return res, q, xs
+
+
+class ScaleModel:
+    def __init__(self, sd: weights.StateDict, device: torch.device):
+        self.lib = _lib.load()
+        self.device = device
+        self.up = _Uploaded(pack.pack_scale(sd), device)
+        self.w = _lib.ScaleWeights(**{k: self.up.ptr(k) for k in pack.SCALE_FIELDS})
+
+    def forward(self, axes: torch.Tensor, pts_feat: torch.Tensor) -> torch.Tensor:
+        axes = require_device_tensor(axes, "axes")
+        pts_feat = require_device_tensor(pts_feat, "pts_feat")
+        B = axes.shape[0]
+        out = torch.empty((B, 3), dtype=torch.float32, device=self.device)
+        check(self.lib.gp_scale_forward(ctypes.byref(self.w), ctypes.c_void_p(axes.data_ptr()),
+                                        ctypes.c_void_p(pts_feat.data_ptr()), B, ctypes.c_void_p(out.data_ptr()),
+                                        ctypes.c_void_p(stream_handle(self.device))), "scale_forward")
+        return out
+
+
+def pose_epilogue_f64(pose: torch.Tensor, k: int, pts_center: torch.Tensor):
+    lib = _lib.load()
+    pose = pose.contiguous()
+    q = torch.empty((pose.shape[0], 7), dtype=torch.float64, device=pose.device)
+    check(lib.gp_pose_epilogue_f64(ctypes.c_void_p(pose.data_ptr()), pose.shape[0], k,
+                                   ctypes.c_void_p(require_device_tensor(pts_center, "pts_center").data_ptr()),
+                                   ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(stream_handle(pose.device))),
+          "pose_epilogue_f64")
+    return pose, q

@@ -1,0 +1,56 @@
+"""Harness counterpart of runners/evaluation_single.py on synthetic batches.
+
+Stages, in the reference's order, with in-memory hand-off instead of the pickles between them
+(evaluation_single.py:120,157,219,288):
+  inference_score  (:78-120)  PoseNet(score).pred_func -> pred_pose (B,K,9), pts_feat
+  inference_energy (:123-157) PoseNet(energy).get_energy(T=1e-5) -> (B,K,2)
+  aggregate_pose   (:160-219) sort by energy, top retain_ratio*K, quaternion average (+DBSCAN)
+  inference_scale  (:222-288) PoseNet(scale).pred_scale_func(axes=aggregated R, pts_feat)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import aggregate
+from .agent import PoseNet
+from .config import GenPoseConfig
+
+
+@dataclass
+class StageOutputs:
+    pred_pose: torch.Tensor
+    pts_feat: torch.Tensor
+    energy: Optional[torch.Tensor] = None
+    aggregated: Optional[torch.Tensor] = None
+    length: Optional[torch.Tensor] = None
+
+
+class EvaluationPipeline:
+    def __init__(self, cfg: GenPoseConfig, with_energy: bool = True, with_scale: bool = False):
+        self.cfg = cfg
+        self.score_agent = PoseNet(cfg.copy(agent_type="score")).eval()
+        self.energy_agent = PoseNet(cfg.copy(agent_type="energy")).eval() if with_energy else None
+        self.scale_agent = PoseNet(cfg.copy(agent_type="scale")).eval() if with_scale else None
+
+    def run(self, batch: Dict[str, torch.Tensor]) -> StageOutputs:
+        cfg = self.cfg
+        data = dict(batch)
+        pred_pose, _ = self.score_agent.pred_func(data=data, repeat_num=cfg.eval_repeat_num, T0=cfg.T0,
+                                                  return_average_res=False, return_process=False)
+        out = StageOutputs(pred_pose=pred_pose, pts_feat=data["pts_feat"])
+        if self.energy_agent is not None:
+            edata = {"pts": batch["pts"], "pts_center": batch["pts_center"]}
+            out.energy = self.energy_agent.get_energy(data=edata, pose_samples=pred_pose, T=1e-5, mode="test",
+                                                      extract_feature=True)
+        energy = out.energy if out.energy is not None else torch.ones(*pred_pose.shape[:2], 2,
+                                                                      device=pred_pose.device)
+        out.aggregated = aggregate.aggregate_pose(pred_pose, energy, cfg.retain_ratio, cfg.clustering,
+                                                  cfg.clustering_eps, cfg.clustering_minpts)
+        if self.scale_agent is not None:
+            sdata = {"pts_feat": out.pts_feat, "rgb_feat": None,
+                     "axes": out.aggregated[:, :3, :3].contiguous()}
+            _, out.length = self.scale_agent.pred_scale_func(sdata)
+        return out

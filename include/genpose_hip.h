@@ -1,0 +1,151 @@
+/*
+ * genpose_hip.h -- C ABI of libgenpose_hip.so, the MI355X (gfx950) implementation of the
+ * GenPose++ pose-candidate path.
+ *
+ * Conventions (replacing the reference's pybind module `pointnet2_cuda`,
+ * networks/pts_encoder/pointnet2_utils/pointnet2/src/pointnet2_api.cpp:10-24):
+ *   - every pointer argument is caller-owned DEVICE memory unless marked "host";
+ *     the library never allocates inside a call (workspaces are sized by *_workspace_size);
+ *   - every call is enqueued on `stream` and returns immediately (no device sync);
+ *   - every call returns 0 (GP_OK) or a negative status; gp_last_error() (thread-local)
+ *     describes the failure. Nothing calls exit() (the reference launchers do, e.g.
+ *     src/ball_query_gpu.cu:61-65);
+ *   - calls are stateless and re-entrant across distinct streams.
+ * Layouts are row-major; "packed" weights are produced by genpose2_amd/pack.py.
+ */
+#ifndef GENPOSE_HIP_H
+#define GENPOSE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { GP_OK = 0, GP_ERR_INVALID = -1, GP_ERR_LAUNCH = -2, GP_ERR_UNSUPPORTED = -3 };
+
+/* Thread-local description of the last failure (empty string if none). */
+const char *gp_last_error(void);
+/* ABI version of this header. */
+int gp_abi_version(void);
+#define GP_ABI_VERSION 1
+
+/* ===================================================================== operator level
+ * Drop-in forward ops of `pointnet2_cuda` (same argument meaning and layouts). */
+
+/* furthest_point_sampling_wrapper(b, n, m, points, temp, idx)  src/sampling.cpp / sampling_gpu.cu:94-253
+ * xyz (b,n,3) fp32, idx (b,m) int32. `temp` (b,n) is accepted for signature parity and may be
+ * NULL: the kernel keeps the running min-distance on chip. Tie rule identical to the reference
+ * (strict > within a thread, lower reduction slot on ties, block size min(2^floor(log2 n),1024)). */
+int gp_furthest_point_sampling(int b, int n, int m, const float *xyz, float *temp, int *idx,
+                               hipStream_t stream);
+
+/* gather_points_wrapper(b, c, n, npoints, points, idx, out)  src/sampling_gpu.cu:8-44
+ * points (b,c,n), idx (b,npoints) int32 -> out (b,c,npoints). */
+int gp_gather_points(int b, int c, int n, int npoints, const float *points, const int *idx,
+                     float *out, hipStream_t stream);
+
+/* ball_query_wrapper(b, n, m, radius, nsample, new_xyz, xyz, idx)  src/ball_query_gpu.cu:9-66
+ * new_xyz (b,m,3), xyz (b,n,3) -> idx (b,m,nsample) int32: first nsample points with
+ * d^2 < radius^2 in index order, padded with the first hit, 0 when there is no hit. */
+int gp_ball_query(int b, int n, int m, float radius, int nsample, const float *new_xyz,
+                  const float *xyz, int *idx, hipStream_t stream);
+
+/* group_points_wrapper(b, c, n, npoints, nsample, points, idx, out)  src/group_points_gpu.cu:47-85
+ * points (b,c,n), idx (b,npoints,nsample) -> out (b,c,npoints,nsample). */
+int gp_group_points(int b, int c, int n, int npoints, int nsample, const float *points,
+                    const int *idx, float *out, hipStream_t stream);
+
+/* ===================================================================== fused encoder
+ * Pointnet2ClsMSG(0) with the Light config (networks/pts_encoder/pointnet2.py:211-252).
+ * `wbuf` holds all packed, BN-folded layers; `layer_off` (HOST, int64 [5][2][3][2]) gives the
+ * float offsets of (weights, bias) of layer i of branch b of level l in `wbuf` (-1 = absent). */
+size_t gp_encoder_workspace_size(int b, int n);
+/* HOST out: byte offsets in the workspace of, per level l<4: fps idx (b,M_l) int32,
+ * new_xyz (b,M_l,3) fp32, ball idx branch0/1 (b,M_l,ns) int32; and per level l<5 the level
+ * features (b,M_l,C_l) point-major fp32.  offsets[l*5 + {0..4}] = {fps, new_xyz, ball0, ball1, feat}. */
+int gp_encoder_workspace_layout(int b, int n, int64_t *offsets);
+/* pts (b,n,3) un-centred points -> feat (b,1024). */
+int gp_encoder_forward(const float *wbuf, const int64_t *layer_off, const float *pts, int b, int n,
+                       void *workspace, size_t workspace_bytes, float *feat, hipStream_t stream);
+
+/* ===================================================================== score / energy heads
+ * PoseScoreNet / PoseEnergyNet with Rx_Ry_and_T heads (scorenet.py:109-275, energynet.py:32-208),
+ * split into per-object (pts), per-step (t) and per-candidate (pose) column blocks of the first
+ * head layer. All "packed" tensors come from genpose2_amd/pack.py. */
+typedef struct {
+    const float *pe0_w; /* pose_encoder.0: packed 256x16 */
+    const float *pe0_b; /* 256 */
+    const float *pe2_w; /* pose_encoder.2: packed 256x256 */
+    const float *pe2_b; /* 256 */
+    const float *h1p_w; /* head layer 1, pose columns: packed 768x256 */
+    const float *h2_w;  /* head layer 2: [3 heads][3][256] */
+    const float *h2_b;  /* [9] */
+    const float *h1pts_t; /* head layer 1, pts columns, transposed (1024, 768) */
+    const float *h1_b;    /* head layer 1 bias (768) */
+    const float *gfp_w;   /* t_encoder.0.W (64) */
+    const float *te_w_t;  /* t_encoder.1.weight transposed (128,128) */
+    const float *te_b;    /* (128) */
+    const float *h1t_t;   /* head layer 1, t columns, transposed (128, 768) */
+} gp_head_weights;
+
+/* Per-object projection P[b] = W1_pts . pts_feat[b] + b1 -> pobj (b,768). */
+int gp_head_object_proj(const gp_head_weights *w, const float *pts_feat, int b, float *pobj,
+                        hipStream_t stream);
+/* Per-time projection tproj[k] = W1_t . relu(W_t . GFP(t_k) + b_t) for t (nt) -> (nt,768). */
+int gp_head_time_proj(const gp_head_weights *w, const float *t, int nt, float *tproj,
+                      hipStream_t stream);
+
+/* Score evaluation s = heads(x, t) / (sigma + 1e-7) for R rows, rows r -> object r / k.
+ * `tproj_row` (768) and `sigma` are those of the single time value of this call. */
+int gp_score_eval(const gp_head_weights *w, const float *pobj, const float *tproj_row,
+                  float sigma, const float *x, int rows, int k, float *score, hipStream_t stream);
+
+/* Energy (IP / score / identical, decoupled rot-trans): pose rows (R,9) with translation
+ * already relative to pts_center -> energy (R,2). t is a single value with its tproj row. */
+int gp_energy_eval(const gp_head_weights *w, const float *pobj, const float *tproj_row,
+                   float sigma, const float *pose, int rows, int k, float *energy,
+                   hipStream_t stream);
+
+/* ===================================================================== PC sampler
+ * cond_pc_sampler (samplers.py:113-177) for R = b*k rows over T steps, fused per step:
+ * [finish step i-1: Langevin corrector with the batch-mean score norm, renormalise,
+ *  reverse-SDE Euler-Maruyama predictor, Gram-Schmidt] + [score at step i].
+ * step_tab (HOST, T x 5 fp32): {t, sigma, g, dt, sqrt_dt} exactly as the reference forms them.
+ * x (R,9) holds the initial state (prior sample or init_x) and is overwritten.
+ * noise: z1/z2 (T,R,9) injected draws, or both NULL to use device Philox4x32 seeded by `seed`.
+ * Outputs: res (R,9) = mean_x of the last step (+pts_center, GS), q (R,7) = [quat_wxyz, trans]
+ * (posenet_agent.py:554-556), xs (R,T,9) trajectory or NULL. */
+size_t gp_pc_workspace_size(int rows);
+int gp_pc_sample(const gp_head_weights *w, const float *pobj, const float *tproj,
+                 const float *step_tab, int steps, float *x, int rows, int k,
+                 const float *pts_center, const float *z1, const float *z2, uint64_t seed,
+                 float snr, float *res, float *q, float *xs, void *workspace,
+                 size_t workspace_bytes, hipStream_t stream);
+
+/* Quaternion / GS epilogue used by the ODE path: rows (R,9) fp64 -> in-place GS of [:6],
+ * + pts_center on [6:], and q (R,7) fp64. */
+int gp_pose_epilogue_f64(double *pose, int rows, int k, const float *pts_center, double *q,
+                         hipStream_t stream);
+
+/* ===================================================================== ScaleNet
+ * ScaleNet.forward (scalenet.py:33-49): axes (b,3,3), pts_feat (b,1024) -> length (b,3). */
+typedef struct {
+    const float *ae0_w; /* (256,180) */
+    const float *ae0_b;
+    const float *ae2_w; /* (256,256) */
+    const float *ae2_b;
+    const float *ft0_w; /* (256,1280) */
+    const float *ft0_b;
+    const float *ft2_w; /* (3,256) */
+    const float *ft2_b;
+} gp_scale_weights;
+int gp_scale_forward(const gp_scale_weights *w, const float *axes, const float *pts_feat, int b,
+                     float *length, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GENPOSE_HIP_H */

@@ -138,15 +138,18 @@ def encoder_forward(sd, pts: np.ndarray, return_levels: bool = False):
 
 # ============================================================ SDE helpers (sde.py:15-35)
 def ve_sigma(t):
-    """sigma_min * (sigma_max/sigma_min) ** t, in the dtype of ``t`` (sde.py:15-18)."""
+    """sigma_min * (sigma_max/sigma_min) ** t, in the dtype of ``t`` (sde.py:15-18). Evaluated
+    with torch's CPU pow, the function the reference calls (numpy's pow differs by 1 ulp)."""
+    import torch
     t = np.asarray(t)
     dt = t.dtype if t.dtype in (np.float32, np.float64) else np.float64
-    return (dt.type(arch.SIGMA_MIN) * np.power(dt.type(arch.SIGMA_MAX / arch.SIGMA_MIN), t)).astype(dt)
+    tt = torch.from_numpy(np.ascontiguousarray(t, dtype=dt))
+    return (arch.SIGMA_MIN * (arch.SIGMA_MAX / arch.SIGMA_MIN) ** tt).numpy().astype(dt)
 
 
 def ve_diffusion(t):
     """sigma(t) * sqrt(2 (ln sigma_max - ln sigma_min)) (sde.py:21-27)."""
-    s = ve_sigma(t)
+    s = np.asarray(ve_sigma(t))
     return (s * s.dtype.type(arch.DIFFUSION_SCALE)).astype(s.dtype)
 
 

@@ -1,0 +1,168 @@
+"""CPU-only tests of the host side: C-ABI exports, packing, SDE scalars, RK45 controller,
+DBSCAN restatement, aggregation, sharding (gloo, world_size 2). No HIP compute calls."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, golden
+
+
+def test_library_exports_every_declared_symbol():
+    hdr = open(os.path.join(REPO, "include", "genpose_hip.h")).read()
+    declared = set(re.findall(r"\b(gp_[a-z0-9_]+)\s*\(", hdr))
+    so = os.path.join(REPO, "genpose2_amd", "libgenpose_hip.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "genpose2_amd", "csrc")], check=True)
+    nm = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (gp_[a-z0-9_]+)$", nm, re.M))
+    assert declared and declared <= exported, declared - exported
+    from genpose2_amd import _lib
+    assert set(_lib.EXPORTED) == declared   # the ctypes binding covers exactly the header
+    lib = _lib.load()
+    assert lib.gp_abi_version() == 1
+    assert lib.gp_encoder_workspace_size(64, 1024) > 0 and lib.gp_pc_workspace_size(3200) >= 3200 * 36
+
+
+def test_invalid_arguments_return_status_not_exit():
+    from genpose2_amd import _lib
+    lib = _lib.load()
+    rc = lib.gp_ball_query(1, 10, 1, 0.1, 0, None, None, None, None)
+    assert rc == -1 and b"ball_query" in lib.gp_last_error()
+    with pytest.raises(_lib.GenPoseHipError):
+        _lib.check(lib.gp_furthest_point_sampling(1, 0, 1, None, None, None, None), "fps")
+
+
+def test_a_fragment_packing_layout():
+    from genpose2_amd import pack
+    rng = np.random.default_rng(0)
+    w = rng.normal(size=(40, 35)).astype(np.float32)
+    p = pack.pack_a_fragments(w)
+    assert p.size == 48 * 48
+    # lane l of (tile T, k-group g) holds W[16T + l%16][16g + 4(l//16) + j]
+    T, g, lane = 1, 2, 37
+    off = ((T * 3 + g) * 64 + lane) * 4
+    assert np.array_equal(p[off:off + 4], np.pad(w, ((0, 8), (0, 13)))[16 * T + lane % 16, 16 * g + 4 * (lane // 16):][:4])
+    np.testing.assert_array_equal(pack.unpack_a_fragments(p, 48, 48)[:40, :35], w)
+
+
+def test_encoder_packing_covers_every_layer(score_sd):
+    from genpose2_amd import arch, pack
+    buf, off = pack.pack_encoder(score_sd)
+    for lv, brs in enumerate(arch.sa_branches()):
+        for br in brs:
+            n = len(br.widths) - 1
+            assert (off[lv, br.branch, :n] >= 0).all() and (off[lv, br.branch, n:] == -1).all()
+            assert (off[lv, br.branch, :n] % 4 == 0).all()    # 16-byte aligned
+    assert off.max() < buf.size
+
+
+def test_pc_step_table_matches_reference_formula():
+    from genpose2_amd import sde
+    from oracle import oracle
+    tab = sde.pc_step_table(500)
+    ts = oracle.time_grid(500)
+    np.testing.assert_array_equal(tab[:, 0], ts)
+    np.testing.assert_array_equal(tab[:, 1], oracle.ve_sigma(ts))
+    np.testing.assert_array_equal(tab[:, 2], oracle.ve_diffusion(ts))
+    assert tab[0, 3] == np.float32(ts[0] - ts[1])
+    assert tab[0, 4] == np.sqrt(np.float32(ts[0] - ts[1]))
+
+
+@pytest.mark.parametrize("t_eval", [None, 15])
+def test_rk45_restatement_matches_scipy(t_eval):
+    from scipy.integrate import solve_ivp
+    from genpose2_amd.ode import rk45_solve
+    A = np.array([[-0.5, 2.0, 0.0], [-2.0, -0.5, 0.3], [0.0, -0.3, -0.1]])
+
+    def f_np(t, y):
+        return A @ y + np.sin(3 * t) * y ** 2 * 0.1
+
+    y0 = np.array([1.0, -0.5, 2.0])
+    te = None if t_eval is None else np.linspace(1.0, 1e-5, t_eval)
+    ref = solve_ivp(f_np, (1.0, 1e-5), y0, method="RK45", rtol=1e-5, atol=1e-5, t_eval=te)
+    ts, ys, nfev = rk45_solve(lambda t, y: torch.from_numpy(f_np(t, y.numpy())), 1.0, torch.from_numpy(y0), 1e-5,
+                              t_eval=te)
+    # same accept/reject sequence; the error estimate sum_i E_i K_i cancels catastrophically, so
+    # BLAS vs torch summation order moves step sizes at ~1e-9 relative
+    assert nfev == ref.nfev
+    np.testing.assert_allclose(ts, ref.t, rtol=1e-7, atol=1e-12)
+    np.testing.assert_allclose(ys.numpy().T, ref.y, rtol=1e-7, atol=1e-10)
+
+
+def test_dbscan_restatement_matches_sklearn():
+    from sklearn.cluster import DBSCAN
+    from genpose2_amd.aggregate import dbscan_labels
+    g = golden("pipeline")
+    rng = np.random.default_rng(1)
+    cases = [rng.normal(size=(20, 20)) * s for s in (0.01, 0.03, 0.1)]
+    for j in range(4):   # the clustered fixture's distance matrices
+        q = torch.from_numpy(g["cl_pose"][j, :20, :6])
+        from genpose2_amd.aggregate import matrix_to_quaternion, rot6_to_matrix
+        qq = matrix_to_quaternion(rot6_to_matrix(q))
+        cases.append((1 - (qq[None] * qq[:, None]).sum(-1) ** 2).numpy())
+    for X in cases:
+        for ms in (1, 3, 5):
+            ref = DBSCAN(eps=0.05, min_samples=ms).fit(X).labels_
+            np.testing.assert_array_equal(dbscan_labels(X, 0.05, ms), ref)
+
+
+def test_aggregate_torch_matches_golden():
+    from genpose2_amd import aggregate
+    g = golden("pipeline")
+    sp, se = aggregate.sort_poses_by_energy(torch.from_numpy(g["pred_pose"]), torch.from_numpy(g["energy"]))
+    np.testing.assert_array_equal(sp.numpy(), g["sorted_pose"])
+    np.testing.assert_array_equal(se.numpy(), g["sorted_energy"])
+    for c in (0, 1):
+        a = aggregate.aggregate_pose(torch.from_numpy(g["pred_pose"]), torch.from_numpy(g["energy"]), clustering=c)
+        assert np.abs(a.numpy() - g[f"aggregated_c{c}"]).max() < 1e-5
+    a = aggregate.aggregate_pose(torch.from_numpy(g["cl_pose"]), torch.from_numpy(g["cl_energy"]))
+    assert np.abs(a.numpy() - g["cl_aggregated"]).max() < 1e-5
+
+
+def test_shard_ranges_cover_every_object_once():
+    from genpose2_amd.shard import shard_range
+    for total, world in [(2048, 8), (64, 2), (65, 8), (3, 8)]:
+        seen = []
+        for r in range(world):
+            lo, hi = shard_range(total, world, r)
+            seen += list(range(lo, hi))
+        assert seen == list(range(total))
+
+
+def _gloo_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from genpose2_amd import pack, shard, synthetic, weights
+    from oracle import oracle
+    # rank 0 owns the packed weights; other ranks receive them by broadcast (the RCCL step)
+    sd = weights.synthetic_state_dict("score", seed=0 if rank == 0 else 99)
+    heads = {k: torch.from_numpy(v) for k, v in sorted(pack.pack_heads(sd).items())}
+    shard.broadcast_tensors(list(heads.values()), src=0)
+    ref = pack.pack_heads(weights.synthetic_state_dict("score", seed=0))
+    ok = all(np.array_equal(heads[k].numpy(), ref[k]) for k in ref)
+    lo, hi = shard.shard_range(6, world, rank)
+    pts, _ = synthetic.make_batch(4, hi - lo, 1024, first_object=lo)
+    feat = oracle.encoder_forward(weights.synthetic_state_dict("score"), pts)
+    np.save(os.path.join(out_dir, f"feat_{rank}.npy"), feat)
+    np.save(os.path.join(out_dir, f"ok_{rank}.npy"), np.array(ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_shards_equal_single_process(tmp_path):
+    import torch.multiprocessing as mp
+    from genpose2_amd import synthetic, weights
+    from oracle import oracle
+    port = 29500 + os.getpid() % 1000
+    mp.spawn(_gloo_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    assert all(np.load(tmp_path / f"ok_{r}.npy") for r in range(2))
+    sharded = np.concatenate([np.load(tmp_path / f"feat_{r}.npy") for r in range(2)])
+    pts, _ = synthetic.make_batch(4, 6, 1024)
+    full = oracle.encoder_forward(weights.synthetic_state_dict("score"), pts)
+    np.testing.assert_array_equal(sharded, full)

@@ -1,0 +1,216 @@
+"""HIP path vs oracle / golden vectors on a real MI355X (all calls go through libgenpose_hip.so).
+
+Tolerances (written here, per north_star): indices bit-exact; fp32 features/scores within
+1e-5 of max |ref|; PC/ODE rotation components within 1e-4 absolute; translations within 1e-5
+relative to max |t| (1e-4 for the ODE T0=1 case, whose adaptive step controller may take a
+different accept/reject path, see tests/test_oracle_golden.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def rel(a, b):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def score_agent():
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    return PoseNet(GenPoseConfig(device=DEV, sampling_steps=20)).eval()
+
+
+# ---------------------------------------------------------------- operator level
+@pytest.mark.parametrize("n,m,grid", [(1024, 512, False), (2048, 512, False), (300, 64, True),
+                                      (1024, 256, True), (37, 37, True), (4096, 128, False)])
+def test_fps_op_bit_exact(n, m, grid):
+    from genpose2_amd import pointnet2_utils as pu
+    from oracle import oracle
+    rng = np.random.default_rng(n + m)
+    xyz = (rng.integers(0, 5, size=(3, n, 3)) if grid else rng.normal(size=(3, n, 3))).astype(np.float32)
+    got = pu.furthest_point_sample(torch.from_numpy(xyz).to(DEV), m).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.furthest_point_sample(xyz, m))
+
+
+@pytest.mark.parametrize("radius,ns,n,m", [(0.2, 16, 1024, 128), (0.5, 32, 500, 33), (0.05, 16, 1024, 64),
+                                           (10.0, 8, 100, 7)])
+def test_ball_query_group_gather_ops(radius, ns, n, m):
+    from genpose2_amd import pointnet2_utils as pu
+    from oracle import oracle
+    rng = np.random.default_rng(ns + n)
+    xyz = rng.uniform(-0.5, 0.5, size=(2, n, 3)).astype(np.float32)
+    xyz[:, n // 2:] = xyz[:, : n - n // 2]          # duplicates
+    new_xyz = xyz[:, rng.choice(n, m, replace=False)].copy()
+    new_xyz[:, 0] = 100.0                             # a centroid with no neighbour
+    idx = pu.ball_query(radius, ns, torch.from_numpy(xyz).to(DEV), torch.from_numpy(new_xyz).to(DEV))
+    np.testing.assert_array_equal(idx.cpu().numpy(), oracle.ball_query(radius, ns, xyz, new_xyz))
+    feats = rng.normal(size=(2, 5, n)).astype(np.float32)
+    g = pu.grouping_operation(torch.from_numpy(feats).to(DEV), idx)
+    np.testing.assert_array_equal(g.cpu().numpy(), oracle.grouping_operation(feats, idx.cpu().numpy()))
+    fidx = torch.from_numpy(rng.integers(0, n, size=(2, m)).astype(np.int32)).to(DEV)
+    ga = pu.gather_operation(torch.from_numpy(feats).to(DEV), fidx)
+    np.testing.assert_array_equal(ga.cpu().numpy(), oracle.gather_operation(feats, fidx.cpu().numpy()))
+
+
+# ---------------------------------------------------------------- encoder
+@pytest.mark.parametrize("tag", ["n1024", "n2048"])
+def test_encoder_levels_vs_golden(tag, score_agent):
+    g = golden("encoder")
+    pts = torch.from_numpy(g[f"{tag}_pts"]).to(DEV)
+    feat, ws = score_agent.encoder.forward(pts, return_workspace=True)
+    torch.cuda.synchronize()
+    B, N = pts.shape[:2]
+    levels = score_agent.encoder.levels(B, N, ws)
+    for lv in range(4):
+        np.testing.assert_array_equal(levels[lv]["fps_idx"].cpu().numpy(), g[f"{tag}_l{lv}_fps"])
+        np.testing.assert_array_equal(levels[lv]["new_xyz"].cpu().numpy(), g[f"{tag}_l{lv}_new_xyz"])
+        for b in range(2):
+            np.testing.assert_array_equal(levels[lv]["ball_idx"][b].cpu().numpy(), g[f"{tag}_l{lv}_ball{b}"])
+        f0 = levels[lv]["features"][0].cpu().numpy().T        # point-major -> (C, M)
+        assert rel(f0, g[f"{tag}_l{lv}_feat0"]) < 1e-5, lv
+    assert rel(feat, g[f"{tag}_feat"]) < 1e-5
+
+
+def test_encoder_batch_independence(score_agent):
+    from genpose2_amd import synthetic
+    pts, _ = synthetic.make_batch(5, 6, 1024, n_unique_every=4)
+    full = score_agent.encoder.forward(torch.from_numpy(pts).to(DEV)).cpu()
+    part = score_agent.encoder.forward(torch.from_numpy(pts[2:4].copy()).to(DEV)).cpu()
+    assert torch.equal(full[2:4], part)   # objects are independent: bitwise
+
+
+# ---------------------------------------------------------------- heads
+def test_score_and_energy_heads_vs_golden(score_agent):
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("heads")
+    for kind, agent in (("score", score_agent), ("energy", PoseNet(GenPoseConfig(device=DEV, agent_type="energy")))):
+        feat = torch.from_numpy(g["pts_feat"]).to(DEV)
+        pobj = agent.heads.object_proj(feat)              # one object per row (k=1)
+        out = []
+        for r in range(g["t"].shape[0]):
+            trow, sig = agent._time_row_and_sigma(agent.heads, float(g["t"][r, 0]))
+            x = torch.from_numpy(g["pose"][r:r + 1]).to(DEV)
+            if kind == "score":
+                out.append(agent.heads.score(pobj[r:r + 1], trow, sig, x, 1))
+            else:
+                out.append(agent.heads.energy(pobj[r:r + 1], trow, sig, x, 1))
+        out = torch.cat(out).cpu().numpy()
+        ref = g[kind]
+        err = np.abs(out - ref).max(1) / np.abs(ref).max(1)
+        assert err.max() < 1e-5, kind
+
+
+# ---------------------------------------------------------------- PC sampler
+@pytest.mark.parametrize("name", ["pc_k10_t100", "pc_k50_t20"])
+def test_pc_pred_func_vs_golden(name):
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden(name)
+    K, T = int(g["K"]), int(g["T"])
+    agent = PoseNet(GenPoseConfig(device=DEV, sampling_steps=T)).eval()
+    agent.noise_feed = NoiseFeed(*(torch.from_numpy(g[k]) for k in ("prior", "z1", "z2")))
+    data = {"pts": torch.from_numpy(g["pts"]).to(DEV), "pts_center": torch.from_numpy(g["pts_center"]).to(DEV)}
+    pose, q, q_avg, xs = agent.pred_func(data, repeat_num=K, return_average_res=True, return_process=True)
+    ref = g["pred_pose"]
+    assert pose.dtype == torch.float32 and pose.shape == ref.shape
+    assert data["rgb_feat"] is None and rel(data["pts_feat"], g["pts_feat"]) < 1e-5
+    p = pose.cpu().numpy()
+    assert np.abs(p[..., :6] - ref[..., :6]).max() < 1e-4
+    assert rel(p[..., 6:], ref[..., 6:]) < 1e-5
+    assert np.abs(q.cpu().numpy()[..., :4] - g["pred_q"][..., :4]).max() < 1e-4
+    assert rel(q.cpu().numpy()[..., 4:], g["pred_q"][..., 4:]) < 1e-5
+    if "xs" in g.files:
+        assert np.abs(xs.cpu().numpy()[..., :6] - g["xs"][..., :6]).max() < 1e-4
+    qa, qa_ref = q_avg.cpu().numpy(), g["pred_q_avg"]
+    assert np.abs(qa[:, :4] - qa_ref[:, :4]).max() < 1e-3 and rel(qa[:, 4:], qa_ref[:, 4:]) < 1e-5
+
+
+def test_pc_full_size_properties():
+    """Config 2 (B=64, N=1024, K=50, T=500) with device Philox noise: size-independent checks."""
+    from genpose2_amd import synthetic
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    pts, center = synthetic.make_batch(2, 64, 1024)
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
+    a1 = PoseNet(GenPoseConfig(device=DEV, sampling_steps=500, noise_seed=3)).eval()
+    a2 = PoseNet(GenPoseConfig(device=DEV, sampling_steps=500, noise_seed=3)).eval()
+    p1, q1 = a1.pred_func(dict(data), repeat_num=50)
+    p2, q2 = a2.pred_func(dict(data), repeat_num=50)
+    assert p1.shape == (64, 50, 9) and q1.shape == (64, 50, 7)
+    assert torch.isfinite(p1).all() and torch.isfinite(q1).all()
+    assert torch.equal(p1, p2) and torch.equal(q1, q2)                  # deterministic given the seed
+    r = p1.reshape(-1, 9).double()
+    b1, b2 = r[:, :3], r[:, 3:6]
+    assert (b1.norm(dim=1) - 1).abs().max() < 1e-5 and (b2.norm(dim=1) - 1).abs().max() < 1e-5
+    assert (b1 * b2).sum(1).abs().max() < 1e-5                            # Gram-Schmidt output
+    assert (q1[..., :4].double().norm(dim=-1) - 1).abs().max() < 1e-5     # unit quaternions
+    p3, _ = a1.pred_func(dict(data), repeat_num=50)                      # next call, next noise
+    assert not torch.equal(p1, p3)
+
+
+# ---------------------------------------------------------------- ODE sampler
+@pytest.mark.parametrize("tag,rot_tol,tr_rel", [("t055_s20", 1e-4, 1e-5), ("t1_none", 5e-4, 1e-4)])
+def test_ode_pred_func_vs_golden(tag, rot_tol, tr_rel):
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("ode")
+    steps = int(g[f"{tag}_steps"])
+    agent = PoseNet(GenPoseConfig(device=DEV, sampler_mode=["ode"], sampling_steps=None if steps < 0 else steps))
+    agent.noise_feed = NoiseFeed(torch.from_numpy(g[f"{tag}_prior"]))
+    data = {"pts": torch.from_numpy(g[f"{tag}_pts"]).to(DEV),
+            "pts_center": torch.from_numpy(g[f"{tag}_pts_center"]).to(DEV)}
+    pose, q = agent.pred_func(data, repeat_num=5, T0=float(g[f"{tag}_T0"]))
+    ref = g[f"{tag}_pred_pose"]
+    assert pose.dtype == torch.float64
+    p = pose.cpu().numpy()
+    assert np.abs(p[..., :6] - ref[..., :6]).max() < rot_tol
+    assert rel(p[..., 6:], ref[..., 6:]) < tr_rel
+    assert np.abs(q.cpu().numpy()[..., :4] - g[f"{tag}_pred_q"][..., :4]).max() < rot_tol * 10
+
+
+# ---------------------------------------------------------------- energy / ranking / scale
+def test_energy_ranking_aggregate_scale_vs_golden():
+    from genpose2_amd import aggregate
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("pipeline")
+    e_agent = PoseNet(GenPoseConfig(device=DEV, agent_type="energy")).eval()
+    data = {"pts": torch.from_numpy(g["pts"]).to(DEV), "pts_center": torch.from_numpy(g["pts_center"]).to(DEV)}
+    pose = torch.from_numpy(g["pred_pose"]).to(DEV)
+    energy = e_agent.get_energy(data, pose, T=1e-5, mode="test", extract_feature=True)
+    assert rel(energy, g["energy"]) < 1e-5
+    order_ref = np.argsort(-g["energy"], axis=1, kind="stable")
+    order = np.argsort(-energy.cpu().numpy(), axis=1, kind="stable")
+    np.testing.assert_array_equal(order, order_ref)                      # identical candidate ranking
+    sp, se = aggregate.sort_poses_by_energy(pose, torch.from_numpy(g["energy"]).to(DEV))
+    np.testing.assert_array_equal(sp.cpu().numpy(), g["sorted_pose"])
+    for c in (0, 1):
+        agg = aggregate.aggregate_pose(pose, torch.from_numpy(g["energy"]).to(DEV), clustering=c)
+        assert np.abs(agg.cpu().numpy() - g[f"aggregated_c{c}"]).max() < 1e-4
+    agg = aggregate.aggregate_pose(torch.from_numpy(g["cl_pose"]).to(DEV), torch.from_numpy(g["cl_energy"]).to(DEV))
+    assert np.abs(agg.cpu().numpy() - g["cl_aggregated"]).max() < 1e-4
+    s_agent = PoseNet(GenPoseConfig(device=DEV, agent_type="scale")).eval()
+    axes, length = s_agent.pred_scale_func({"pts_feat": torch.from_numpy(g["pts_feat"]).to(DEV), "rgb_feat": None,
+                                            "axes": torch.from_numpy(g["scale_axes"]).to(DEV)})
+    assert rel(length, g["scale_length"]) < 1e-5
+
+
+def test_runner_pipeline_smoke():
+    from genpose2_amd import synthetic
+    from genpose2_amd.config import GenPoseConfig
+    from genpose2_amd.runner import EvaluationPipeline
+    pts, center = synthetic.make_batch(3, 8, 1024)
+    pipe = EvaluationPipeline(GenPoseConfig(device=DEV, sampling_steps=50, eval_repeat_num=50), with_scale=True)
+    out = pipe.run({"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)})
+    assert out.pred_pose.shape == (8, 50, 9) and out.energy.shape == (8, 50, 2)
+    assert out.aggregated.shape == (8, 4, 4) and out.length.shape == (8, 3)
+    assert torch.isfinite(out.aggregated).all() and torch.isfinite(out.length).all()
