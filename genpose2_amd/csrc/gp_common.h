@@ -44,17 +44,32 @@ __device__ __forceinline__ f32x4 relu4(f32x4 v) {
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
-// Non-contracted fp32 arithmetic (mirrors the reference's separately rounded torch ops).
-__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
-__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
-__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
-__device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+// Non-contracted fp32 arithmetic (mirrors the reference's separately rounded ops). hipcc's
+// __fmul_rn is a plain multiply that -ffp-contract=fast may still fuse into v_fma, so every
+// helper carries its own `fp contract(off)` scope.
+__device__ __forceinline__ float fmul(float a, float b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
+__device__ __forceinline__ float fadd(float a, float b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+__device__ __forceinline__ float fsub(float a, float b) {
+#pragma clang fp contract(off)
+    return a - b;
+}
+__device__ __forceinline__ float fdiv(float a, float b) {
+#pragma clang fp contract(off)
+    return a / b;
+}
 
 // Squared distance exactly as the reference CUDA text writes it: (dx*dx + dy*dy) + dz*dz
-// with every operation rounded separately (no FMA contraction).
+// with every operation rounded separately (no FMA contraction, no reassociation).
 __device__ __forceinline__ float dist2_ref(float ax, float ay, float az, float bx, float by, float bz) {
-    const float dx = fsub(ax, bx), dy = fsub(ay, by), dz = fsub(az, bz);
-    return fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz));
+#pragma clang fp contract(off)
+    const float dx = ax - bx, dy = ay - by, dz = az - bz;
+    return (dx * dx + dy * dy) + dz * dz;
 }
 
 // --------------------------------------------------------------- Philox4x32-10 + Box-Muller
