@@ -10,7 +10,7 @@ import os
 from typing import Dict, Iterable
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgenpose_hip.so")
+LIB_PATH = os.environ.get("GENPOSE_HIP_LIB", os.path.join(_HERE, "libgenpose_hip.so"))
 
 c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 c_int64_p = ctypes.POINTER(ctypes.c_int64)

@@ -42,6 +42,15 @@ __device__ __forceinline__ f32x4 relu4(f32x4 v) {
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// Buffer resource over `bytes` bytes at p (p must be wave-uniform: a kernel argument).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// 16-byte buffer load: voffset per lane (VGPR), soffset wave-uniform (SGPR).
+__device__ __forceinline__ f32x4 ldbuf4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
 // Non-contracted fp32 arithmetic (mirrors the reference's separately rounded ops). hipcc's

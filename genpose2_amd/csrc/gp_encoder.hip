@@ -104,15 +104,18 @@ __global__ __launch_bounds__(SA_THREADS) void sa_branch_kernel(SAArgs a) {
 #pragma unroll
                     for (int ct = 0; ct < CT; ++ct) bf[ct] = in_lds[(g * CT + ct) * 64 + lane];
                 }
+                f32x4 af[TC];
 #pragma unroll
-                for (int t = 0; t < TC; ++t) {
-                    const int T = T0 + t;
-                    if (T < NT) {
-                        const f32x4 af = ld4(W + ((size_t)(T * KG + g) * 64 + lane) * 4);
+                for (int t = 0; t < TC; ++t)
+                    af[t] = (T0 + t < NT) ? ld4(W + ((size_t)((T0 + t) * KG + g) * 64 + lane) * 4)
+                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+                // k-step outermost so consecutive MFMAs use different accumulators
 #pragma unroll
-                        for (int ct = 0; ct < CT; ++ct) acc[t][ct] = mfma_kgroup(af, bf[ct], acc[t][ct]);
-                    }
-                }
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int t = 0; t < TC; ++t)
+#pragma unroll
+                        for (int ct = 0; ct < CT; ++ct) acc[t][ct] = mfma4(af[t][j], bf[ct][j], acc[t][ct]);
             }
 #pragma unroll
             for (int t = 0; t < TC; ++t) {

@@ -24,105 +24,194 @@
 constexpr int HT = 256;          // threads per workgroup
 constexpr int HID = 256;         // pose/head hidden width
 constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
+#ifndef PC_WV1
+#define PC_WV1 8                 // waves per workgroup, 16-candidate PC tiles
+#endif
+#ifndef PC_WV2
+#define PC_WV2 4                 // waves per workgroup, 32-candidate PC tiles
+#endif
+#ifndef EVAL_WV
+#define EVAL_WV 8                // waves per workgroup, score/energy evaluation
+#endif
+#ifndef HEAD_PREFETCH
+#define HEAD_PREFETCH 2          // k-groups of head-layer-1 weights kept in flight
+#endif
 
 // ============================================================================ shared head trunk
+// NT = column tiles (16 candidates each) per workgroup.
+template <int NT, int WV>
 struct HeadSmem {
-    float xin[16 * 16];            // input poses, [col][16] (9 used)
-    f32x4 act1[KG_HID * 64];       // pose_encoder.0 output (accumulator-native layout)
-    f32x4 act2[KG_HID * 64];       // pose_encoder.2 output
-    float red[4][9][16];           // per-wave head-layer-2 partials
-    float f[16][9];                // head output before the sigma division
-    float scratch[HT];
+    float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
+    f32x4 act1[KG_HID * NT * 64];      // pose_encoder.0 output, accumulator-native [g][ct][lane]
+    f32x4 act2[KG_HID * NT * 64];      // pose_encoder.2 output
+    float red[WV][9][NT * 16];         // per-wave head-layer-2 partials
+    float f[NT * 16][9];               // head output before the sigma division
+    float noise[NT * 16][2][12];       // PC corrector / predictor draws of this step
+    float scratch[WV * 64];
+    // small per-launch weights staged once per workgroup (their loads overlap the PC update)
+    f32x4 pe0w[16 * 64];               // pose_encoder.0 packed A fragments
+    float pe0b[HID], pe2b[HID];
+    float h2w[9 * HID];                // head layer 2, [head*3 + out][256]
+    float h2b[12];
 };
 
-// Computes f (16 cols x 9) = heads(x) into sm.f for the 16 candidates of this tile.
-// `obj` maps column -> object row of pobj; `tproj` is the 768-vector of this time value.
-__device__ void head_trunk(const gp_head_weights& w, const float* __restrict__ pobj,
-                           const float* __restrict__ tproj, const int* obj_of_col, HeadSmem& sm) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+template <int NT, int WV>
+__device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, HeadSmem<NT, WV>& sm) {
+    constexpr int NTH = WV * 64;
+    for (int i = threadIdx.x; i < 16 * 64; i += NTH) sm.pe0w[i] = ld4(w.pe0_w + (size_t)i * 4);
+    for (int i = threadIdx.x; i < HID; i += NTH) {
+        sm.pe0b[i] = w.pe0_b[i];
+        sm.pe2b[i] = w.pe2_b[i];
+    }
+    for (int i = threadIdx.x; i < 9 * HID / 4; i += NTH) st4(&sm.h2w[i * 4], ld4(w.h2_w + (size_t)i * 4));
+    if (threadIdx.x < 9) sm.h2b[threadIdx.x] = w.h2_b[threadIdx.x];
+}
+
+// acc[t][ct] += sum_g A(tile T[t], k-group g) . B(k-group g, column tile ct) over KG k-groups.
+// A fragments stream from global (L2-resident packed weights) through a (D+1)-slot register ring
+// so that the loads of k-group g+D are in flight while k-group g feeds the MFMAs; B fragments
+// come from LDS. Loads are raw buffer loads: the tile/k-group offset is a wave-uniform SGPR
+// (soffset) and the only per-lane address is lane*16 (voffset), so the fully unrolled ring needs
+// no 64-bit address registers. Every ring index is a compile-time constant.
+template <int G, int TT, int NT, int KG, int D>
+__device__ __forceinline__ void stream_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f32x4* __restrict__ B,
+                                            int lane, int voff, f32x4 (&ring)[D + 1][TT], f32x4 (&acc)[TT][NT]) {
+    if constexpr (G < KG + D) {
+        if constexpr (G < KG) {
+#pragma unroll
+            for (int t = 0; t < TT; ++t) ring[G % (D + 1)][t] = ldbuf4(W, voff, (T[t] * KG + G) * 1024);
+        }
+        // keep the prefetch where it is: without this fence the scheduler sinks every load next to
+        // its MFMAs and waits vmcnt(0) per k-group (checked in the .s)
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (G >= D) {
+            constexpr int GG = G - D;
+            f32x4 bf[NT];
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) bf[ct] = B[(GG * NT + ct) * 64 + lane];
+            // k-step outermost: consecutive MFMAs hit different accumulators (16x16x4 f32 has a
+            // 40-cycle dependent latency vs a 32-cycle issue interval)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int t = 0; t < TT; ++t)
+#pragma unroll
+                    for (int ct = 0; ct < NT; ++ct)
+                        acc[t][ct] = mfma4(ring[GG % (D + 1)][t][j], bf[ct][j], acc[t][ct]);
+        }
+        stream_step<G + 1, TT, NT, KG, D>(W, T, B, lane, voff, ring, acc);
+    }
+}
+
+// acc[t][ct] += sum_g A(tile T[t], k-group g) . B(k-group g, column tile ct) over KG k-groups.
+// A fragments stream from global (L2-resident packed weights) through a (D+1)-slot register ring
+// so that the loads of k-group g+D are in flight while k-group g feeds the MFMAs; B fragments
+// come from LDS. Loads are raw buffer loads: the tile/k-group offset is a wave-uniform SGPR
+// (soffset) and the only per-lane address is lane*16 (voffset). The k-group loop is unrolled by
+// template recursion, so every ring index is a compile-time constant (no scratch).
+template <int TT, int NT, int KG, int D>
+__device__ __forceinline__ void stream_layer(__amdgpu_buffer_rsrc_t W, const int (&T)[TT],
+                                             const f32x4* __restrict__ B, int lane, f32x4 (&acc)[TT][NT]) {
+    f32x4 ring[D + 1][TT];
+    stream_step<0, TT, NT, KG, D>(W, T, B, lane, lane * 16, ring, acc);
+}
+
+// Computes f (NT*16 cols x 9) = heads(x) into sm.f for the candidates of this workgroup.
+// `obj_of_col` maps column -> object row of pobj; `tproj` is the 768-vector of this time value.
+template <int NT, int WV>
+__device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float* __restrict__ pobj,
+                           const float* __restrict__ tproj, const int* obj_of_col, HeadSmem<NT, WV>& sm) {
+    constexpr int TPW = 16 / WV;   // output tiles per wave and per 256-wide layer
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
     const int q = lane >> 4, n = lane & 15;
     // ---- pose_encoder.0 (9 -> 256), one k-group
     {
-        const f32x4 bf = ld4(&sm.xin[n * 16 + 4 * q]);
+        f32x4 bf[NT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int T = wid * 4 + t;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            acc = mfma_kgroup(ld4(w.pe0_w + ((size_t)T * 64 + lane) * 4), bf, acc);
-            sm.act1[T * 64 + lane] = relu4(acc + ld4(w.pe0_b + 16 * T + 4 * q));
+        for (int ct = 0; ct < NT; ++ct) bf[ct] = ld4(&sm.xin[(ct * 16 + n) * 16 + 4 * q]);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const int T = wid * TPW + t;
+            const f32x4 a = sm.pe0w[T * 64 + lane];
+            const f32x4 bias = ld4(&sm.pe0b[16 * T + 4 * q]);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct)
+                sm.act1[(T * NT + ct) * 64 + lane] = relu4(mfma_kgroup(a, bf[ct], f32x4{0.f, 0.f, 0.f, 0.f}) + bias);
         }
     }
     __syncthreads();
-    // ---- pose_encoder.2 (256 -> 256)
+    // ---- pose_encoder.2 (256 -> 256): TPW output tiles per wave
     {
-        f32x4 acc[4];
+        f32x4 acc[TPW][NT];
+        int Ts[TPW];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int g = 0; g < KG_HID; ++g) {
-            const f32x4 bf = sm.act1[g * 64 + lane];
+        for (int t = 0; t < TPW; ++t) {
+            Ts[t] = wid * TPW + t;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int T = wid * 4 + t;
-                acc[t] = mfma_kgroup(ld4(w.pe2_w + ((size_t)(T * KG_HID + g) * 64 + lane) * 4), bf, acc[t]);
-            }
+            for (int ct = 0; ct < NT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+        stream_layer<TPW, NT, KG_HID, 3>(make_rsrc(w.pe2_w, HID * HID * 4), Ts, sm.act1, lane, acc);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int T = wid * 4 + t;
-            sm.act2[T * 64 + lane] = relu4(acc[t] + ld4(w.pe2_b + 16 * T + 4 * q));
+        for (int t = 0; t < TPW; ++t) {
+            const f32x4 bias = ld4(&sm.pe2b[16 * Ts[t] + 4 * q]);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) sm.act2[(Ts[t] * NT + ct) * 64 + lane] = relu4(acc[t][ct] + bias);
         }
     }
     __syncthreads();
-    // ---- head layer 1 (pose block 256 -> 3x256) + hoisted pts/t blocks, ReLU, head layer 2 partials
-    const int ob = obj_of_col[n];
-    f32x4 acc[3][4];
+    // ---- head layer 1 (pose block 256 -> 3x256) + hoisted pts/t blocks; 3*TPW output tiles per wave
+    f32x4 acc[3 * TPW][NT];
+    int Ts[3 * TPW];
 #pragma unroll
     for (int h = 0; h < 3; ++h)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int ch = h * HID + 16 * (wid * 4 + t) + 4 * q;
-            acc[h][t] = ld4(pobj + (size_t)ob * (3 * HID) + ch) + ld4(tproj + ch);
+        for (int t = 0; t < TPW; ++t) {
+            const int T = h * 16 + wid * TPW + t;
+            Ts[h * TPW + t] = T;
+            const f32x4 tp = ld4(tproj + 16 * T + 4 * q);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct)
+                acc[h * TPW + t][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q) + tp;
         }
-    for (int g = 0; g < KG_HID; ++g) {
-        const f32x4 bf = sm.act2[g * 64 + lane];
-#pragma unroll
-        for (int h = 0; h < 3; ++h)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int T = h * 16 + wid * 4 + t;
-                acc[h][t] = mfma_kgroup(ld4(w.h1p_w + ((size_t)(T * KG_HID + g) * 64 + lane) * 4), bf, acc[h][t]);
-            }
-    }
+    stream_layer<3 * TPW, NT, KG_HID, HEAD_PREFETCH>(make_rsrc(w.h1p_w, 3 * HID * HID * 4), Ts, sm.act2, lane, acc);
+    // ---- ReLU -> head layer 2 (block diagonal 3 x (256 -> 3)) partial dot products
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
-        float p0 = 0.f, p1 = 0.f, p2 = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const f32x4 u = relu4(acc[h][t]);
-            const int ch = 16 * (wid * 4 + t) + 4 * q;
-            const f32x4 w0 = ld4(w.h2_w + (h * 3 + 0) * HID + ch);
-            const f32x4 w1 = ld4(w.h2_w + (h * 3 + 1) * HID + ch);
-            const f32x4 w2 = ld4(w.h2_w + (h * 3 + 2) * HID + ch);
-            p0 += u.x * w0.x + u.y * w0.y + u.z * w0.z + u.w * w0.w;
-            p1 += u.x * w1.x + u.y * w1.y + u.z * w1.z + u.w * w1.w;
-            p2 += u.x * w2.x + u.y * w2.y + u.z * w2.z + u.w * w2.w;
-        }
+        for (int ct = 0; ct < NT; ++ct) {
+            float p0 = 0.f, p1 = 0.f, p2 = 0.f;
 #pragma unroll
-        for (int off = 16; off <= 32; off <<= 1) {
-            p0 += __shfl_xor(p0, off, 64);
-            p1 += __shfl_xor(p1, off, 64);
-            p2 += __shfl_xor(p2, off, 64);
-        }
-        if (q == 0) {
-            sm.red[wid][h * 3 + 0][n] = p0;
-            sm.red[wid][h * 3 + 1][n] = p1;
-            sm.red[wid][h * 3 + 2][n] = p2;
+            for (int t = 0; t < TPW; ++t) {
+                const f32x4 u = relu4(acc[h * TPW + t][ct]);
+                const int ch = 16 * (wid * TPW + t) + 4 * q;
+                const f32x4 w0 = ld4(&sm.h2w[(h * 3 + 0) * HID + ch]);
+                const f32x4 w1 = ld4(&sm.h2w[(h * 3 + 1) * HID + ch]);
+                const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
+                p0 += u.x * w0.x + u.y * w0.y + u.z * w0.z + u.w * w0.w;
+                p1 += u.x * w1.x + u.y * w1.y + u.z * w1.z + u.w * w1.w;
+                p2 += u.x * w2.x + u.y * w2.y + u.z * w2.z + u.w * w2.w;
+            }
+#pragma unroll
+            for (int off = 16; off <= 32; off <<= 1) {
+                p0 += __shfl_xor(p0, off, 64);
+                p1 += __shfl_xor(p1, off, 64);
+                p2 += __shfl_xor(p2, off, 64);
+            }
+            if (q == 0) {
+                sm.red[wid][h * 3 + 0][ct * 16 + n] = p0;
+                sm.red[wid][h * 3 + 1][ct * 16 + n] = p1;
+                sm.red[wid][h * 3 + 2][ct * 16 + n] = p2;
+            }
         }
     }
     __syncthreads();
-    if (threadIdx.x < 16 * 9) {
-        const int c = threadIdx.x / 9, o = threadIdx.x - c * 9;
-        sm.f[c][o] = w.h2_b[o] + ((sm.red[0][o][c] + sm.red[1][o][c]) + (sm.red[2][o][c] + sm.red[3][o][c]));
+    for (int e = threadIdx.x; e < NT * 16 * 9; e += WV * 64) {
+        const int c = e / 9, o = e - c * 9;
+        float acc2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < WV; ++v) acc2 += sm.red[v][o][c];
+        sm.f[c][o] = sm.h2b[o] + acc2;
     }
     __syncthreads();
 }
@@ -250,14 +339,15 @@ extern "C" int gp_head_time_proj(const gp_head_weights* w, const float* t, int n
 
 // ============================================================================ score / energy eval
 template <int MODE>  // 0: score f/(sigma+1e-7), 1: energy (IP, decoupled)
-__global__ __launch_bounds__(HT) void head_eval_kernel(gp_head_weights w, const float* __restrict__ pobj,
+__global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights w, const float* __restrict__ pobj,
                                                        const float* __restrict__ tproj, float sigma,
                                                        const float* __restrict__ x, int rows, int kper,
                                                        float* __restrict__ out) {
-    __shared__ HeadSmem sm;
+    __shared__ HeadSmem<1, EVAL_WV> sm;
     __shared__ int obj[16];
     const int r0 = blockIdx.x * 16;
-    for (int i = threadIdx.x; i < 256; i += HT) {
+    stage_small_weights<1, EVAL_WV>(w, sm);
+    for (int i = threadIdx.x; i < 256; i += EVAL_WV * 64) {
         const int c = i >> 4, j = i & 15;
         const int r = r0 + c;
         sm.xin[i] = (r < rows && j < 9) ? x[(size_t)r * 9 + j] : 0.f;
@@ -267,7 +357,7 @@ __global__ __launch_bounds__(HT) void head_eval_kernel(gp_head_weights w, const 
         obj[threadIdx.x] = (r < rows ? r : rows - 1) / kper;
     }
     __syncthreads();
-    head_trunk(w, pobj, tproj, obj, sm);
+    head_trunk<1, EVAL_WV>(w, pobj, tproj, obj, sm);
     if (MODE == 0) {
         if (threadIdx.x < 144) {
             const int c = threadIdx.x / 9, o = threadIdx.x - c * 9;
@@ -290,7 +380,7 @@ extern "C" int gp_score_eval(const gp_head_weights* w, const float* pobj, const 
                              const float* x, int rows, int k, float* score, hipStream_t stream) {
     GP_REQUIRE(w && pobj && tproj_row && x && score && rows >= 0 && k >= 1, "score_eval: bad arguments");
     if (!rows) return GP_OK;
-    hipLaunchKernelGGL(head_eval_kernel<0>, dim3((rows + 15) / 16), dim3(HT), 0, stream, *w, pobj, tproj_row,
+    hipLaunchKernelGGL(head_eval_kernel<0>, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
                        sigma, x, rows, k, score);
     return gp_check_launch("head_eval_kernel<score>");
 }
@@ -299,7 +389,7 @@ extern "C" int gp_energy_eval(const gp_head_weights* w, const float* pobj, const
                               const float* pose, int rows, int k, float* energy, hipStream_t stream) {
     GP_REQUIRE(w && pobj && tproj_row && pose && energy && rows >= 0 && k >= 1, "energy_eval: bad arguments");
     if (!rows) return GP_OK;
-    hipLaunchKernelGGL(head_eval_kernel<1>, dim3((rows + 15) / 16), dim3(HT), 0, stream, *w, pobj, tproj_row,
+    hipLaunchKernelGGL(head_eval_kernel<1>, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
                        sigma, pose, rows, k, energy);
     return gp_check_launch("head_eval_kernel<energy>");
 }
@@ -315,7 +405,7 @@ struct PCArgs {
     const float* tproj;   // (T, 768)
     float* x;             // (R, 9) state
     float* s;             // (R, 9) score of the previous step
-    float* part;          // (2, ntiles) per-tile sums of row score norms
+    float* part;          // (2, nwg) per-workgroup sums of row score norms
     const float* z1;      // (T, R, 9) or null -> Philox
     const float* z2;
     uint64_t seed;
@@ -323,51 +413,65 @@ struct PCArgs {
     float* res;           // (R, 9)
     float* q;             // (R, 7)
     float* xs;            // (R, T, 9) or null
-    int rows, kper, steps, ntiles;
+    int rows, kper, steps, nwg;
     float ls_coef;        // snr * sqrt(pose_dim)
 };
 
-__device__ __forceinline__ float noise_at(const float* z, uint64_t seed, int stream, int step, int rows, int r,
-                                          int j) {
-    if (z) return z[((size_t)step * rows + r) * 9 + j];
-    const f32x4 v = philox_normal4(seed, (uint32_t)(stream + 2 * step), (uint32_t)r, (uint32_t)(j >> 2));
-    const int c = j & 3;
-    return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
-}
-
 // Launch i in [0, steps]: finish step i-1 (if i > 0), then score at step i (if i < steps).
-__global__ __launch_bounds__(HT) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
-    __shared__ HeadSmem sm;
-    __shared__ int obj[16];
+template <int NT, int WV>
+__global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
+    constexpr int ROWS = NT * 16;
+    constexpr int NTH = WV * 64;
+    __shared__ HeadSmem<NT, WV> sm;
+    __shared__ int obj[ROWS];
     __shared__ float s_gn;
     const int tid = threadIdx.x;
-    const int tile = blockIdx.x;
-    const int r0 = tile * 16;
-    if (tid < 16) {
+    const int r0 = blockIdx.x * ROWS;
+    if (i < a.steps) stage_small_weights<NT, WV>(a.w, sm);
+    if (tid < ROWS) {
         const int r = r0 + tid;
         obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
     }
     if (i == 0) {
-        for (int e = tid; e < 256; e += HT) {
+        for (int e = tid; e < ROWS * 16; e += NTH) {
             const int c = e >> 4, j = e & 15;
             const int r = r0 + c;
             sm.xin[e] = (r < a.rows && j < 9) ? a.x[(size_t)r * 9 + j] : 0.f;
         }
     } else {
         // ---- grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143), fixed order
-        const float* part = a.part + (size_t)((i - 1) & 1) * a.ntiles;
+        const float* part = a.part + (size_t)((i - 1) & 1) * a.nwg;
         float acc = 0.f;
-        for (int t = tid; t < a.ntiles; t += HT) acc += part[t];
+        for (int t = tid; t < a.nwg; t += NTH) acc += part[t];
         sm.scratch[tid] = acc;
+        // ---- this step's draws: 2 streams x 3 blocks of 4 normals per row, one per thread
+        for (int e = tid; e < ROWS * 6; e += NTH) {
+            const int c = e / 6, st = (e - c * 6) / 3, blk = e - c * 6 - st * 3;
+            const int r = r0 + c;
+            float* dst = &sm.noise[c][st][blk * 4];
+            const float* z = st ? a.z2 : a.z1;
+            if (r >= a.rows) {
+                dst[0] = dst[1] = dst[2] = dst[3] = 0.f;
+            } else if (z) {
+                const float* src = z + ((size_t)(i - 1) * a.rows + r) * 9 + blk * 4;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dst[j] = (blk * 4 + j < 9) ? src[j] : 0.f;
+            } else {
+                const f32x4 v = philox_normal4(a.seed, (uint32_t)(st + 2 * (i - 1)), (uint32_t)r, (uint32_t)blk);
+                dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+            }
+        }
         __syncthreads();
         if (tid < 64) {
-            float v = (sm.scratch[tid] + sm.scratch[tid + 64]) + (sm.scratch[tid + 128] + sm.scratch[tid + 192]);
+            float v = 0.f;
+#pragma unroll
+            for (int u = 0; u < WV; ++u) v += sm.scratch[tid + 64 * u];
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
             if (tid == 0) s_gn = v / (float)a.rows;
         }
         __syncthreads();
-        if (tid < 16) {
+        if (tid < ROWS) {
 #pragma clang fp contract(off)
             const int r = r0 + tid;
             float xv[9];
@@ -377,12 +481,13 @@ __global__ __launch_bounds__(HT) void pc_step_kernel(PCArgs a, int i, PCStep cur
                 const float ls = 2.0f * (ratio * ratio);
                 const float sq2ls = sqrtf(2.0f * ls);
                 const float* sp = a.s + (size_t)r * 9;
+                const float* z1 = sm.noise[tid][0];
+                const float* z2 = sm.noise[tid][1];
                 float sv[9];
 #pragma unroll
                 for (int j = 0; j < 9; ++j) {
                     sv[j] = sp[j];
-                    const float z = noise_at(a.z1, a.seed, 0, i - 1, a.rows, r, j);
-                    xv[j] = (a.x[(size_t)r * 9 + j] + ls * sv[j]) + sq2ls * z;
+                    xv[j] = (a.x[(size_t)r * 9 + j] + ls * sv[j]) + sq2ls * z1[j];
                 }
                 // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
                 const float na = sqrtf((xv[0] * xv[0] + xv[1] * xv[1]) + xv[2] * xv[2]);
@@ -397,8 +502,7 @@ __global__ __launch_bounds__(HT) void pc_step_kernel(PCArgs a, int i, PCStep cur
                 for (int j = 0; j < 9; ++j) {
                     const float drift = 0.0f - g2 * sv[j];
                     mean[j] = xv[j] + drift * prev.dt;
-                    const float z = noise_at(a.z2, a.seed, 1, i - 1, a.rows, r, j);
-                    xv[j] = mean[j] + gs * z;
+                    xv[j] = mean[j] + gs * z2[j];
                 }
                 gram_schmidt6<float>(xv);
                 const float* cen = a.center + (size_t)obj[tid] * 3;
@@ -437,31 +541,41 @@ __global__ __launch_bounds__(HT) void pc_step_kernel(PCArgs a, int i, PCStep cur
     }
     if (i == a.steps) return;  // finalize launch: no score evaluation
     __syncthreads();
-    head_trunk(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm);
-    // ---- s = f / (sigma + 1e-7); tile partial of sum_r ||s_r||
-    if (tid < 16) {
-        const int r = r0 + tid;
+    head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm);
+    // ---- s = f / (sigma + 1e-7); workgroup partial of sum_r ||s_r||
+    if (tid < 64) {
         float nrm = 0.f;
-        if (r < a.rows) {
-            const float den = fadd(cur.sigma, 1e-7f);
-            float ss = 0.f;
+        for (int c = tid; c < ROWS; c += 64) {
+            const int r = r0 + c;
+            if (r < a.rows) {
+                const float den = fadd(cur.sigma, 1e-7f);
+                float ss = 0.f;
 #pragma unroll
-            for (int j = 0; j < 9; ++j) {
-                const float v = fdiv(sm.f[tid][j], den);
-                a.s[(size_t)r * 9 + j] = v;
-                ss = fadd(ss, fmul(v, v));
+                for (int j = 0; j < 9; ++j) {
+                    const float v = fdiv(sm.f[c][j], den);
+                    a.s[(size_t)r * 9 + j] = v;
+                    ss = fadd(ss, fmul(v, v));
+                }
+                nrm += sqrtf(ss);
             }
-            nrm = sqrtf(ss);
         }
 #pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) nrm += __shfl_xor(nrm, off, 16);
-        if (tid == 0) a.part[(size_t)(i & 1) * a.ntiles + tile] = nrm;
+        for (int off = 32; off >= 1; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
+        if (tid == 0) a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = nrm;
     }
 }
 
 extern "C" size_t gp_pc_workspace_size(int rows) {
     const size_t ntiles = ((size_t)rows + 15) / 16;
     return sizeof(float) * ((size_t)rows * 9 + 2 * ntiles) + 256;
+}
+
+static int pc_pick_nt(int rows) {
+    // Measured on MI355X (scripts/kbench.py): 16 candidates x 8 waves per workgroup beats 32 x 4
+    // at every size (R=25,600: 125 vs 153 us/step) because 112 VGPRs leave room for two
+    // workgroups per CU, while the 32-wide tile needs 373 registers (one wave per SIMD).
+    (void)rows;
+    return 1;
 }
 
 extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const float* tproj, const float* step_tab,
@@ -473,6 +587,7 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     GP_REQUIRE(steps >= 2 && rows >= 1 && k >= 1, "pc_sample: need steps>=2, rows>=1, k>=1");
     GP_REQUIRE((z1 == nullptr) == (z2 == nullptr), "pc_sample: z1/z2 must both be given or both null");
     GP_REQUIRE(workspace_bytes >= gp_pc_workspace_size(rows), "pc_sample: workspace too small");
+    const int nt = pc_pick_nt(rows);
     PCArgs a;
     a.w = *w;
     a.pobj = pobj;
@@ -490,16 +605,19 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     a.rows = rows;
     a.kper = k;
     a.steps = steps;
-    a.ntiles = (rows + 15) / 16;
+    a.nwg = (rows + 16 * nt - 1) / (16 * nt);
     a.ls_coef = snr * 3.0f;  // snr * sqrt(pose_dim=9) in fp32 (0.48 rounds identically)
-    const dim3 grid(a.ntiles);
+    const dim3 grid(a.nwg);
     for (int i = 0; i <= steps; ++i) {
         PCStep cur = {}, prev = {};
         if (i < steps) cur = PCStep{step_tab[5 * i], step_tab[5 * i + 1], step_tab[5 * i + 2], step_tab[5 * i + 3],
                                     step_tab[5 * i + 4]};
         if (i > 0) prev = PCStep{step_tab[5 * (i - 1)], step_tab[5 * (i - 1) + 1], step_tab[5 * (i - 1) + 2],
                                  step_tab[5 * (i - 1) + 3], step_tab[5 * (i - 1) + 4]};
-        hipLaunchKernelGGL(pc_step_kernel, grid, dim3(HT), 0, stream, a, i, cur, prev);
+        if (nt == 2)
+            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV2>), grid, dim3(PC_WV2 * 64), 0, stream, a, i, cur, prev);
+        else
+            hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
     }
     return gp_check_launch("pc_step_kernel");
 }
