@@ -74,21 +74,27 @@ __global__ __launch_bounds__(SA_THREADS) void sa_branch_kernel(SAArgs a) {
         bx[ct] = v;
     }
     const int feat_groups = a.c_prev >> 4;
+    const int wid_u = __builtin_amdgcn_readfirstlane(wid);   // wave-uniform tile ids -> SGPR offsets
+    const int voff = lane * 16;
 
     for (int L = 0; L < a.nlayers; ++L) {
         const int KG = a.kg[L], NT = a.nt[L];
-        const float* __restrict__ W = a.w[L];
+        const __amdgpu_buffer_rsrc_t W = make_rsrc(a.w[L], (uint32_t)(NT * KG) * 1024u);
         const f32x4* in_lds = (L == 1) ? lds : lds + a.buf1_off;   // L>=1 reads buffer (L-1)&1
         f32x4* out_lds = (L == 0) ? lds : lds + a.buf1_off;         // L<last writes buffer L&1
         const bool last = (L == a.nlayers - 1);
-        for (int T0 = wid * TC; T0 < NT; T0 += 4 * TC) {
+        for (int T0 = wid_u * TC; T0 < NT; T0 += 4 * TC) {
             f32x4 acc[TC][CT];
 #pragma unroll
             for (int t = 0; t < TC; ++t)
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-            for (int g = 0; g < KG; ++g) {
-                f32x4 bf[CT];
+            // operand fetch for k-group g: A = packed weights (buffer load, SGPR offset), B = the
+            // gathered neighbour features (layer 0) or the previous layer in LDS
+            auto fetch = [&](int g, f32x4 (&af)[TC], f32x4 (&bf)[CT]) {
+#pragma unroll
+                for (int t = 0; t < TC; ++t)
+                    af[t] = (T0 + t < NT) ? ldbuf4(W, voff, ((T0 + t) * KG + g) * 1024) : f32x4{0.f, 0.f, 0.f, 0.f};
                 if (L == 0) {
                     if (g < feat_groups) {
 #pragma unroll
@@ -104,18 +110,27 @@ __global__ __launch_bounds__(SA_THREADS) void sa_branch_kernel(SAArgs a) {
 #pragma unroll
                     for (int ct = 0; ct < CT; ++ct) bf[ct] = in_lds[(g * CT + ct) * 64 + lane];
                 }
-                f32x4 af[TC];
-#pragma unroll
-                for (int t = 0; t < TC; ++t)
-                    af[t] = (T0 + t < NT) ? ld4(W + ((size_t)((T0 + t) * KG + g) * 64 + lane) * 4)
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
-                // k-step outermost so consecutive MFMAs use different accumulators
+            };
+            // k-step outermost so consecutive MFMAs use different accumulators
+            auto compute = [&](const f32x4 (&af)[TC], const f32x4 (&bf)[CT]) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
 #pragma unroll
                     for (int t = 0; t < TC; ++t)
 #pragma unroll
                         for (int ct = 0; ct < CT; ++ct) acc[t][ct] = mfma4(af[t][j], bf[ct][j], acc[t][ct]);
+            };
+            // two-slot ping-pong: the operands of k-group g+1 are in flight while g computes;
+            // sched_barrier keeps the compiler from sinking the loads back next to their MFMAs
+            f32x4 aA[TC], bA[CT], aB[TC], bB[CT];
+            fetch(0, aA, bA);
+            for (int g = 0; g < KG; g += 2) {
+                if (g + 1 < KG) fetch(g + 1, aB, bB);
+                __builtin_amdgcn_sched_barrier(0);
+                compute(aA, bA);
+                if (g + 2 < KG) fetch(g + 2, aA, bA);
+                __builtin_amdgcn_sched_barrier(0);
+                if (g + 1 < KG) compute(aB, bB);
             }
 #pragma unroll
             for (int t = 0; t < TC; ++t) {
@@ -313,7 +328,9 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                 gp_set_error("encoder_forward: nsample %d not a multiple of 16", a.ns);
                 return GP_ERR_UNSUPPORTED;
             }
-            rc = (l == 3) ? launch_sa<2>(a, B, st) : launch_sa<4>(a, B, st);
+            // level 3 at 32 columns (its 640-channel LDS ping-pong), GroupAll split over 2 workgroups
+            // per (object, branch) with atomicMax pooling (4x the workgroups of one per object)
+            rc = (l >= 3) ? launch_sa<2>(a, B, st) : launch_sa<4>(a, B, st);
             if (rc) return rc;
         }
     }
