@@ -78,16 +78,19 @@ def cpu_baseline(cfg, threads):
                       f"({t_step*1e3:.0f} ms/step), extrapolated to B={B}, T={T}"}
 
 
-def load_traffic():
-    """HBM bytes per pc_step launch from a committed PMC pass (profiles/*pmc*.json), or None."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_pc_step*.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+def load_traffic(rows):
+    """HBM(+Infinity Cache) bytes per pc_step launch from the newest committed PMC pass for the
+    same row count (profiles/**/pmc_pc_step*.json, scripts/pmc_passes.sh), or None."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "**", "pmc_pc_step*.json"), recursive=True))
+    for fn in reversed(files):
+        try:
+            with open(fn) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("rows") == rows:
+            return d.get("hbm_bytes_per_launch")
+    return None
 
 
 def main():
@@ -198,7 +201,7 @@ def main():
                                    f"{' + ScaleNet' if cfgd['scale'] else ''} (encoder + sampler per step)",
                        "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": load_traffic(),
+                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": load_traffic(B * K),
                          "kernel": "pc_step_kernel", "flop_per_launch": flop_launch,
                          "avg_launch_us": per_launch_s * 1e6, "sampler_ms_per_step": samp_ms},
         }
