@@ -40,140 +40,164 @@ struct SAArgs {
 
 constexpr int SA_THREADS = 256;
 
-template <int CT, int TC, int SPAN>
-__global__ __launch_bounds__(SA_THREADS) void sa_branch_kernel(SAArgs a) {
-    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+// One layer for the CTW column tiles [cbase, cbase+CTW) of this wave and the output tiles
+// wt*TC, wt*TC + WT*TC, ... (WT = waves sharing the columns). Layers narrower than 4*TC output
+// tiles split the workgroup's columns over waves instead of leaving waves idle.
+template <int CT, int CTW, int TC, int SPAN>
+__device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int b, int col0, int cbase,
+                                         int wt, int WT) {
+    const int lane = threadIdx.x & 63;
     const int q = lane >> 4, nn = lane & 15;
-    const int b = blockIdx.y;
-    const int col0 = blockIdx.x * CT * 16;
-    const int tpc = a.ns >> 4;  // column tiles per centroid
-
-    // per-lane gathered point of each column tile + the xyz k-group fragment
-    int pi[CT];
-    bool valid[CT];
-    f32x4 bx[CT];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-        const int col = col0 + ct * 16 + nn;
-        valid[ct] = col < a.cols;
-        const int m = col / a.ns, s = col - m * a.ns;
-        int p = 0;
-        if (valid[ct]) p = a.nbr ? a.nbr[((size_t)b * a.m + m) * a.ns + s] : s;
-        pi[ct] = p;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (valid[ct] && q == 0) {
-            const float* px = a.xyz_prev + ((size_t)b * a.n_prev + p) * 3;
-            if (a.cent) {  // grouped_xyz -= new_xyz (pointnet2_utils.py:281-282)
-                const float* c = a.cent + ((size_t)b * a.m + m) * 3;
-                v = f32x4{fsub(px[0], c[0]), fsub(px[1], c[1]), fsub(px[2], c[2]), 0.f};
-            } else {       // GroupAll keeps raw xyz (pointnet2_utils.py:316-324)
-                v = f32x4{px[0], px[1], px[2], 0.f};
-            }
-        }
-        bx[ct] = v;
-    }
-    const int feat_groups = a.c_prev >> 4;
-    const int wid_u = __builtin_amdgcn_readfirstlane(wid);   // wave-uniform tile ids -> SGPR offsets
+    const int KG = a.kg[L], NT = a.nt[L];
     const int voff = lane * 16;
+    const int tpc = a.ns >> 4;
+    const __amdgpu_buffer_rsrc_t W = make_rsrc(a.w[L], (uint32_t)(NT * KG) * 1024u);
+    const f32x4* in_lds = (L == 1) ? lds : lds + a.buf1_off;   // L>=1 reads buffer (L-1)&1
+    f32x4* out_lds = (L == 0) ? lds : lds + a.buf1_off;         // L<last writes buffer L&1
+    const bool last = (L == a.nlayers - 1);
+    const int feat_groups = a.c_prev >> 4;
 
-    for (int L = 0; L < a.nlayers; ++L) {
-        const int KG = a.kg[L], NT = a.nt[L];
-        const __amdgpu_buffer_rsrc_t W = make_rsrc(a.w[L], (uint32_t)(NT * KG) * 1024u);
-        const f32x4* in_lds = (L == 1) ? lds : lds + a.buf1_off;   // L>=1 reads buffer (L-1)&1
-        f32x4* out_lds = (L == 0) ? lds : lds + a.buf1_off;         // L<last writes buffer L&1
-        const bool last = (L == a.nlayers - 1);
-        for (int T0 = wid_u * TC; T0 < NT; T0 += 4 * TC) {
-            f32x4 acc[TC][CT];
+    // layer 0: per-lane gathered neighbour of each of this wave's column tiles + xyz fragment
+    int pi[CTW];
+    bool valid[CTW];
+    f32x4 bx[CTW];
+    if (L == 0) {
+#pragma unroll
+        for (int c = 0; c < CTW; ++c) {
+            const int col = col0 + (cbase + c) * 16 + nn;
+            valid[c] = col < a.cols;
+            const int m = col / a.ns, s = col - m * a.ns;
+            int p = 0;
+            if (valid[c]) p = a.nbr ? a.nbr[((size_t)b * a.m + m) * a.ns + s] : s;
+            pi[c] = p;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (valid[c] && q == 0) {
+                const float* px = a.xyz_prev + ((size_t)b * a.n_prev + p) * 3;
+                if (a.cent) {  // grouped_xyz -= new_xyz (pointnet2_utils.py:281-282)
+                    const float* cc = a.cent + ((size_t)b * a.m + m) * 3;
+                    v = f32x4{fsub(px[0], cc[0]), fsub(px[1], cc[1]), fsub(px[2], cc[2]), 0.f};
+                } else {       // GroupAll keeps raw xyz (pointnet2_utils.py:316-324)
+                    v = f32x4{px[0], px[1], px[2], 0.f};
+                }
+            }
+            bx[c] = v;
+        }
+    }
+    for (int T0 = wt * TC; T0 < NT; T0 += WT * TC) {
+        f32x4 acc[TC][CTW];
+#pragma unroll
+        for (int t = 0; t < TC; ++t)
+#pragma unroll
+            for (int c = 0; c < CTW; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // operand fetch for k-group g: A = packed weights (buffer load, SGPR offset), B = the
+        // gathered neighbour features (layer 0) or the previous layer in LDS
+        auto fetch = [&](int g, f32x4 (&af)[TC], f32x4 (&bf)[CTW]) {
 #pragma unroll
             for (int t = 0; t < TC; ++t)
+                af[t] = (T0 + t < NT) ? ldbuf4(W, voff, ((T0 + t) * KG + g) * 1024) : f32x4{0.f, 0.f, 0.f, 0.f};
+            if (L == 0) {
+                if (g < feat_groups) {
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-            // operand fetch for k-group g: A = packed weights (buffer load, SGPR offset), B = the
-            // gathered neighbour features (layer 0) or the previous layer in LDS
-            auto fetch = [&](int g, f32x4 (&af)[TC], f32x4 (&bf)[CT]) {
+                    for (int c = 0; c < CTW; ++c)
+                        bf[c] = valid[c] ? ld4(a.feat_prev + ((size_t)b * a.n_prev + pi[c]) * a.c_prev + 16 * g + 4 * q)
+                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+                } else {
+#pragma unroll
+                    for (int c = 0; c < CTW; ++c) bf[c] = bx[c];
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < CTW; ++c) bf[c] = in_lds[(g * CT + cbase + c) * 64 + lane];
+            }
+        };
+        // k-step outermost so consecutive MFMAs use different accumulators
+        auto compute = [&](const f32x4 (&af)[TC], const f32x4 (&bf)[CTW]) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int t = 0; t < TC; ++t)
-                    af[t] = (T0 + t < NT) ? ldbuf4(W, voff, ((T0 + t) * KG + g) * 1024) : f32x4{0.f, 0.f, 0.f, 0.f};
-                if (L == 0) {
-                    if (g < feat_groups) {
 #pragma unroll
-                        for (int ct = 0; ct < CT; ++ct)
-                            bf[ct] = valid[ct] ? ld4(a.feat_prev + ((size_t)b * a.n_prev + pi[ct]) * a.c_prev +
-                                                     16 * g + 4 * q)
-                                               : f32x4{0.f, 0.f, 0.f, 0.f};
-                    } else {
+                    for (int c = 0; c < CTW; ++c) acc[t][c] = mfma4(af[t][j], bf[c][j], acc[t][c]);
+        };
+        // two-slot ping-pong: the operands of k-group g+1 are in flight while g computes;
+        // sched_barrier keeps the compiler from sinking the loads back next to their MFMAs
+        f32x4 aA[TC], bA[CTW], aB[TC], bB[CTW];
+        fetch(0, aA, bA);
+        for (int g = 0; g < KG; g += 2) {
+            if (g + 1 < KG) fetch(g + 1, aB, bB);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(aA, bA);
+            if (g + 2 < KG) fetch(g + 2, aA, bA);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g + 1 < KG) compute(aB, bB);
+        }
 #pragma unroll
-                        for (int ct = 0; ct < CT; ++ct) bf[ct] = bx[ct];
+        for (int t = 0; t < TC; ++t) {
+            const int T = T0 + t;
+            if (T >= NT) continue;
+            const f32x4 bias = ld4(a.bias[L] + 16 * T + 4 * q);
+            if (!last) {
+#pragma unroll
+                for (int c = 0; c < CTW; ++c) out_lds[(T * CT + cbase + c) * 64 + lane] = relu4(acc[t][c] + bias);
+            } else {
+                // max over nsample: across the centroid's SPAN column tiles, then 16 lanes
+#pragma unroll
+                for (int cb = 0; cb < CTW; cb += SPAN) {
+                    f32x4 v = relu4(acc[t][cb] + bias);
+#pragma unroll
+                    for (int u = 1; u < SPAN; ++u) {
+                        const f32x4 w2 = relu4(acc[t][cb + u] + bias);
+                        v = f32x4{fmaxf(v.x, w2.x), fmaxf(v.y, w2.y), fmaxf(v.z, w2.z), fmaxf(v.w, w2.w)};
                     }
-                } else {
 #pragma unroll
-                    for (int ct = 0; ct < CT; ++ct) bf[ct] = in_lds[(g * CT + ct) * 64 + lane];
-                }
-            };
-            // k-step outermost so consecutive MFMAs use different accumulators
-            auto compute = [&](const f32x4 (&af)[TC], const f32x4 (&bf)[CT]) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int t = 0; t < TC; ++t)
-#pragma unroll
-                        for (int ct = 0; ct < CT; ++ct) acc[t][ct] = mfma4(af[t][j], bf[ct][j], acc[t][ct]);
-            };
-            // two-slot ping-pong: the operands of k-group g+1 are in flight while g computes;
-            // sched_barrier keeps the compiler from sinking the loads back next to their MFMAs
-            f32x4 aA[TC], bA[CT], aB[TC], bB[CT];
-            fetch(0, aA, bA);
-            for (int g = 0; g < KG; g += 2) {
-                if (g + 1 < KG) fetch(g + 1, aB, bB);
-                __builtin_amdgcn_sched_barrier(0);
-                compute(aA, bA);
-                if (g + 2 < KG) fetch(g + 2, aA, bA);
-                __builtin_amdgcn_sched_barrier(0);
-                if (g + 1 < KG) compute(aB, bB);
-            }
-#pragma unroll
-            for (int t = 0; t < TC; ++t) {
-                const int T = T0 + t;
-                if (T >= NT) continue;
-                const f32x4 bias = ld4(a.bias[L] + 16 * T + 4 * q);
-                if (!last) {
-#pragma unroll
-                    for (int ct = 0; ct < CT; ++ct) out_lds[(T * CT + ct) * 64 + lane] = relu4(acc[t][ct] + bias);
-                } else {
-                    // max over nsample: across the centroid's SPAN column tiles, then 16 lanes
-#pragma unroll
-                    for (int cb = 0; cb < CT; cb += SPAN) {
-                        f32x4 v = relu4(acc[t][cb] + bias);
-#pragma unroll
-                        for (int u = 1; u < SPAN; ++u) {
-                            const f32x4 w2 = relu4(acc[t][cb + u] + bias);
-                            v = f32x4{fmaxf(v.x, w2.x), fmaxf(v.y, w2.y), fmaxf(v.z, w2.z), fmaxf(v.w, w2.w)};
-                        }
-#pragma unroll
-                        for (int off = 8; off >= 1; off >>= 1) {
-                            v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
-                            v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
-                            v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
-                            v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
-                        }
-                        const int colc = col0 + cb * 16;
-                        if (nn == 0 && colc < a.cols) {
-                            const int m = colc / a.ns;
-                            float* o = a.out + ((size_t)b * a.m + m) * a.c_out_total + a.out_off + 16 * T + 4 * q;
-                            if (tpc <= CT) {
-                                st4(o, v);
-                            } else {  // centroid split over workgroups: post-ReLU values are >= 0
-                                unsigned int* u = reinterpret_cast<unsigned int*>(o);
-                                atomicMax(u + 0, __float_as_uint(v.x));
-                                atomicMax(u + 1, __float_as_uint(v.y));
-                                atomicMax(u + 2, __float_as_uint(v.z));
-                                atomicMax(u + 3, __float_as_uint(v.w));
-                            }
+                    for (int off = 8; off >= 1; off >>= 1) {
+                        v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
+                        v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
+                        v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
+                        v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
+                    }
+                    const int colc = col0 + (cbase + cb) * 16;
+                    if (nn == 0 && colc < a.cols) {
+                        const int m = colc / a.ns;
+                        float* o = a.out + ((size_t)b * a.m + m) * a.c_out_total + a.out_off + 16 * T + 4 * q;
+                        if (tpc <= SPAN) {
+                            st4(o, v);
+                        } else {  // centroid split over workgroups: post-ReLU values are >= 0
+                            unsigned int* u = reinterpret_cast<unsigned int*>(o);
+                            atomicMax(u + 0, __float_as_uint(v.x));
+                            atomicMax(u + 1, __float_as_uint(v.y));
+                            atomicMax(u + 2, __float_as_uint(v.z));
+                            atomicMax(u + 3, __float_as_uint(v.w));
                         }
                     }
                 }
             }
+        }
+    }
+}
+
+template <int CT, int TC, int SPAN>
+__global__ __launch_bounds__(SA_THREADS, 2) void sa_branch_kernel(SAArgs a) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    const int col0 = blockIdx.x * CT * 16;
+    for (int L = 0; L < a.nlayers; ++L) {
+        // waves over columns: 4 / (output tiles this layer can feed at TC per wave), kept >= the
+        // pooling span on the last layer
+        const int nt = a.nt[L];
+        int wc = nt >= 4 * TC ? 1 : (nt > TC ? 2 : 4);
+        if (wc > CT) wc = CT;
+        if (L == a.nlayers - 1)
+            while (wc > 1 && CT / wc < SPAN) wc >>= 1;
+        const int wt = wid / wc, WT = 4 / wc;
+        if (wc == 1) {
+            sa_layer<CT, CT, TC, SPAN>(a, lds, L, b, col0, 0, wt, WT);
+        } else if (wc == 2) {
+            if constexpr (CT >= 2 && CT / 2 >= 1) sa_layer<CT, CT / 2, TC, (SPAN <= CT / 2 ? SPAN : 1)>(
+                a, lds, L, b, col0, (wid % 2) * (CT / 2), wt, WT);
+        } else {
+            if constexpr (CT >= 4) sa_layer<CT, CT / 4, TC, 1>(a, lds, L, b, col0, (wid % 4) * (CT / 4), wt, WT);
         }
         __syncthreads();
     }

@@ -81,13 +81,37 @@ __device__ __forceinline__ unsigned long long fps_pack(float d2, uint32_t key) {
 
 constexpr int FPS_THREADS = 256;
 
-// One FPS run over `n` points held in LDS (s_xyz, xyz interleaved). Writes m indices to
-// out_idx (global, may be null) and the selected coordinates to s_out (LDS, may be null) and
-// out_xyz (global, may be null). All 256 threads must call it.
+// Wave-wide max of a 64-bit key with DPP row operations (quad perms, half/full row mirror,
+// row_bcast15/31) instead of 6 ds_bpermute shuffle rounds; the result is read from lane 63.
+#define GP_DPP_MAX_STEP(CTRL, ROWMASK)                                                          \
+    {                                                                                           \
+        const uint32_t ohi = (uint32_t)__builtin_amdgcn_update_dpp((int)hi, (int)hi, CTRL, ROWMASK, 0xF, false); \
+        const uint32_t olo = (uint32_t)__builtin_amdgcn_update_dpp((int)lo, (int)lo, CTRL, ROWMASK, 0xF, false); \
+        const bool take = (ohi > hi) || (ohi == hi && olo > lo);                                 \
+        hi = take ? ohi : hi;                                                                   \
+        lo = take ? olo : lo;                                                                   \
+    }
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+    uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    GP_DPP_MAX_STEP(0xB1, 0xF)   // quad_perm [1,0,3,2]
+    GP_DPP_MAX_STEP(0x4E, 0xF)   // quad_perm [2,3,0,1]
+    GP_DPP_MAX_STEP(0x141, 0xF)  // row_half_mirror
+    GP_DPP_MAX_STEP(0x140, 0xF)  // row_mirror
+    GP_DPP_MAX_STEP(0x142, 0xA)  // row_bcast:15 -> rows 1, 3
+    GP_DPP_MAX_STEP(0x143, 0xC)  // row_bcast:31 -> rows 2, 3
+    const uint32_t rhi = (uint32_t)__builtin_amdgcn_readlane((int)hi, 63);
+    const uint32_t rlo = (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+    return ((unsigned long long)rhi << 32) | rlo;
+}
+
+// One FPS run over `n` points held in LDS (s_xyz, xyz interleaved). Writes the m indices to
+// s_idx and the selected coordinates to s_out (both LDS; s_out may be null). Nothing touches
+// global memory inside the iteration loop, so the per-iteration barrier never waits on a store.
+// All 256 threads must call it.
 template <int PMAX>
 __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits,
-                        unsigned long long* s_red /* [2][4] */, int* out_idx, float* s_out,
-                        float* out_xyz) {
+                        unsigned long long* s_red /* [2][4] */, int* s_idx, float* s_out) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     float px[PMAX], py[PMAX], pz[PMAX], tmin[PMAX];
     uint32_t key[PMAX];
@@ -103,13 +127,8 @@ __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits,
     }
     int old = 0;
     if (m <= 0) return;
-    if (tid == 0) {
-        if (out_idx) out_idx[0] = 0;
-    }
-    if (tid < 3) {
-        if (s_out) s_out[tid] = s_xyz[tid];
-        if (out_xyz) out_xyz[tid] = s_xyz[tid];
-    }
+    if (tid == 0) s_idx[0] = 0;
+    if (tid < 3 && s_out) s_out[tid] = s_xyz[tid];
     for (int j = 1; j < m; ++j) {
         const float x1 = s_xyz[3 * old + 0], y1 = s_xyz[3 * old + 1], z1 = s_xyz[3 * old + 2];
         unsigned long long best = 0ull;
@@ -124,11 +143,7 @@ __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits,
                 best = c > best ? c : best;
             }
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const unsigned long long o = __shfl_xor(best, off, 64);
-            best = o > best ? o : best;
-        }
+        best = wave_max_u64(best);
         unsigned long long* red = s_red + (j & 1) * 4;
         if (lane == 0) red[wid] = best;
         __syncthreads();
@@ -136,12 +151,8 @@ __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits,
 #pragma unroll
         for (int w = 1; w < FPS_THREADS / 64; ++w) b = red[w] > b ? red[w] : b;
         old = fps_key_to_k(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull), nb, jbits);
-        if (tid == 0 && out_idx) out_idx[j] = old;
-        if (tid < 3) {
-            const float v = s_xyz[3 * old + tid];
-            if (s_out) s_out[3 * j + tid] = v;
-            if (out_xyz) out_xyz[3 * j + tid] = v;
-        }
+        if (tid == 0) s_idx[j] = old;
+        if (tid < 3 && s_out) s_out[3 * j + tid] = s_xyz[3 * old + tid];
     }
 }
 
@@ -153,14 +164,21 @@ __global__ __launch_bounds__(FPS_THREADS) void fps_kernel(const float* __restric
     float* s_xyz = reinterpret_cast<float*>(smem + 64);
     const int b = blockIdx.x;
     const float* src = xyz + (size_t)b * n * 3;
+    int* s_idx = reinterpret_cast<int*>(s_xyz + 3 * n);
     for (int i = threadIdx.x; i < 3 * n; i += FPS_THREADS) s_xyz[i] = src[i];
     __syncthreads();
-    fps_run<PMAX>(s_xyz, n, m, nb, jbits, s_red, idx + (size_t)b * m, nullptr, nullptr);
+    fps_run<PMAX>(s_xyz, n, m, nb, jbits, s_red, s_idx, nullptr);
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += FPS_THREADS) idx[(size_t)b * m + i] = s_idx[i];
 }
 
 static int launch_fps(const float* xyz, int b, int n, int m, int* idx, hipStream_t st) {
     const FpsGeom g = fps_geom(n);
-    const size_t lds = 64 + sizeof(float) * 3 * (size_t)n;
+    const size_t lds = 64 + sizeof(float) * 3 * (size_t)n + sizeof(int) * (size_t)m;
+    if (lds > 160 * 1024) {
+        gp_set_error("furthest_point_sampling: n=%d, m=%d exceed the LDS budget", n, m);
+        return GP_ERR_UNSUPPORTED;
+    }
     const int p = (n + FPS_THREADS - 1) / FPS_THREADS;
 #define GP_FPS_CASE(PM)                                                                      \
     if (p <= PM) {                                                                           \
@@ -202,6 +220,7 @@ __global__ __launch_bounds__(FPS_THREADS) void fps_chain_kernel(const float* __r
     unsigned long long* s_red = reinterpret_cast<unsigned long long*>(smem);
     float* bufA = reinterpret_cast<float*>(smem + 64);
     float* bufB = bufA + 3 * a.n[0];
+    int* s_idx = reinterpret_cast<int*>(bufB + 3 * a.m[0]);
     const int b = blockIdx.x;
     const float* src = xyz + (size_t)b * a.n[0] * 3;
     for (int i = threadIdx.x; i < 3 * a.n[0]; i += FPS_THREADS) bufA[i] = src[i];
@@ -209,8 +228,12 @@ __global__ __launch_bounds__(FPS_THREADS) void fps_chain_kernel(const float* __r
     float* cur = bufA;
     float* nxt = bufB;
     for (int l = 0; l < a.nlev; ++l) {
-        fps_run<PMAX>(cur, a.n[l], a.m[l], a.nb[l], a.jbits[l], s_red, a.idx[l] + (size_t)b * a.m[l],
-                      nxt, a.nxyz[l] + (size_t)b * a.m[l] * 3);
+        fps_run<PMAX>(cur, a.n[l], a.m[l], a.nb[l], a.jbits[l], s_red, s_idx, nxt);
+        __syncthreads();
+        int* gi = a.idx[l] + (size_t)b * a.m[l];
+        float* gx = a.nxyz[l] + (size_t)b * a.m[l] * 3;
+        for (int i = threadIdx.x; i < a.m[l]; i += FPS_THREADS) gi[i] = s_idx[i];
+        for (int i = threadIdx.x; i < 3 * a.m[l]; i += FPS_THREADS) gx[i] = nxt[i];
         __syncthreads();
         float* t = cur;
         cur = nxt;
@@ -231,7 +254,7 @@ int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const i
         a.idx[l] = idx[l];
         a.nxyz[l] = nxyz[l];
     }
-    const size_t lds = 64 + sizeof(float) * 3 * ((size_t)n[0] + (size_t)m[0]);
+    const size_t lds = 64 + sizeof(float) * 3 * ((size_t)n[0] + (size_t)m[0]) + sizeof(int) * (size_t)m[0];
     const int p = (n[0] + FPS_THREADS - 1) / FPS_THREADS;
 #define GP_CHAIN_CASE(PM)                                                                       \
     if (p <= PM) {                                                                              \

@@ -73,10 +73,12 @@ __device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, He
 // come from LDS. Loads are raw buffer loads: the tile/k-group offset is a wave-uniform SGPR
 // (soffset) and the only per-lane address is lane*16 (voffset), so the fully unrolled ring needs
 // no 64-bit address registers. Every ring index is a compile-time constant.
-template <int G, int TT, int NT, int KG, int D>
+// Steps G..GEND-1 of the pipelined stream (step G issues k-group G's loads and computes k-group
+// G-D). Steps 0..D-1 only prime the ring, so they can be issued early (before a barrier).
+template <int G, int GEND, int TT, int NT, int KG, int D>
 __device__ __forceinline__ void stream_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f32x4* __restrict__ B,
                                             int lane, int voff, f32x4 (&ring)[D + 1][TT], f32x4 (&acc)[TT][NT]) {
-    if constexpr (G < KG + D) {
+    if constexpr (G < GEND) {
         if constexpr (G < KG) {
 #pragma unroll
             for (int t = 0; t < TT; ++t) ring[G % (D + 1)][t] = ldbuf4(W, voff, (T[t] * KG + G) * 1024);
@@ -99,7 +101,7 @@ __device__ __forceinline__ void stream_step(__amdgpu_buffer_rsrc_t W, const int 
                     for (int ct = 0; ct < NT; ++ct)
                         acc[t][ct] = mfma4(ring[GG % (D + 1)][t][j], bf[ct][j], acc[t][ct]);
         }
-        stream_step<G + 1, TT, NT, KG, D>(W, T, B, lane, voff, ring, acc);
+        stream_step<G + 1, GEND, TT, NT, KG, D>(W, T, B, lane, voff, ring, acc);
     }
 }
 
@@ -113,7 +115,7 @@ template <int TT, int NT, int KG, int D>
 __device__ __forceinline__ void stream_layer(__amdgpu_buffer_rsrc_t W, const int (&T)[TT],
                                              const f32x4* __restrict__ B, int lane, f32x4 (&acc)[TT][NT]) {
     f32x4 ring[D + 1][TT];
-    stream_step<0, TT, NT, KG, D>(W, T, B, lane, lane * 16, ring, acc);
+    stream_step<0, KG + D, TT, NT, KG, D>(W, T, B, lane, lane * 16, ring, acc);
 }
 
 // Computes f (NT*16 cols x 9) = heads(x) into sm.f for the candidates of this workgroup.
@@ -125,6 +127,25 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
     const int q = lane >> 4, n = lane & 15;
+    const int voff = lane * 16;
+    const __amdgpu_buffer_rsrc_t W2 = make_rsrc(w.pe2_w, HID * HID * 4);
+    const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_w, 3 * HID * HID * 4);
+    constexpr int D2 = 3, DH = HEAD_PREFETCH;
+    int T2[TPW], TH[3 * TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) T2[t] = wid * TPW + t;
+#pragma unroll
+    for (int h = 0; h < 3; ++h)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) TH[h * TPW + t] = h * 16 + wid * TPW + t;
+    f32x4 acc2[TPW][NT];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) acc2[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 ring2[D2 + 1][TPW];
+    // prime pose_encoder.2's weight ring before pose_encoder.0 (no B operand read yet)
+    stream_step<0, D2, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
     // ---- pose_encoder.0 (9 -> 256), one k-group
     {
         f32x4 bf[NT];
@@ -142,39 +163,29 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
     }
     __syncthreads();
     // ---- pose_encoder.2 (256 -> 256): TPW output tiles per wave
-    {
-        f32x4 acc[TPW][NT];
-        int Ts[TPW];
+    stream_step<D2, KG_HID + D2, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
+    // ---- head layer 1 prologue, issued before the barrier: accumulator init with the hoisted
+    //      pts/t blocks, and the first DH k-groups of the pose-block weights
+    f32x4 acc[3 * TPW][NT];
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            Ts[t] = wid * TPW + t;
+    for (int i = 0; i < 3 * TPW; ++i) {
+        const int T = TH[i];
+        const f32x4 tp = ld4(tproj + 16 * T + 4 * q);
 #pragma unroll
-            for (int ct = 0; ct < NT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        stream_layer<TPW, NT, KG_HID, 3>(make_rsrc(w.pe2_w, HID * HID * 4), Ts, sm.act1, lane, acc);
+        for (int ct = 0; ct < NT; ++ct)
+            acc[i][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q) + tp;
+    }
+    f32x4 ringh[DH + 1][3 * TPW];
+    stream_step<0, DH, 3 * TPW, NT, KG_HID, DH>(WH, TH, sm.act2, lane, voff, ringh, acc);
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            const f32x4 bias = ld4(&sm.pe2b[16 * Ts[t] + 4 * q]);
+    for (int t = 0; t < TPW; ++t) {
+        const f32x4 bias = ld4(&sm.pe2b[16 * T2[t] + 4 * q]);
 #pragma unroll
-            for (int ct = 0; ct < NT; ++ct) sm.act2[(Ts[t] * NT + ct) * 64 + lane] = relu4(acc[t][ct] + bias);
-        }
+        for (int ct = 0; ct < NT; ++ct) sm.act2[(T2[t] * NT + ct) * 64 + lane] = relu4(acc2[t][ct] + bias);
     }
     __syncthreads();
-    // ---- head layer 1 (pose block 256 -> 3x256) + hoisted pts/t blocks; 3*TPW output tiles per wave
-    f32x4 acc[3 * TPW][NT];
-    int Ts[3 * TPW];
-#pragma unroll
-    for (int h = 0; h < 3; ++h)
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            const int T = h * 16 + wid * TPW + t;
-            Ts[h * TPW + t] = T;
-            const f32x4 tp = ld4(tproj + 16 * T + 4 * q);
-#pragma unroll
-            for (int ct = 0; ct < NT; ++ct)
-                acc[h * TPW + t][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q) + tp;
-        }
-    stream_layer<3 * TPW, NT, KG_HID, HEAD_PREFETCH>(make_rsrc(w.h1p_w, 3 * HID * HID * 4), Ts, sm.act2, lane, acc);
+    // ---- head layer 1 (pose block 256 -> 3x256): 3*TPW output tiles per wave
+    stream_step<DH, KG_HID + DH, 3 * TPW, NT, KG_HID, DH>(WH, TH, sm.act2, lane, voff, ringh, acc);
     // ---- ReLU -> head layer 2 (block diagonal 3 x (256 -> 3)) partial dot products
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
