@@ -1,33 +1,47 @@
-"""Ranking and aggregation of pose candidates (runner side of the path).
+"""Ranking and aggregation of pose candidates (runner side of the path, SURVEY §8f).
 
-* ``sort_poses_by_energy``      <- networks/reward.py:131-155 (rotation part ordered by the
-  rotation energy, translation part by the translation energy, both descending)
-* ``average_quaternion_batch``  <- utils/misc.py:295-317 (w>0 orientation, weighted outer
-  products, top eigenvector, w>0 orientation of the result)
-* ``aggregate_pose``            <- runners/evaluation_single.py:160-219 (top retain_ratio*K,
+* ``sort_poses_by_energy``  <- networks/reward.py:131-155 (rotation part ordered by the rotation
+  energy, translation part by the translation energy, both descending)
+* ``aggregate_pose``        <- runners/evaluation_single.py:160-219 (top retain_ratio*K, quaternion
   average, optional DBSCAN re-average of the largest cluster, mean translation, 4x4)
-* ``dbscan_labels``             restates sklearn.cluster.DBSCAN(eps, min_samples) with its
-  default Euclidean metric applied to the ROWS of the quaternion distance matrix:
-  core points have >= min_samples neighbours within eps (self included), clusters grow by
-  depth-first expansion from core points in index order.
 
-Device tensors stay on device; the per-object DBSCAN labelling (<= 20 points each) runs on the
-host, as in the reference (ranked "next" for a device kernel in SURVEY §8f).
+Both run as ONE launch of ``gp_rank_aggregate`` (csrc/gp_aggregate.hip) over the whole batch; the
+reference does a per-object host loop with .cpu().numpy() round trips and sklearn DBSCAN. The torch
+rotation helpers below serve ``PoseNet.pred_func(return_average_res=True)`` (posenet_agent.py:560),
+which the reference also runs as torch ops on device.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Tuple
 
-import numpy as np
 import torch
+
+from . import _lib
+from .device import require_device_tensor, stream_handle
+
+
+def _rank_aggregate(poses: torch.Tensor, energy: torch.Tensor, retain: int, clustering: int, eps: float,
+                    min_samples: int, want_sorted: bool):
+    poses = require_device_tensor(poses, "pred_pose")
+    energy = require_device_tensor(energy, "pred_energy")
+    bs, K = poses.shape[:2]
+    if tuple(poses.shape) != (bs, K, 9) or tuple(energy.shape) != (bs, K, 2):
+        raise ValueError(f"pred_pose {tuple(poses.shape)} / pred_energy {tuple(energy.shape)}: need (B,K,9)/(B,K,2)")
+    agg = torch.empty((bs, 4, 4), dtype=torch.float32, device=poses.device)
+    sp = torch.empty_like(poses) if want_sorted else None
+    se = torch.empty_like(energy) if want_sorted else None
+    vp = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else None)  # noqa: E731
+    _lib.check(_lib.load().gp_rank_aggregate(vp(poses), vp(energy), bs, K, retain, int(bool(clustering)),
+                                             float(eps), int(min_samples), vp(agg), vp(sp), vp(se),
+                                             ctypes.c_void_p(stream_handle(poses.device))), "rank_aggregate")
+    return agg, sp, se
 
 
 def sort_poses_by_energy(poses: torch.Tensor, energy: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    sorted_energy, order = torch.sort(energy, descending=True, dim=1, stable=True)
-    o_rot, o_tr = order[..., 0], order[..., 1]
-    sp = torch.gather(poses, 1, o_rot.unsqueeze(-1).expand(-1, -1, poses.shape[-1])).clone()
-    sp[..., -3:] = torch.gather(poses, 1, o_tr.unsqueeze(-1).expand(-1, -1, poses.shape[-1]))[..., -3:]
-    return sp, sorted_energy
+    """-> (sorted_pose (B,K,9), sorted_energy (B,K,2)); ties keep the lower candidate index."""
+    _, sp, se = _rank_aggregate(poses.to(torch.float32), energy.to(torch.float32), 1, 0, 0.0, 1, True)
+    return sp, se
 
 
 def average_quaternion_batch(Q: torch.Tensor, weights: torch.Tensor = None) -> torch.Tensor:
@@ -77,51 +91,13 @@ def quaternion_to_matrix(q: torch.Tensor) -> torch.Tensor:
     return o.reshape(q.shape[:-1] + (3, 3))
 
 
-def dbscan_labels(X: np.ndarray, eps: float, min_samples: int) -> np.ndarray:
-    """sklearn DBSCAN (metric='euclidean', algorithm brute) on the rows of X."""
-    X = np.asarray(X, np.float64)
-    n = X.shape[0]
-    d = np.sqrt(np.maximum(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1), 0.0))
-    nbrs = [np.nonzero(d[i] <= eps)[0] for i in range(n)]
-    core = np.array([len(v) >= min_samples for v in nbrs])
-    labels = np.full(n, -1, np.int64)
-    label = 0
-    for i in range(n):
-        if labels[i] != -1 or not core[i]:
-            continue
-        stack = [i]
-        while stack:
-            p = stack.pop()
-            if labels[p] != -1:
-                continue
-            labels[p] = label
-            if core[p]:
-                stack.extend(int(j) for j in nbrs[p][::-1] if labels[j] == -1)
-        label += 1
-    return labels
-
-
 def aggregate_pose(pred_pose: torch.Tensor, pred_energy: torch.Tensor, retain_ratio: float = 0.4,
                    clustering: int = 1, clustering_eps: float = 0.05, clustering_minpts: float = 0.1667):
-    """evaluation_single.py:160-219 for one batch: -> (B, 4, 4) float32 on pred_pose's device."""
-    bs, K = pred_pose.shape[:2]
-    pred_pose = pred_pose.to(torch.float32)
-    sp, _ = sort_poses_by_energy(pred_pose, pred_energy.to(pred_pose.device))
+    """evaluation_single.py:160-219 for one batch -> (B, 4, 4) float32 on pred_pose's device."""
+    K = pred_pose.shape[1]
     keep = int(K * retain_ratio)
-    good = sp[:, :keep, :]
-    q = matrix_to_quaternion(rot6_to_matrix(good[:, :, :6].reshape(bs * keep, -1))).reshape(bs, keep, 4)
-    qa = average_quaternion_batch(q)
-    if clustering:
-        D = 1 - torch.sum(q.unsqueeze(1) * q.unsqueeze(2), dim=3) ** 2    # (bs, keep, keep)
-        Dh = D.cpu().numpy()
-        for j in range(bs):
-            labels = dbscan_labels(Dh[j], clustering_eps, int(clustering_minpts * keep))
-            if np.any(labels >= 0):
-                best = int(np.argmax(np.bincount(labels[labels >= 0])))
-                sel = torch.from_numpy(labels == best).to(q.device)
-                qa[j] = average_quaternion_batch(q[j, sel].unsqueeze(0))[0]
-    out = torch.zeros(bs, 4, 4, device=pred_pose.device)
-    out[:, 3, 3] = 1
-    out[:, :3, :3] = quaternion_to_matrix(qa)
-    out[:, :3, 3] = torch.mean(good[:, :, -3:], dim=1)
-    return out
+    if keep < 1:
+        raise ValueError(f"retain_ratio {retain_ratio} keeps no candidate of K={K}")
+    agg, _, _ = _rank_aggregate(pred_pose.to(torch.float32), pred_energy.to(torch.float32), keep, clustering,
+                                clustering_eps, int(clustering_minpts * keep), False)
+    return agg

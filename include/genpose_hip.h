@@ -145,6 +145,19 @@ typedef struct {
 int gp_scale_forward(const gp_scale_weights *w, const float *axes, const float *pts_feat, int b,
                      float *length, hipStream_t stream);
 
+/* ===================================================================== ranking / aggregation
+ * sort_poses_by_energy (networks/reward.py:131-155) + aggregate_pose
+ * (runners/evaluation_single.py:160-219) for b objects of k candidates, one launch.
+ * poses (b,k,9) fp32 [rot6 | trans], energy (b,k,2) fp32 [rot, trans] -> aggregated (b,4,4).
+ * retain = int(k * retain_ratio) (1..min(k,128)); clustering != 0 runs DBSCAN(eps, min_samples)
+ * on the rows of D = 1 - <q_i,q_j>^2 of the retained quaternions and re-averages the largest
+ * cluster (min_samples = int(clustering_minpts * retain) as the reference passes it).
+ * sorted_pose (b,k,9) / sorted_energy (b,k,2) may be NULL; when given they receive the
+ * reference's sort_poses_by_energy outputs (descending, ties by lower index). */
+int gp_rank_aggregate(const float *poses, const float *energy, int b, int k, int retain,
+                      int clustering, float eps, int min_samples, float *aggregated,
+                      float *sorted_pose, float *sorted_energy, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

