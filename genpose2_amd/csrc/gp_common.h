@@ -101,11 +101,15 @@ __device__ __forceinline__ float u01(uint32_t v) {  // (0,1]
     return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f);
 }
 
-// 4 standard normals for (seed, stream, row, block).
+// 4 standard normals for (seed, stream, row, block): Box-Muller on the hardware transcendentals
+// (v_log_f32 = log2, v_sin/v_cos_f32 take revolutions, so sin(2*pi*u) needs no range reduction).
 __device__ __forceinline__ f32x4 philox_normal4(uint64_t seed, uint32_t stream, uint32_t row,
                                                 uint32_t blk) {
     u32x4 r = philox4x32_10(u32x4{row, blk, stream, 0x5EEDu}, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const float r0 = sqrtf(-2.0f * logf(u01(r.x))), r1 = sqrtf(-2.0f * logf(u01(r.z)));
-    const float a0 = 6.2831853071795864f * u01(r.y), a1 = 6.2831853071795864f * u01(r.w);
-    return f32x4{r0 * cosf(a0), r0 * sinf(a0), r1 * cosf(a1), r1 * sinf(a1)};
+    constexpr float kM2Ln2 = -1.3862943611198906f;   // -2 ln 2
+    const float r0 = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.x)));
+    const float r1 = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.z)));
+    const float a0 = u01(r.y), a1 = u01(r.w);
+    return f32x4{r0 * __builtin_amdgcn_cosf(a0), r0 * __builtin_amdgcn_sinf(a0), r1 * __builtin_amdgcn_cosf(a1),
+                 r1 * __builtin_amdgcn_sinf(a1)};
 }

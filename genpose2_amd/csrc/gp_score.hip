@@ -37,6 +37,22 @@ constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
 #define HEAD_PREFETCH 2          // k-groups of head-layer-1 weights kept in flight
 #endif
 
+// Phase timestamps for tuning builds only (make EXTRA=-DPC_TRACE; read by scripts/pc_trace.py).
+#ifdef PC_TRACE
+__device__ unsigned long long g_pc_trace[2 * 256 * 8 * 16];
+#define PC_MARK(k)                                                                                       \
+    do {                                                                                                 \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)                                                 \
+            g_pc_trace[((trace_slot * 256 + blockIdx.x) * 8 + (threadIdx.x >> 6)) * 16 + (k)] =          \
+                __builtin_amdgcn_s_memtime();                                                            \
+    } while (0)
+extern "C" int gp_debug_pc_trace(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pc_trace), sizeof(g_pc_trace)) == hipSuccess ? 0 : -1;
+}
+#else
+#define PC_MARK(k) ((void)trace_slot)
+#endif
+
 // ============================================================================ shared head trunk
 // NT = column tiles (16 candidates each) per workgroup.
 template <int NT, int WV>
@@ -44,8 +60,9 @@ struct HeadSmem {
     float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
     f32x4 act1[KG_HID * NT * 64];      // pose_encoder.0 output, accumulator-native [g][ct][lane]
     f32x4 act2[KG_HID * NT * 64];      // pose_encoder.2 output
-    float red[WV][9][NT * 16];         // per-wave head-layer-2 partials
-    float f[NT * 16][9];               // head output before the sigma division
+    float red[WV][9][NT * 16];         // per-wave head-layer-2 partials (head output: head_out())
+    float xu[NT * 16 * 9];             // PC update inputs: state x and score s of this tile's rows
+    float su[NT * 16 * 9];
     float noise[NT * 16][2][12];       // PC corrector / predictor draws of this step
     float scratch[WV * 64];
     // small per-launch weights staged once per workgroup (their loads overlap the PC update)
@@ -55,16 +72,34 @@ struct HeadSmem {
     float h2b[12];
 };
 
-template <int NT, int WV>
+// Threads [FIRST, WV*64) copy the small weights into LDS.
+template <int NT, int WV, int FIRST = 0>
 __device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, HeadSmem<NT, WV>& sm) {
-    constexpr int NTH = WV * 64;
-    for (int i = threadIdx.x; i < 16 * 64; i += NTH) sm.pe0w[i] = ld4(w.pe0_w + (size_t)i * 4);
-    for (int i = threadIdx.x; i < HID; i += NTH) {
+    constexpr int NTH = WV * 64 - FIRST;
+    const int t0 = (int)threadIdx.x - FIRST;
+    if (t0 < 0) return;
+    for (int i = t0; i < 16 * 64; i += NTH) sm.pe0w[i] = ld4(w.pe0_w + (size_t)i * 4);
+    for (int i = t0; i < HID; i += NTH) {
         sm.pe0b[i] = w.pe0_b[i];
         sm.pe2b[i] = w.pe2_b[i];
     }
-    for (int i = threadIdx.x; i < 9 * HID / 4; i += NTH) st4(&sm.h2w[i * 4], ld4(w.h2_w + (size_t)i * 4));
-    if (threadIdx.x < 9) sm.h2b[threadIdx.x] = w.h2_b[threadIdx.x];
+    for (int i = t0; i < 9 * HID / 4; i += NTH) st4(&sm.h2w[i * 4], ld4(w.h2_w + (size_t)i * 4));
+    if (t0 < 9) sm.h2b[t0] = w.h2_b[t0];
+}
+
+// Head output o of column c (valid after head_trunk): bias + the per-wave partials in wave order.
+template <int NT, int WV>
+__device__ __forceinline__ float head_out(const HeadSmem<NT, WV>& sm, int c, int o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int v = 0; v < WV; ++v) acc += sm.red[v][o][c];
+    return sm.h2b[o] + acc;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // acc[t][ct] += sum_g A(tile T[t], k-group g) . B(k-group g, column tile ct) over KG k-groups.
@@ -118,11 +153,14 @@ __device__ __forceinline__ void stream_layer(__amdgpu_buffer_rsrc_t W, const int
     stream_step<0, KG + D, TT, NT, KG, D>(W, T, B, lane, lane * 16, ring, acc);
 }
 
-// Computes f (NT*16 cols x 9) = heads(x) into sm.f for the candidates of this workgroup.
+// Computes the head outputs (read with head_out) for the candidates of this workgroup. Starts with
+// the workgroup barrier that publishes sm.xin, obj_of_col and the staged weights (callers write
+// them before the call without a barrier of their own; the first weight loads are issued before it).
 // `obj_of_col` maps column -> object row of pobj; `tproj` is the 768-vector of this time value.
 template <int NT, int WV>
 __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float* __restrict__ pobj,
-                           const float* __restrict__ tproj, const int* obj_of_col, HeadSmem<NT, WV>& sm) {
+                           const float* __restrict__ tproj, const int* obj_of_col, HeadSmem<NT, WV>& sm,
+                           int trace_slot = 0) {
     constexpr int TPW = 16 / WV;   // output tiles per wave and per 256-wide layer
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
@@ -146,6 +184,8 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
     f32x4 ring2[D2 + 1][TPW];
     // prime pose_encoder.2's weight ring before pose_encoder.0 (no B operand read yet)
     stream_step<0, D2, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
+    __syncthreads();
+    PC_MARK(1);
     // ---- pose_encoder.0 (9 -> 256), one k-group
     {
         f32x4 bf[NT];
@@ -162,10 +202,12 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
         }
     }
     __syncthreads();
+    PC_MARK(2);
     // ---- pose_encoder.2 (256 -> 256): TPW output tiles per wave
     stream_step<D2, KG_HID + D2, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
     // ---- head layer 1 prologue, issued before the barrier: accumulator init with the hoisted
     //      pts/t blocks, and the first DH k-groups of the pose-block weights
+    PC_MARK(3);
     f32x4 acc[3 * TPW][NT];
 #pragma unroll
     for (int i = 0; i < 3 * TPW; ++i) {
@@ -184,8 +226,10 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
         for (int ct = 0; ct < NT; ++ct) sm.act2[(T2[t] * NT + ct) * 64 + lane] = relu4(acc2[t][ct] + bias);
     }
     __syncthreads();
+    PC_MARK(4);
     // ---- head layer 1 (pose block 256 -> 3x256): 3*TPW output tiles per wave
     stream_step<DH, KG_HID + DH, 3 * TPW, NT, KG_HID, DH>(WH, TH, sm.act2, lane, voff, ringh, acc);
+    PC_MARK(5);
     // ---- ReLU -> head layer 2 (block diagonal 3 x (256 -> 3)) partial dot products
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
@@ -217,14 +261,7 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
         }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < NT * 16 * 9; e += WV * 64) {
-        const int c = e / 9, o = e - c * 9;
-        float acc2 = 0.f;
-#pragma unroll
-        for (int v = 0; v < WV; ++v) acc2 += sm.red[v][o][c];
-        sm.f[c][o] = sm.h2b[o] + acc2;
-    }
-    __syncthreads();
+    PC_MARK(6);
 }
 
 // ============================================================================ pose helpers
@@ -253,6 +290,26 @@ __device__ __forceinline__ void gram_schmidt6(T* v) {
     v[3] = c0 / n2;
     v[4] = c1 / n2;
     v[5] = c2 / n2;
+}
+
+// gram_schmidt6 spread over the four lanes of a row (lane part p: 0 -> v[0:3], 1 -> v[3:6],
+// 2 -> translation, untouched; 3 idle). Same operations and order as gram_schmidt6<float>.
+__device__ __forceinline__ void gram_schmidt6_quad(float* v, int p, int lane) {
+#pragma clang fp contract(off)
+    float n1 = sqrtf((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+    n1 = n1 > 1e-12f ? n1 : 1e-12f;
+    const float b0 = v[0] / n1, b1 = v[1] / n1, b2 = v[2] / n1;   // meaningful on p == 0
+    const int src = lane & ~3;
+    const float B0 = __shfl(b0, src, 64), B1 = __shfl(b1, src, 64), B2 = __shfl(b2, src, 64);
+    const float d = (B0 * v[0] + B1 * v[1]) + B2 * v[2];
+    float c0 = v[0] - d * B0, c1 = v[1] - d * B1, c2 = v[2] - d * B2;
+    float n2 = sqrtf((c0 * c0 + c1 * c1) + c2 * c2);
+    n2 = n2 > 1e-12f ? n2 : 1e-12f;
+    if (p == 0) {
+        v[0] = b0; v[1] = b1; v[2] = b2;
+    } else if (p == 1) {
+        v[0] = c0 / n2; v[1] = c1 / n2; v[2] = c2 / n2;
+    }
 }
 
 // matrix_to_quaternion (rotation_conversions.py:102-161) of R = [b1 b2 b1xb2] (columns), input
@@ -367,12 +424,11 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
         const int r = r0 + threadIdx.x;
         obj[threadIdx.x] = (r < rows ? r : rows - 1) / kper;
     }
-    __syncthreads();
     head_trunk<1, EVAL_WV>(w, pobj, tproj, obj, sm);
     if (MODE == 0) {
         if (threadIdx.x < 144) {
             const int c = threadIdx.x / 9, o = threadIdx.x - c * 9;
-            if (r0 + c < rows) out[(size_t)(r0 + c) * 9 + o] = fdiv(sm.f[c][o], fadd(sigma, 1e-7f));
+            if (r0 + c < rows) out[(size_t)(r0 + c) * 9 + o] = fdiv(head_out(sm, c, o), fadd(sigma, 1e-7f));
         }
     } else {
         if (threadIdx.x < 32) {
@@ -380,7 +436,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
             if (r0 + c < rows) {
                 const int lo = part ? 6 : 0, hi = part ? 9 : 6;
                 float e = 0.f;
-                for (int o = lo; o < hi; ++o) e += sm.xin[c * 16 + o] * fdiv(sm.f[c][o], sigma);
+                for (int o = lo; o < hi; ++o) e += sm.xin[c * 16 + o] * fdiv(head_out(sm, c, o), sigma);
                 out[(size_t)(r0 + c) * 2 + part] = e;
             }
         }
@@ -417,6 +473,7 @@ struct PCArgs {
     float* x;             // (R, 9) state
     float* s;             // (R, 9) score of the previous step
     float* part;          // (2, nwg) per-workgroup sums of row score norms
+    float* zbuf;          // (2, R, 9) Philox draws for the update of the current step
     const float* z1;      // (T, R, 9) or null -> Philox
     const float* z2;
     uint64_t seed;
@@ -429,156 +486,227 @@ struct PCArgs {
 };
 
 // Launch i in [0, steps]: finish step i-1 (if i > 0), then score at step i (if i < steps).
+// Wave 0 runs the update (its global loads, the draws and the grad-norm reduction overlap) while
+// the other waves stage the small weights and issue their first weight-stream loads; one barrier
+// (inside head_trunk) joins them.
 template <int NT, int WV>
 __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
     constexpr int ROWS = NT * 16;
-    constexpr int NTH = WV * 64;
+    constexpr int NLD = (ROWS * 9 + 63) / 64;   // per-lane loads covering the tile's rows
+    static_assert(ROWS <= 64, "one wave updates the tile");
     __shared__ HeadSmem<NT, WV> sm;
     __shared__ int obj[ROWS];
-    __shared__ float s_gn;
     const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r0 = blockIdx.x * ROWS;
-    if (i < a.steps) stage_small_weights<NT, WV>(a.w, sm);
-    if (tid < ROWS) {
-        const int r = r0 + tid;
-        obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
-    }
-    if (i == 0) {
-        for (int e = tid; e < ROWS * 16; e += NTH) {
-            const int c = e >> 4, j = e & 15;
-            const int r = r0 + c;
-            sm.xin[e] = (r < a.rows && j < 9) ? a.x[(size_t)r * 9 + j] : 0.f;
-        }
-    } else {
-        // ---- grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143), fixed order
-        const float* part = a.part + (size_t)((i - 1) & 1) * a.nwg;
-        float acc = 0.f;
-        for (int t = tid; t < a.nwg; t += NTH) acc += part[t];
-        sm.scratch[tid] = acc;
-        // ---- this step's draws: 2 streams x 3 blocks of 4 normals per row, one per thread
-        for (int e = tid; e < ROWS * 6; e += NTH) {
-            const int c = e / 6, st = (e - c * 6) / 3, blk = e - c * 6 - st * 3;
-            const int r = r0 + c;
-            float* dst = &sm.noise[c][st][blk * 4];
-            const float* z = st ? a.z2 : a.z1;
-            if (r >= a.rows) {
-                dst[0] = dst[1] = dst[2] = dst[3] = 0.f;
-            } else if (z) {
-                const float* src = z + ((size_t)(i - 1) * a.rows + r) * 9 + blk * 4;
+    const int nval = min(ROWS, a.rows - r0) * 9;   // valid floats of this tile's (R,9) block
+    const int trace_slot = i & 1;
+    PC_MARK(0);
+    if (wid == 0) {
+        // ---- loads first: x, s (and injected draws) of the tile, grad-norm partials of step i-1
+        float xr[NLD], sr[NLD], z1r[NLD], z2r[NLD];
+        const size_t base = (size_t)r0 * 9;
+        const bool inj = a.z1 != nullptr;
+        const float* z1p = inj ? a.z1 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : a.zbuf;
+        const float* z2p = inj ? a.z2 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : a.zbuf + (size_t)a.rows * 9;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) dst[j] = (blk * 4 + j < 9) ? src[j] : 0.f;
-            } else {
-                const f32x4 v = philox_normal4(a.seed, (uint32_t)(st + 2 * (i - 1)), (uint32_t)r, (uint32_t)blk);
-                dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+        for (int j = 0; j < NLD; ++j) {
+            const int e = lane + 64 * j;
+            const bool v = e < nval && i > 0;
+            xr[j] = e < nval ? a.x[base + e] : 0.f;
+            sr[j] = v ? a.s[base + e] : 0.f;
+            z1r[j] = v ? z1p[base + e] : 0.f;
+            z2r[j] = v ? z2p[base + e] : 0.f;
+        }
+        float gacc = 0.f;
+        if (i > 0) {   // 8 independent loads per lane in flight, summed in a fixed order
+            const float* part = a.part + (size_t)((i - 1) & 1) * a.nwg;
+            for (int t0 = 0; t0 < a.nwg; t0 += 512) {
+                float pv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int t = t0 + lane + 64 * u;
+                    pv[u] = t < a.nwg ? part[t] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) gacc += pv[u];
             }
         }
-        __syncthreads();
-        if (tid < 64) {
-            float v = 0.f;
-#pragma unroll
-            for (int u = 0; u < WV; ++u) v += sm.scratch[tid + 64 * u];
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-            if (tid == 0) s_gn = v / (float)a.rows;
+        __builtin_amdgcn_sched_barrier(0);
+        PC_MARK(9);
+        if (lane < ROWS) {
+            const int r = r0 + lane;
+            obj[lane] = (r < a.rows ? r : a.rows - 1) / a.kper;
         }
-        __syncthreads();
-        if (tid < ROWS) {
+        PC_MARK(10);
+#pragma unroll
+        for (int j = 0; j < NLD; ++j) {
+            const int e = lane + 64 * j;
+            if (e < ROWS * 9) {
+                sm.xu[e] = xr[j];
+                sm.su[e] = sr[j];
+                const int c = e / 9, k = e - c * 9;
+                sm.noise[c][0][k] = z1r[j];
+                sm.noise[c][1][k] = z2r[j];
+            }
+        }
+        // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); the same lane
+        // order and xor tree in every workgroup, so all derive the identical value
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) gacc += __shfl_xor(gacc, off, 64);
+        wave_sync();
+        PC_MARK(11);
+        // four lanes per row: part p < 3 owns elements [3p, 3p+3) (rot6 columns a1, a2, translation)
+        {
 #pragma clang fp contract(off)
-            const int r = r0 + tid;
-            float xv[9];
-            if (r < a.rows) {
-                const float gn = s_gn;
+            const int c = lane >> 2, p = lane & 3;
+            const int r = r0 + c;
+            const int e0 = 3 * (p < 3 ? p : 0);
+            float xv[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) xv[k] = sm.xu[c * 9 + e0 + k];
+            const bool upd = i > 0 && r < a.rows && p < 3;
+            if (upd) {
+                const float gn = gacc / (float)a.rows;
                 const float ratio = a.ls_coef / gn;
                 const float ls = 2.0f * (ratio * ratio);
                 const float sq2ls = sqrtf(2.0f * ls);
-                const float* sp = a.s + (size_t)r * 9;
-                const float* z1 = sm.noise[tid][0];
-                const float* z2 = sm.noise[tid][1];
-                float sv[9];
+                float sv[3], mean[3];
 #pragma unroll
-                for (int j = 0; j < 9; ++j) {
-                    sv[j] = sp[j];
-                    xv[j] = (a.x[(size_t)r * 9 + j] + ls * sv[j]) + sq2ls * z1[j];
+                for (int k = 0; k < 3; ++k) {
+                    sv[k] = sm.su[c * 9 + e0 + k];
+                    xv[k] = (xv[k] + ls * sv[k]) + sq2ls * sm.noise[c][0][e0 + k];
                 }
-                // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
-                const float na = sqrtf((xv[0] * xv[0] + xv[1] * xv[1]) + xv[2] * xv[2]);
-                const float nb = sqrtf((xv[3] * xv[3] + xv[4] * xv[4]) + xv[5] * xv[5]);
-                xv[0] /= na; xv[1] /= na; xv[2] /= na;
-                xv[3] /= nb; xv[4] /= nb; xv[5] /= nb;
+                if (p < 2) {   // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
+                    const float nn = sqrtf((xv[0] * xv[0] + xv[1] * xv[1]) + xv[2] * xv[2]);
+                    xv[0] /= nn; xv[1] /= nn; xv[2] /= nn;
+                }
                 // reverse-SDE Euler-Maruyama predictor (samplers.py:163-166; sign as in the reference)
                 const float g2 = prev.g * prev.g;
                 const float gs = prev.g * prev.sqrt_dt;
-                float mean[9];
 #pragma unroll
-                for (int j = 0; j < 9; ++j) {
-                    const float drift = 0.0f - g2 * sv[j];
-                    mean[j] = xv[j] + drift * prev.dt;
-                    xv[j] = mean[j] + gs * z2[j];
+                for (int k = 0; k < 3; ++k) {
+                    const float drift = 0.0f - g2 * sv[k];
+                    mean[k] = xv[k] + drift * prev.dt;
+                    xv[k] = mean[k] + gs * sm.noise[c][1][e0 + k];
                 }
-                gram_schmidt6<float>(xv);
-                const float* cen = a.center + (size_t)obj[tid] * 3;
+                gram_schmidt6_quad(xv, p, lane);
+                const float* cen = a.center + (size_t)obj[c] * 3;
                 if (a.xs) {
-                    float* o = a.xs + ((size_t)r * a.steps + (i - 1)) * 9;
+                    float* o = a.xs + ((size_t)r * a.steps + (i - 1)) * 9 + e0;
 #pragma unroll
-                    for (int j = 0; j < 6; ++j) o[j] = xv[j];
-                    o[6] = xv[6] + cen[0];
-                    o[7] = xv[7] + cen[1];
-                    o[8] = xv[8] + cen[2];
+                    for (int k = 0; k < 3; ++k) o[k] = p == 2 ? xv[k] + cen[k] : xv[k];
                 }
                 if (i == a.steps) {  // res = mean_x of the last step (+centre, GS), samplers.py:174-177
-                    mean[6] += cen[0];
-                    mean[7] += cen[1];
-                    mean[8] += cen[2];
-                    gram_schmidt6<float>(mean);
-                    float qq[4];
-                    quat_from_gs<float>(mean, qq);
+                    if (p == 2) {
+                        mean[0] += cen[0];
+                        mean[1] += cen[1];
+                        mean[2] += cen[2];
+                    }
+                    gram_schmidt6_quad(mean, p, lane);
 #pragma unroll
-                    for (int j = 0; j < 9; ++j) a.res[(size_t)r * 9 + j] = mean[j];
+                    for (int k = 0; k < 3; ++k) {
+                        a.res[(size_t)r * 9 + e0 + k] = mean[k];
+                        sm.xu[c * 9 + e0 + k] = mean[k];   // gathered below for the quaternion
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) a.x[(size_t)r * 9 + e0 + k] = xv[k];
+            }
+            if (i == a.steps) {
+                wave_sync();
+                if (p == 0 && r < a.rows) {
+                    float m9[9], qq[4];
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) m9[j] = sm.xu[c * 9 + j];
+                    quat_from_gs<float>(m9, qq);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) a.q[(size_t)r * 7 + j] = qq[j];
-                    a.q[(size_t)r * 7 + 4] = mean[6];
-                    a.q[(size_t)r * 7 + 5] = mean[7];
-                    a.q[(size_t)r * 7 + 6] = mean[8];
+                    a.q[(size_t)r * 7 + 4] = m9[6];
+                    a.q[(size_t)r * 7 + 5] = m9[7];
+                    a.q[(size_t)r * 7 + 6] = m9[8];
                 }
+            }
+            if (p < 3) {
 #pragma unroll
-                for (int j = 0; j < 9; ++j) a.x[(size_t)r * 9 + j] = xv[j];
+                for (int k = 0; k < 3; ++k) sm.xin[c * 16 + e0 + k] = (r < a.rows) ? xv[k] : 0.f;
             } else {
 #pragma unroll
-                for (int j = 0; j < 9; ++j) xv[j] = 0.f;
+                for (int j = 9; j < 16; ++j) sm.xin[c * 16 + j] = 0.f;
             }
-#pragma unroll
-            for (int j = 0; j < 16; ++j) sm.xin[tid * 16 + j] = j < 9 ? xv[j] : 0.f;
         }
+        PC_MARK(12);
     }
     if (i == a.steps) return;  // finalize launch: no score evaluation
-    __syncthreads();
-    head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm);
-    // ---- s = f / (sigma + 1e-7); workgroup partial of sum_r ||s_r||
-    if (tid < 64) {
-        float nrm = 0.f;
-        for (int c = tid; c < ROWS; c += 64) {
+    if (wid > 0 && a.z1 == nullptr) {
+        // draws for the update of step i (applied by launch i+1), made while wave 0 updates:
+        // 2 streams x 3 blocks of 4 normals per row, streams 2i (corrector) and 2i+1 (predictor)
+        for (int e = tid - 64; e < ROWS * 6; e += (WV - 1) * 64) {
+            const int c = e / 6, st = (e - c * 6) / 3, blk = e - c * 6 - st * 3;
             const int r = r0 + c;
             if (r < a.rows) {
-                const float den = fadd(cur.sigma, 1e-7f);
-                float ss = 0.f;
-#pragma unroll
-                for (int j = 0; j < 9; ++j) {
-                    const float v = fdiv(sm.f[c][j], den);
-                    a.s[(size_t)r * 9 + j] = v;
-                    ss = fadd(ss, fmul(v, v));
+                const f32x4 v = philox_normal4(a.seed, (uint32_t)(st + 2 * i), (uint32_t)r, (uint32_t)blk);
+                float* dst = a.zbuf + ((size_t)st * a.rows + r) * 9 + blk * 4;
+                dst[0] = v.x;
+                if (blk < 2) {
+                    dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
                 }
-                nrm += sqrtf(ss);
             }
+        }
+    }
+    stage_small_weights<NT, WV, 64>(a.w, sm);
+    head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
+    PC_MARK(7);
+    // ---- s = f / (sigma + 1e-7); workgroup partial of sum_r ||s_r||
+    if (wid == 0) {
+        float nrm = 0.f;
+        const int r = r0 + lane;
+        if (lane < ROWS && r < a.rows) {
+            const float den = fadd(cur.sigma, 1e-7f);
+            float ss = 0.f;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                const float v = fdiv(head_out(sm, lane, j), den);
+                a.s[(size_t)r * 9 + j] = v;
+                ss = fadd(ss, fmul(v, v));
+            }
+            nrm = sqrtf(ss);
         }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
-        if (tid == 0) a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = nrm;
+        if (lane == 0) a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = nrm;
     }
+    PC_MARK(8);
+}
+
+// Device standard normals in the PC sampler's draw layout: out[r][c] = philox_normal4(seed, stream,
+// r, c / 4)[c % 4]. gp_pc_sample's draws of step j are streams 2j (corrector) and 2j+1 (predictor)
+// with cols = 9, so a sampler run fed these as z1/z2 reproduces its Philox run exactly.
+__global__ void randn_kernel(uint64_t seed, uint32_t stream, int rows, int cols, float* __restrict__ out) {
+    const int nb = (cols + 3) >> 2;
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (long long)rows * nb) return;
+    const int r = (int)(e / nb), blk = (int)(e - (long long)r * nb);
+    const f32x4 v = philox_normal4(seed, stream, (uint32_t)r, (uint32_t)blk);
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (4 * blk + k < cols) out[(size_t)r * cols + 4 * blk + k] = vv[k];
+}
+
+extern "C" int gp_randn(uint64_t seed, uint32_t stream, int rows, int cols, float* out, hipStream_t hs) {
+    GP_REQUIRE(rows >= 0 && cols >= 1 && (out || rows == 0), "randn: bad arguments");
+    if (!rows) return GP_OK;
+    const long long n = (long long)rows * ((cols + 3) >> 2);
+    hipLaunchKernelGGL(randn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, hs, seed, stream, rows, cols, out);
+    return gp_check_launch("randn_kernel");
 }
 
 extern "C" size_t gp_pc_workspace_size(int rows) {
     const size_t ntiles = ((size_t)rows + 15) / 16;
-    return sizeof(float) * ((size_t)rows * 9 + 2 * ntiles) + 256;
+    // s (R,9) | grad-norm partials (2, ntiles) | next step's Philox draws (2, R, 9)
+    return sizeof(float) * ((size_t)rows * 9 * 3 + 2 * ntiles) + 256;
 }
 
 static int pc_pick_nt(int rows) {
@@ -606,6 +734,7 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     a.x = x;
     a.s = static_cast<float*>(workspace);
     a.part = a.s + (size_t)rows * 9;
+    a.zbuf = a.part + 2 * (((size_t)rows + 15) / 16);
     a.z1 = z1;
     a.z2 = z2;
     a.seed = seed;

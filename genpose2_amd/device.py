@@ -187,3 +187,12 @@ def pose_epilogue_f64(pose: torch.Tensor, k: int, pts_center: torch.Tensor):
                                    ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(stream_handle(pose.device))),
           "pose_epilogue_f64")
     return pose, q
+
+
+def randn(seed: int, stream: int, rows: int, cols: int, device) -> torch.Tensor:
+    """gp_randn: the device draws gp_pc_sample uses (streams 2j / 2j+1 for step j, cols = 9)."""
+    lib = _lib.load()
+    out = torch.empty((rows, cols), dtype=torch.float32, device=device)
+    check(lib.gp_randn(ctypes.c_uint64(seed), ctypes.c_uint32(stream), rows, cols, ctypes.c_void_p(out.data_ptr()),
+                       ctypes.c_void_p(stream_handle(out.device))), "randn")
+    return out

@@ -125,6 +125,12 @@ int gp_pc_sample(const gp_head_weights *w, const float *pobj, const float *tproj
                  float snr, float *res, float *q, float *xs, void *workspace,
                  size_t workspace_bytes, hipStream_t stream);
 
+/* Standard normals (Philox4x32-10 keyed by seed, counter {row, col/4, stream, 0x5EED}, Box-Muller)
+ * -> out (rows, cols). The replacement of torch.randn_like in cond_pc_sampler (samplers.py:147,165):
+ * gp_pc_sample with z1 = z2 = NULL draws step j's corrector / predictor noise as streams 2j / 2j+1
+ * with cols = 9, identical to gp_randn(seed, 2j (+1), rows, 9, ...). */
+int gp_randn(uint64_t seed, uint32_t stream, int rows, int cols, float *out, hipStream_t hs);
+
 /* Quaternion / GS epilogue used by the ODE path: rows (R,9) fp64 -> in-place GS of [:6],
  * + pts_center on [6:], and q (R,7) fp64. */
 int gp_pose_epilogue_f64(double *pose, int rows, int k, const float *pts_center, double *q,

@@ -282,6 +282,39 @@ def ode_sample(score_fn: Callable, x0: np.ndarray, pts_center_rows: np.ndarray, 
     return xs.transpose(1, 0, 2), x, int(res.nfev)
 
 
+# ============================================================ device noise (gp_randn)
+def philox4x32_10(ctr: np.ndarray, key: np.ndarray) -> np.ndarray:
+    """Philox4x32-10 (Salmon et al., SC'11; Random123's philox4x32 with its round constants):
+    ctr (..., 4) uint32, key (..., 2) uint32 -> (..., 4) uint32. Pinned by the Random123
+    known-answer vectors in tests/test_oracle_pointops.py."""
+    c = [np.asarray(ctr[..., j], np.uint64) for j in range(4)]
+    k0 = np.asarray(key[..., 0], np.uint64)
+    k1 = np.asarray(key[..., 1], np.uint64)
+    m32 = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c[0]
+        p1 = np.uint64(0xCD9E8D57) * c[2]
+        c = [(p1 >> np.uint64(32)) ^ c[1] ^ k0, p1 & m32, (p0 >> np.uint64(32)) ^ c[3] ^ k1, p0 & m32]
+        k0 = (k0 + np.uint64(0x9E3779B9)) & m32
+        k1 = (k1 + np.uint64(0xBB67AE85)) & m32
+    return np.stack(c, -1).astype(np.uint32)
+
+
+def randn(seed: int, stream: int, rows: int, cols: int) -> np.ndarray:
+    """gp_randn's draws in float64: counter {row, col//4, stream, 0x5EED}, key = seed halves,
+    u = ((v >> 8) + 1) / 2^24, Box-Muller (cos, sin) pairs (csrc/gp_common.h philox_normal4)."""
+    nb = (cols + 3) // 4
+    r, b = np.meshgrid(np.arange(rows, dtype=np.uint64), np.arange(nb, dtype=np.uint64), indexing="ij")
+    ctr = np.stack([r, b, np.full_like(r, stream), np.full_like(r, 0x5EED)], -1)
+    key = np.array([seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF], np.uint64)
+    v = philox4x32_10(ctr, np.broadcast_to(key, ctr.shape[:-1] + (2,)))
+    u = ((v >> 8).astype(np.float64) + 1.0) / 16777216.0
+    rad0, rad1 = np.sqrt(-2.0 * np.log(u[..., 0])), np.sqrt(-2.0 * np.log(u[..., 2]))
+    a0, a1 = 2 * np.pi * u[..., 1], 2 * np.pi * u[..., 3]
+    z = np.stack([rad0 * np.cos(a0), rad0 * np.sin(a0), rad1 * np.cos(a1), rad1 * np.sin(a1)], -1)
+    return z.reshape(rows, nb * 4)[:, :cols]
+
+
 # ============================================================ rotations (rotation_conversions.py)
 def rot6_to_matrix(rot6: np.ndarray) -> np.ndarray:
     """get_rot_matrix(.., 'rot_matrix') = rotation_6d_to_matrix(x).permute(0,2,1): columns

@@ -1,0 +1,62 @@
+"""Phase breakdown of pc_step_kernel from in-kernel s_memtime marks (tuning aid, not a test).
+
+Needs the trace build of the library (built here, travels with the snapshot):
+    make -C genpose2_amd/csrc OUT=../../variants/trace/libgenpose_hip.so BUILD=../../variants/trace/build EXTRA=-DPC_TRACE
+    GENPOSE_HIP_LIB=variants/trace/libgenpose_hip.so python scripts/pc_trace.py [B] [K]
+Marks (per wave): 0 start, 1 after the PC update + barrier, 2 after pose_encoder.0 + barrier, 3 after the
+pose_encoder.2 stream, 4 after its epilogue + barrier, 5 after the head-layer-1 stream, 6 after the layer-2
+partials + barrier, 7 after the head output, 8 end.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from genpose2_amd import _lib, sde  # noqa: E402
+from genpose2_amd.agent import PoseNet  # noqa: E402
+from genpose2_amd.config import GenPoseConfig  # noqa: E402
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    K = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    T = 20
+    dev = torch.device("cuda:0")
+    lib = _lib.load()
+    fn = lib.gp_debug_pc_trace
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p]
+    agent = PoseNet(GenPoseConfig(device="cuda:0", sampling_steps=T)).eval()
+    tab = sde.pc_step_table(T)
+    tproj = agent.heads.time_proj(torch.from_numpy(tab[:, 0]).to(dev))
+    pobj = agent.heads.object_proj(torch.rand(B, 1024, device=dev))
+    center = torch.zeros(B, 3, device=dev)
+    x0 = torch.randn(B * K, 9, device=dev) * 50
+    for _ in range(3):
+        agent.heads.pc_sample(pobj, tproj, tab, x0.clone(), K, center, seed=1)
+    torch.cuda.synchronize()
+    buf = np.zeros(2 * 256 * 8 * 16, np.uint64)
+    assert fn(buf.ctypes.data) == 0
+    nwg = min((B * K + 15) // 16, 256)
+    tr = buf.reshape(2, 256, 8, 16)[(T - 1) & 1, :nwg, :, :9].astype(np.int64)
+    t0 = tr[:, :, 0].min()
+    d = np.diff(tr, axis=-1)                       # (wg, wave, 8)
+    names = ["update", "pe0", "pe2_stream", "pe2_epi+bar", "h1_stream", "l2+bar", "f", "s+norm"]
+    out = {"B": B, "K": K, "nwg": int(nwg),
+           "phase_cycles_mean": {n: float(d[..., j].mean()) for j, n in enumerate(names)},
+           "phase_cycles_max": {n: float(d[..., j].max()) for j, n in enumerate(names)},
+           "wg_start_spread_cycles": float(tr[:, :, 0].min(1).max() - t0),
+           "wg_end_max_cycles": float(tr[:, :, 8].max() - t0),
+           "wg_lifetime_mean_cycles": float((tr[:, :, 8].max(1) - tr[:, :, 0].min(1)).mean())}
+    w0 = buf.reshape(2, 256, 8, 16)[(T - 1) & 1, :nwg, 0, :].astype(np.int64)
+    seq = [0, 9, 10, 11, 12, 1]
+    out["wave0_update_cycles_mean"] = {f"{a}->{b}": float((w0[:, b] - w0[:, a]).mean()) for a, b in zip(seq, seq[1:])}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -287,3 +287,36 @@ def test_rank_aggregate_edge_cases():
 
 def _t(a):
     return torch.from_numpy(np.asarray(a, np.float32)).to(DEV)
+
+
+# ---------------------------------------------------------------- device noise
+def test_randn_matches_philox_restatement():
+    from genpose2_amd import device
+    from oracle import oracle
+    for seed, stream, rows, cols in [(1234, 0, 5000, 9), (2**40 + 7, 17, 999, 13), (0, 5, 3, 1)]:
+        got = device.randn(seed, stream, rows, cols, DEV).cpu().numpy().astype(np.float64)
+        ref = oracle.randn(seed, stream, rows, cols)
+        # hardware log2 / sin / cos / sqrt in the Box-Muller transform: a few ulp, not bit-exact
+        assert np.abs(got - ref).max() < 2e-5 * max(1.0, np.abs(ref).max()), (seed, stream)
+    z = device.randn(99, 1, 1 << 18, 9, DEV).double()
+    assert abs(z.mean().item()) < 5e-3 and abs(z.std().item() - 1) < 5e-3
+    assert abs(((z ** 4).mean() / (z ** 2).mean() ** 2).item() - 3) < 0.05   # Gaussian kurtosis
+
+
+def test_pc_philox_equals_injected_draws(score_agent):
+    """The in-kernel draws are exactly gp_randn's streams 2j / 2j+1: feeding those as injected
+    noise reproduces the Philox run bit for bit (so the injected-noise parity tests cover it)."""
+    from genpose2_amd import device, sde
+    B, K, T, seed = 4, 8, 10, 77
+    R = B * K
+    heads = score_agent.heads
+    tab = sde.pc_step_table(T)
+    tproj = heads.time_proj(torch.from_numpy(tab[:, 0]).to(DEV))
+    pobj = heads.object_proj(torch.rand(B, 1024, device=DEV))
+    center = torch.rand(B, 3, device=DEV)
+    x0 = torch.randn(R, 9, device=DEV) * 50
+    res_p, q_p, xs_p = heads.pc_sample(pobj, tproj, tab, x0.clone(), K, center, seed=seed, want_xs=True)
+    z1 = torch.stack([device.randn(seed, 2 * j, R, 9, DEV) for j in range(T)])
+    z2 = torch.stack([device.randn(seed, 2 * j + 1, R, 9, DEV) for j in range(T)])
+    res_i, q_i, xs_i = heads.pc_sample(pobj, tproj, tab, x0.clone(), K, center, z1=z1, z2=z2, want_xs=True)
+    assert torch.equal(res_p, res_i) and torch.equal(q_p, q_i) and torch.equal(xs_p, xs_i)

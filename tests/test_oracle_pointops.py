@@ -84,3 +84,21 @@ def test_group_and_gather_layouts():
     assert g[1, 2, 0, 1] == f[1, 2, 3]
     gi = oracle.gather_operation(f, np.array([[4, 1], [0, 2]], np.int32))
     assert gi[0, 1].tolist() == [f[0, 1, 4], f[0, 1, 1]]
+
+
+def test_philox_known_answer_vectors():
+    """Random123 kat_vectors for philox4x32 (10 rounds)."""
+    from oracle import oracle
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kat:
+        got = oracle.philox4x32_10(np.array(ctr, np.uint64), np.array(key, np.uint64))
+        assert [int(v) for v in got] == list(want)
+
+
+def test_randn_restatement_statistics():
+    from oracle import oracle
+    z = oracle.randn(1234, 3, 20000, 9)
+    assert abs(z.mean()) < 0.02 and abs(z.std() - 1) < 0.02
