@@ -127,10 +127,22 @@ def main():
     data0 = {"pts": torch.from_numpy(pts).to(dev), "pts_center": torch.from_numpy(center).to(dev)}
 
     stream = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(device=dev)
     samp_ev = []
 
     def one_step(record=False):
         data = dict(data0)
+        edata = None
+        if energy is not None:
+            # the energy encoder needs only the points: overlap it with the score sampler
+            # (as genpose2_amd.runner.EvaluationPipeline does)
+            edata = {"pts": data0["pts"], "pts_center": data0["pts_center"]}
+
+            def start_energy_encoder():
+                side.wait_stream(stream)
+                with torch.cuda.stream(side):
+                    energy.encode_func(edata)
+            score.after_encode = start_energy_encoder
         if record:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -148,7 +160,9 @@ def main():
             score.heads.pc_sample = orig
             samp_ev.append((e0, e1))
         if energy is not None:
-            e = energy.get_energy({"pts": data0["pts"], "pts_center": data0["pts_center"]}, pose, T=1e-5)
+            stream.wait_stream(side)
+            edata["pts_feat"].record_stream(stream)
+            e = energy.get_energy(edata, pose, T=1e-5, extract_feature=False)
             agg = aggregate.aggregate_pose(pose, e)
             if scale is not None:
                 scale.pred_scale_func({"pts_feat": data["pts_feat"], "axes": agg[:, :3, :3].contiguous()})

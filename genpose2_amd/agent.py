@@ -48,6 +48,7 @@ class PoseNet:
         self.pts_feature = False
         self.noise_feed: Optional[NoiseFeed] = None
         self._calls = 0
+        self.after_encode = None                   # optional callable run by pred_func after the encoder
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(self.cfg.noise_seed)
         self.weights_source = f"synthetic(seed={self.cfg.seed})"
@@ -94,6 +95,12 @@ class PoseNet:
     def _encode(self, data) -> torch.Tensor:
         return self.encoder.forward(data["pts"])
 
+    @torch.no_grad()
+    def encode_func(self, data):
+        """posenet_agent.py:385-387: data["pts_feat"] (no rgb branch with dino 'none')."""
+        data["pts_feat"] = self._encode(data)
+        data["rgb_feat"] = None
+
     @staticmethod
     def _time_row_and_sigma(heads: dev.HeadModel, t: float):
         t32 = torch.tensor([t], dtype=torch.float32)
@@ -111,6 +118,8 @@ class PoseNet:
         feat = self._encode(data)
         data["pts_feat"] = feat
         data["rgb_feat"] = None                    # dino none (posenet.py:316-318)
+        if self.after_encode is not None:          # pipeline hook: start side-stream work here
+            self.after_encode()
         bs = data["pts"].shape[0]
         K = int(repeat_num)
         R = bs * K

@@ -34,17 +34,37 @@ class EvaluationPipeline:
         self.score_agent = PoseNet(cfg.copy(agent_type="score")).eval()
         self.energy_agent = PoseNet(cfg.copy(agent_type="energy")).eval() if with_energy else None
         self.scale_agent = PoseNet(cfg.copy(agent_type="scale")).eval() if with_scale else None
+        self._side = None
 
     def run(self, batch: Dict[str, torch.Tensor]) -> StageOutputs:
+        """One batch through the stages. The energy network's point encoder depends only on the
+        points, so it runs on a side stream concurrently with the score sampler (started after the
+        score encoder, whose kernels want the whole chip) and is joined before the energy evaluation."""
         cfg = self.cfg
         data = dict(batch)
-        pred_pose, _ = self.score_agent.pred_func(data=data, repeat_num=cfg.eval_repeat_num, T0=cfg.T0,
-                                                  return_average_res=False, return_process=False)
+        edata = None
+        if self.energy_agent is not None:
+            main = torch.cuda.current_stream(batch["pts"].device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=batch["pts"].device)
+            edata = {"pts": batch["pts"], "pts_center": batch["pts_center"]}
+
+            def start_energy_encoder():   # after the score encoder, beside the sampler
+                self._side.wait_stream(main)
+                with torch.cuda.stream(self._side):
+                    self.energy_agent.encode_func(edata)
+            self.score_agent.after_encode = start_energy_encoder
+        try:
+            pred_pose, _ = self.score_agent.pred_func(data=data, repeat_num=cfg.eval_repeat_num, T0=cfg.T0,
+                                                      return_average_res=False, return_process=False)
+        finally:
+            self.score_agent.after_encode = None
         out = StageOutputs(pred_pose=pred_pose, pts_feat=data["pts_feat"])
         if self.energy_agent is not None:
-            edata = {"pts": batch["pts"], "pts_center": batch["pts_center"]}
+            main.wait_stream(self._side)
+            edata["pts_feat"].record_stream(main)
             out.energy = self.energy_agent.get_energy(data=edata, pose_samples=pred_pose, T=1e-5, mode="test",
-                                                      extract_feature=True)
+                                                      extract_feature=False)
         energy = out.energy if out.energy is not None else torch.ones(*pred_pose.shape[:2], 2,
                                                                       device=pred_pose.device)
         out.aggregated = aggregate.aggregate_pose(pred_pose, energy, cfg.retain_ratio, cfg.clustering,

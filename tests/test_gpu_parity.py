@@ -79,6 +79,25 @@ def test_encoder_levels_vs_golden(tag, score_agent):
     assert rel(feat, g[f"{tag}_feat"]) < 1e-5
 
 
+@pytest.mark.parametrize("n,grid", [(1024, True), (2048, True), (1500, False), (600, True)])
+def test_encoder_fps_chain_vs_oracle(n, grid, score_agent):
+    """The encoder's per-object FPS chain (one wave per object) vs the serialized oracle, level by
+    level, on tie-heavy integer grids and ragged sizes."""
+    from genpose2_amd import arch
+    from oracle import oracle
+    rng = np.random.default_rng(n)
+    pts = (rng.integers(0, 6, size=(2, n, 3)) * 0.05 if grid else rng.normal(size=(2, n, 3)) * 0.1)
+    pts = pts.astype(np.float32)
+    _, ws = score_agent.encoder.forward(torch.from_numpy(pts).to(DEV), return_workspace=True)
+    levels = score_agent.encoder.levels(2, n, ws)
+    cur = pts
+    for lv in range(4):
+        idx = oracle.furthest_point_sample(cur, arch.NPOINTS[lv])
+        np.testing.assert_array_equal(levels[lv]["fps_idx"].cpu().numpy(), idx, err_msg=f"level {lv}")
+        cur = np.take_along_axis(cur, idx[..., None].astype(np.int64), 1)
+        np.testing.assert_array_equal(levels[lv]["new_xyz"].cpu().numpy(), cur)
+
+
 def test_encoder_batch_independence(score_agent):
     from genpose2_amd import synthetic
     pts, _ = synthetic.make_batch(5, 6, 1024, n_unique_every=4)
