@@ -36,7 +36,34 @@ struct SAArgs {
     float* out;                       // (B, m, c_out_total)
     int c_out_total, out_off;
     int buf1_off;                     // float4 offset of the second LDS buffer
+    int tag;                          // level * 2 + branch (tuning traces)
+    // layer 0 by per-point projection (levels 0-3): h0(c, s) = relu(Q[nbr] - W0_xyz . x_c), where
+    // Q[p] = W0_feat . f_p + W0_xyz . x_p + b0 was computed once per point by proj_kernel
+    const float* qin;                 // (B, n_prev, q_stride) or null -> layer 0 by MFMA
+    int q_stride, q_off;
+    float* proj_out;                  // proj_kernel: Q output (B, n_prev, q_stride) at q_off
 };
+
+// Per-wave layer timestamps for tuning builds only (make EXTRA=-DSA_TRACE; scripts/sa_trace.py).
+#ifdef SA_TRACE
+__device__ unsigned long long g_sa_trace[8192 * 4 * 8];
+__device__ int g_sa_trace_sel = -1;
+#define SA_MARK(k)                                                                                         \
+    do {                                                                                                   \
+        const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                               \
+        if (a.tag == g_sa_trace_sel && (threadIdx.x & 63) == 0 && wg_ < 8192)                              \
+            g_sa_trace[(wg_ * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime();          \
+    } while (0)
+extern "C" int gp_debug_sa_trace(int sel, unsigned long long* host) {
+    if (host) return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sa_trace), sizeof(g_sa_trace)) == hipSuccess ? 0 : -1;
+    void* ptr = nullptr;
+    if (hipGetSymbolAddress(&ptr, HIP_SYMBOL(g_sa_trace)) != hipSuccess || hipMemset(ptr, 0, sizeof(g_sa_trace)) != hipSuccess)
+        return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sa_trace_sel), &sel, sizeof(int)) == hipSuccess ? 0 : -1;
+}
+#else
+#define SA_MARK(k) ((void)0)
+#endif
 
 constexpr int SA_THREADS = 256;
 
@@ -139,6 +166,14 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
             if (!last) {
 #pragma unroll
                 for (int c = 0; c < CTW; ++c) out_lds[(T * CT + cbase + c) * 64 + lane] = relu4(acc[t][c] + bias);
+            } else if (a.proj_out) {   // per-point projection: pre-activation, point-major
+#pragma unroll
+                for (int c = 0; c < CTW; ++c) {
+                    const int col = col0 + (cbase + c) * 16 + nn;
+                    if (col < a.cols)
+                        st4(a.proj_out + ((size_t)b * a.n_prev + col) * a.q_stride + a.q_off + 16 * T + 4 * q,
+                            acc[t][c] + bias);
+                }
             } else {
                 // max over nsample: across the centroid's SPAN column tiles, then 16 lanes
 #pragma unroll
@@ -176,13 +211,61 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
     }
 }
 
+// Layer 0 from the per-point projection: for each (output tile, column tile) pair of the workgroup,
+// h0 = relu(Q[nbr(col)] - W0_xyz . x_centroid) into LDS buffer 0 in the accumulator layout. The
+// xyz weights are read from the packed layer-0 fragments (k-group c_prev/16, lanes 0..15).
+template <int CT>
+__device__ __forceinline__ void sa_gather0(const SAArgs& a, f32x4* lds, int b, int col0) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int q = lane >> 4, nn = lane & 15;
+    const int NT0 = a.nt[0], KG0 = a.kg[0], gx = a.c_prev >> 4;
+    const f32x4* w0 = reinterpret_cast<const f32x4*>(a.w[0]);
+    int pcol[CT], mcol[CT];
+    bool ok[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        const int col = col0 + ct * 16 + nn;
+        ok[ct] = col < a.cols;
+        const int m = ok[ct] ? col / a.ns : 0, s = ok[ct] ? col - (col / a.ns) * a.ns : 0;
+        mcol[ct] = m;
+        pcol[ct] = ok[ct] ? a.nbr[((size_t)b * a.m + m) * a.ns + s] : 0;
+    }
+    for (int pr = wid; pr < NT0 * CT; pr += 4) {
+        const int T = pr / CT, ct = pr - (pr / CT) * CT;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (ok[ct]) {
+            const f32x4 qv = ld4(a.qin + ((size_t)b * a.n_prev + pcol[ct]) * a.q_stride + a.q_off + 16 * T + 4 * q);
+            const float* cc = a.cent + ((size_t)b * a.m + mcol[ct]) * 3;
+            const float cx = cc[0], cy = cc[1], cz = cc[2];
+            float r[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const f32x4 wx = w0[(T * KG0 + gx) * 64 + 4 * q + j];   // W0[16T+4q+j][c_prev + 0..2]
+                r[j] = fmaxf(qv[j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
+            }
+            v = f32x4{r[0], r[1], r[2], r[3]};
+        }
+        lds[(T * CT + ct) * 64 + lane] = v;
+    }
+}
+
 template <int CT, int TC, int SPAN>
 __global__ __launch_bounds__(SA_THREADS, 2) void sa_branch_kernel(SAArgs a) {
     extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.y;
     const int col0 = blockIdx.x * CT * 16;
-    for (int L = 0; L < a.nlayers; ++L) {
+    SA_MARK(0);
+    int L0 = 0;
+    if (a.qin) {
+        sa_gather0<CT>(a, lds, b, col0);
+        SA_MARK(1);
+        __syncthreads();
+        SA_MARK(2);
+        L0 = 1;
+    }
+    for (int L = L0; L < a.nlayers; ++L) {
         // waves over columns: 4 / (output tiles this layer can feed at TC per wave), kept >= the
         // pooling span on the last layer
         const int nt = a.nt[L];
@@ -199,7 +282,9 @@ __global__ __launch_bounds__(SA_THREADS, 2) void sa_branch_kernel(SAArgs a) {
         } else {
             if constexpr (CT >= 4) sa_layer<CT, CT / 4, TC, 1>(a, lds, L, b, col0, (wid % 4) * (CT / 4), wt, WT);
         }
+        SA_MARK(1 + 2 * L);
         __syncthreads();
+        SA_MARK(2 + 2 * L);
     }
 }
 
@@ -218,8 +303,11 @@ static const int kCout[5] = {96, 256, 512, 1024, 1024};
 static inline int pad16(int v) { return (v + 15) & ~15; }
 
 struct EncLayout {
-    size_t fps[4], nxyz[4], ball[4][2], feat[5], total;
+    size_t fps[4], nxyz[4], ball[4][2], feat[5], proj[4], total;
 };
+
+// Per-point layer-0 projection width of level l (both branches, each padded to 16).
+static inline int proj_stride(int l) { return pad16(kWidths[l][0][1]) + pad16(kWidths[l][1][1]); }
 
 static EncLayout enc_layout(int B, int N) {
     EncLayout L;
@@ -237,8 +325,9 @@ static EncLayout enc_layout(int B, int N) {
         L.ball[l][1] = take(sizeof(int) * B * M * kNs[1]);
     }
     for (int l = 0; l < 5; ++l) L.feat[l] = take(sizeof(float) * B * (l < 4 ? kNpoint[l] : 1) * kCout[l]);
+    for (int l = 0; l < 4; ++l)
+        L.proj[l] = take(sizeof(float) * B * (size_t)(l == 0 ? N : kNpoint[l - 1]) * proj_stride(l));
     L.total = off;
-    (void)N;
     return L;
 }
 
@@ -317,6 +406,35 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                                        xyz_prev, b0, b1, st);
             if (rc) return rc;
         }
+        // layer 0 once per input point for both branches (levels 0-3)
+        float* qbuf = l < 4 ? reinterpret_cast<float*>(ws + L.proj[l]) : nullptr;
+        if (l < 4) {
+            int q_off = 0;
+            for (int br = 0; br < 2; ++br) {
+                SAArgs pa = {};
+                pa.n_prev = n_prev;
+                pa.c_prev = l == 0 ? 0 : kCout[l - 1];
+                pa.m = 1;
+                pa.ns = n_prev;
+                pa.cols = n_prev;
+                pa.xyz_prev = xyz_prev;
+                pa.feat_prev = l == 0 ? nullptr : reinterpret_cast<const float*>(ws + L.feat[l - 1]);
+                pa.nlayers = 1;
+                const int64_t* o = layer_off + ((l * 2 + br) * 3 + 0) * 2;
+                GP_REQUIRE(o[0] >= 0 && o[1] >= 0, "encoder_forward: missing layer %d/%d/0", l, br);
+                pa.w[0] = wbuf + o[0];
+                pa.bias[0] = wbuf + o[1];
+                pa.kg[0] = (pa.c_prev + 16) / 16;
+                pa.nt[0] = pad16(kWidths[l][br][1]) / 16;
+                pa.proj_out = qbuf;
+                pa.q_stride = proj_stride(l);
+                pa.q_off = q_off;
+                pa.tag = 16 + l * 2 + br;
+                q_off += pad16(kWidths[l][br][1]);
+                rc = launch_sa<4>(pa, B, st);
+                if (rc) return rc;
+            }
+        }
         float* out = l < 4 ? reinterpret_cast<float*>(ws + L.feat[l]) : feat;
         if (l == 4) {  // group-all pools with atomicMax when a centroid spans workgroups
             if (hipMemsetAsync(out, 0, sizeof(float) * B * kCout[4], st) != hipSuccess)
@@ -345,6 +463,12 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                 a.nt[i] = pad16(kWidths[l][br][i + 1]) / 16;
             }
             a.out = out;
+            a.tag = l * 2 + br;
+            if (l < 4) {
+                a.qin = qbuf;
+                a.q_stride = proj_stride(l);
+                a.q_off = br == 0 ? 0 : pad16(kWidths[l][0][1]);
+            }
             a.c_out_total = kCout[l];
             a.out_off = out_off;
             out_off += kWidths[l][br][a.nlayers];
