@@ -15,6 +15,8 @@
 //     writes and the next reads 1 KiB per wave-instruction, linear and conflict-free;
 //   * the max over nsample is taken on the accumulators with 16-lane shuffles.
 // Exact f32 MFMA (v_mfma_f32_16x16x4_f32): no precision is traded.
+#include <algorithm>
+
 #include "gp_common.h"
 
 int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const int* m, int* const* idx,
@@ -288,6 +290,140 @@ __global__ __launch_bounds__(SA_THREADS, 2) void sa_branch_kernel(SAArgs a) {
     }
 }
 
+// ============================================================================ narrow levels
+// Levels 0 and 1 (layers <= 128 wide): every wave owns whole centroids and runs layer 1, layer 2
+// and the max-pool for them entirely in registers -- the accumulator of one layer is the next
+// layer's B operand as is, so there is no LDS round trip and no barrier after the weights are
+// staged. Layer 0 comes from the per-point projection (relu(Q[nbr] - W0_xyz . x_c)).
+struct NarrowArgs {
+    const float* qin;      // (B, n_prev, q_stride)
+    int q_stride, q_off, n_prev;
+    const float* w0;       // packed layer 0 (for its xyz columns), KG0 k-groups
+    int kg0, gx;           // k-groups of layer 0, index of its xyz k-group
+    const float* w1;       // packed layer 1 / 2 and biases
+    const float* b1;
+    const float* w2;
+    const float* b2;
+    const int* nbr;        // (B, m, ns)
+    const float* cent;     // (B, m, 3)
+    int m, ns, nobj;
+    float* out;            // (B, m, c_out_total)
+    int c_out_total, out_off;
+};
+
+template <int KG1, int NT1, int NT2, int SPAN>
+__device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
+    constexpr int KG2 = NT1;
+    constexpr int NA1 = NT1 * KG1 * 64, NA2 = NT2 * KG2 * 64;
+    f32x4* sA1 = lds;
+    f32x4* sA2 = sA1 + NA1;
+    f32x4* sW0x = sA2 + NA2;              // [KG1*16] (wx, wy, wz, 0) per layer-0 output channel
+    float* sB1 = reinterpret_cast<float*>(sW0x + KG1 * 16);
+    float* sB2 = sB1 + NT1 * 16;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < NA1; i += SA_THREADS) sA1[i] = ld4(a.w1 + (size_t)i * 4);
+    for (int i = tid; i < NA2; i += SA_THREADS) sA2[i] = ld4(a.w2 + (size_t)i * 4);
+    for (int ch = tid; ch < KG1 * 16; ch += SA_THREADS)   // packed layer-0 fragment of channel ch, q = 0
+        sW0x[ch] = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
+    for (int i = tid; i < NT1 * 16; i += SA_THREADS) sB1[i] = a.b1[i];
+    for (int i = tid; i < NT2 * 16; i += SA_THREADS) sB2[i] = a.b2[i];
+    __syncthreads();
+    const int lane = tid & 63, q = lane >> 4, nn = lane & 15;
+    const int nw = gridDim.x * (SA_THREADS / 64);
+    const int total = a.nobj * a.m;
+    for (int task = blockIdx.x * (SA_THREADS / 64) + (tid >> 6); task < total; task += nw) {
+        const int b = task / a.m;
+        const float* cc = a.cent + (size_t)task * 3;
+        const float cx = cc[0], cy = cc[1], cz = cc[2];
+        f32x4 rmax[NT2];
+#pragma unroll
+        for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{0.f, 0.f, 0.f, 0.f};   // max of ReLU outputs
+#pragma unroll
+        for (int ct = 0; ct < SPAN; ++ct) {
+            const int p = a.nbr[(size_t)task * a.ns + ct * 16 + nn];
+            const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
+            f32x4 bf[KG1];
+#pragma unroll
+            for (int g = 0; g < KG1; ++g) bf[g] = ld4(qrow + 16 * g);
+#pragma unroll
+            for (int g = 0; g < KG1; ++g) {
+#pragma clang fp contract(off)
+                float r[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 wx = sW0x[16 * g + 4 * q + j];
+                    r[j] = fmaxf(bf[g][j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
+                }
+                bf[g] = f32x4{r[0], r[1], r[2], r[3]};
+            }
+            f32x4 acc1[NT1];
+#pragma unroll
+            for (int t = 0; t < NT1; ++t) acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int g = 0; g < KG1; ++g) {
+                f32x4 af[NT1];
+#pragma unroll
+                for (int t = 0; t < NT1; ++t) af[t] = sA1[(t * KG1 + g) * 64 + lane];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int t = 0; t < NT1; ++t) acc1[t] = mfma4(af[t][j], bf[g][j], acc1[t]);
+                __builtin_amdgcn_sched_barrier(0);   // bound the live A fragments to one k-group
+            }
+#pragma unroll
+            for (int t = 0; t < NT1; ++t) acc1[t] = relu4(acc1[t] + ld4(&sB1[16 * t + 4 * q]));
+            f32x4 acc2[NT2];
+#pragma unroll
+            for (int t = 0; t < NT2; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int g = 0; g < KG2; ++g) {
+                f32x4 af[NT2];
+#pragma unroll
+                for (int t = 0; t < NT2; ++t) af[t] = sA2[(t * KG2 + g) * 64 + lane];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int t = 0; t < NT2; ++t) acc2[t] = mfma4(af[t][j], acc1[g][j], acc2[t]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int t = 0; t < NT2; ++t) {
+                const f32x4 v = relu4(acc2[t] + ld4(&sB2[16 * t + 4 * q]));
+                rmax[t] = f32x4{fmaxf(rmax[t].x, v.x), fmaxf(rmax[t].y, v.y), fmaxf(rmax[t].z, v.z),
+                                fmaxf(rmax[t].w, v.w)};
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        float* o = a.out + (size_t)task * a.c_out_total + a.out_off + 4 * q;
+#pragma unroll
+        for (int t = 0; t < NT2; ++t) {
+            f32x4 v = rmax[t];
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) {
+                v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
+                v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
+                v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
+                v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
+            }
+            if (nn == 0) st4(o + 16 * t, v);
+        }
+    }
+}
+
+// Both branches of a narrow level in one launch: blockIdx.y = branch.
+template <int KG1a, int NT1a, int NT2a, int SPANa, int KG1b, int NT1b, int NT2b, int SPANb>
+__global__ __launch_bounds__(SA_THREADS) void sa_narrow_kernel(NarrowArgs a0, NarrowArgs a1) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+    if (blockIdx.y == 0)
+        narrow_branch<KG1a, NT1a, NT2a, SPANa>(a0, lds);
+    else
+        narrow_branch<KG1b, NT1b, NT2b, SPANb>(a1, lds);
+}
+
+static size_t narrow_lds(int kg1, int nt1, int nt2) {
+    return sizeof(f32x4) * ((size_t)nt1 * kg1 * 64 + (size_t)nt2 * nt1 * 64 + kg1 * 16) + sizeof(float) * 16 * (nt1 + nt2);
+}
+
 // ============================================================================ host side
 static const int kNpoint[4] = {512, 256, 128, 64};
 static const int kNs[2] = {16, 32};
@@ -439,6 +575,53 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
         if (l == 4) {  // group-all pools with atomicMax when a centroid spans workgroups
             if (hipMemsetAsync(out, 0, sizeof(float) * B * kCout[4], st) != hipSuccess)
                 return gp_check_launch("encoder memset");
+        }
+        if (l <= 1) {   // narrow levels: one launch, wave-independent centroids
+            NarrowArgs na[2];
+            int out_off = 0, q_off = 0;
+            for (int br = 0; br < 2; ++br) {
+                NarrowArgs& n = na[br];
+                n = {};
+                n.qin = qbuf;
+                n.q_stride = proj_stride(l);
+                n.q_off = q_off;
+                q_off += pad16(kWidths[l][br][1]);
+                n.n_prev = n_prev;
+                const int64_t* o0 = layer_off + ((l * 2 + br) * 3 + 0) * 2;
+                const int64_t* o1 = layer_off + ((l * 2 + br) * 3 + 1) * 2;
+                const int64_t* o2 = layer_off + ((l * 2 + br) * 3 + 2) * 2;
+                GP_REQUIRE(o1[0] >= 0 && o2[0] >= 0, "encoder_forward: missing layers of %d/%d", l, br);
+                n.w0 = wbuf + o0[0];
+                n.c_out_total = kCout[l];
+                const int c_prev = l == 0 ? 0 : kCout[l - 1];
+                n.kg0 = (c_prev + 16) / 16;
+                n.gx = c_prev / 16;
+                n.w1 = wbuf + o1[0];
+                n.b1 = wbuf + o1[1];
+                n.w2 = wbuf + o2[0];
+                n.b2 = wbuf + o2[1];
+                n.nbr = br == 0 ? b0 : b1;
+                n.cent = nxyz[l];
+                n.m = kNpoint[l];
+                n.ns = kNs[br];
+                n.nobj = B;
+                n.out = out;
+                n.out_off = out_off;
+                out_off += kWidths[l][br][3];
+            }
+            const dim3 grid(512, 2);
+            if (l == 0) {
+                const size_t lds = std::max(narrow_lds(1, 1, 2), narrow_lds(2, 2, 4));
+                hipLaunchKernelGGL((sa_narrow_kernel<1, 1, 2, 1, 2, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
+                                   na[1]);
+            } else {
+                const size_t lds = std::max(narrow_lds(4, 4, 8), narrow_lds(4, 6, 8));
+                hipLaunchKernelGGL((sa_narrow_kernel<4, 4, 8, 1, 4, 6, 8, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
+                                   na[1]);
+            }
+            rc = gp_check_launch("sa_narrow_kernel");
+            if (rc) return rc;
+            continue;
         }
         int out_off = 0;
         for (int br = 0; br < 2; ++br) {
