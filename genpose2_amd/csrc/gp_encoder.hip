@@ -112,7 +112,13 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
             bx[c] = v;
         }
     }
-    for (int T0 = wt * TC; T0 < NT; T0 += WT * TC) {
+    // this wave's output tiles wt, wt+WT, wt+2WT, ... (round robin keeps waves within one tile
+    // of each other), TC of them per pass
+    const int cnt = NT > wt ? (NT - wt + WT - 1) / WT : 0;
+    for (int i0 = 0; i0 < cnt; i0 += TC) {
+        int Tt[TC];
+#pragma unroll
+        for (int t = 0; t < TC; ++t) Tt[t] = (i0 + t < cnt) ? wt + (i0 + t) * WT : NT;   // NT = none
         f32x4 acc[TC][CTW];
 #pragma unroll
         for (int t = 0; t < TC; ++t)
@@ -123,7 +129,7 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
         auto fetch = [&](int g, f32x4 (&af)[TC], f32x4 (&bf)[CTW]) {
 #pragma unroll
             for (int t = 0; t < TC; ++t)
-                af[t] = (T0 + t < NT) ? ldbuf4(W, voff, ((T0 + t) * KG + g) * 1024) : f32x4{0.f, 0.f, 0.f, 0.f};
+                af[t] = (Tt[t] < NT) ? ldbuf4(W, voff, (Tt[t] * KG + g) * 1024) : f32x4{0.f, 0.f, 0.f, 0.f};
             if (L == 0) {
                 if (g < feat_groups) {
 #pragma unroll
@@ -162,7 +168,7 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
         }
 #pragma unroll
         for (int t = 0; t < TC; ++t) {
-            const int T = T0 + t;
+            const int T = Tt[t];
             if (T >= NT) continue;
             const f32x4 bias = ld4(a.bias[L] + 16 * T + 4 * q);
             if (!last) {
@@ -659,9 +665,9 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                 gp_set_error("encoder_forward: nsample %d not a multiple of 16", a.ns);
                 return GP_ERR_UNSUPPORTED;
             }
-            // level 3 at 32 columns (its 640-channel LDS ping-pong), GroupAll split over 2 workgroups
+            // levels 2-3 at 32 columns (LDS ping-pong <= 80 KiB: 2-3 workgroups per CU), GroupAll split over 2 workgroups
             // per (object, branch) with atomicMax pooling (4x the workgroups of one per object)
-            rc = (l >= 3) ? launch_sa<2>(a, B, st) : launch_sa<4>(a, B, st);
+            rc = (l >= 2) ? launch_sa<2>(a, B, st) : launch_sa<4>(a, B, st);
             if (rc) return rc;
         }
     }

@@ -41,6 +41,8 @@ def main():
             nl = 3 if lv < 4 else 2
             tr = buf.reshape(8192, 4, 8).astype(np.int64)
             used = tr[:, 0, 0] != 0
+            if not used.any():   # level not run by sa_branch_kernel (narrow levels)
+                continue
             tr = tr[used][:, :, : 2 * nl + 1]
             d = np.diff(tr, axis=-1)
             widths = br[lv][b].widths
