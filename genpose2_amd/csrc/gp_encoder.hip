@@ -259,8 +259,7 @@ __device__ __forceinline__ void sa_gather0(const SAArgs& a, f32x4* lds, int b, i
 }
 
 template <int CT, int TC, int SPAN>
-__global__ __launch_bounds__(SA_THREADS, 2) void sa_branch_kernel(SAArgs a) {
-    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+__device__ __forceinline__ void sa_body(const SAArgs& a, f32x4* lds) {
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.y;
     const int col0 = blockIdx.x * CT * 16;
@@ -293,6 +292,18 @@ __global__ __launch_bounds__(SA_THREADS, 2) void sa_branch_kernel(SAArgs a) {
         SA_MARK(1 + 2 * L);
         __syncthreads();
         SA_MARK(2 + 2 * L);
+    }
+}
+
+// Both branches of a level (or both branch projections) in one launch: blockIdx.z = branch.
+// Each branch keeps its own column count, layer widths and pooling span.
+template <int CT, int SPAN0, int SPAN1>
+__global__ __launch_bounds__(SA_THREADS, 2) void sa_pair_kernel(SAArgs a0, SAArgs a1) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+    if (blockIdx.z == 0) {
+        if ((int)blockIdx.x * CT * 16 < a0.cols) sa_body<CT, 4, SPAN0>(a0, lds);
+    } else {
+        if ((int)blockIdx.x * CT * 16 < a1.cols) sa_body<CT, 4, SPAN1>(a1, lds);
     }
 }
 
@@ -489,32 +500,44 @@ extern "C" int gp_encoder_workspace_layout(int b, int n, int64_t* offsets) {
 }
 
 template <int CT>
-static int launch_sa(const SAArgs& a, int B, hipStream_t st) {
+static size_t sa_lds(SAArgs& a) {
     size_t buf0 = 0, buf1 = 0;
     if (a.nlayers >= 2) buf0 = (size_t)CT * 16 * a.nt[0] * 16;                 // floats
     if (a.nlayers >= 3) buf1 = (size_t)CT * 16 * a.nt[1] * 16;
-    SAArgs args = a;
-    args.buf1_off = (int)(buf0 / 4);
-    const size_t lds = (buf0 + buf1) * sizeof(float);
-    if (lds > 160 * 1024) {
-        gp_set_error("sa_branch_kernel: LDS %zu bytes exceeds 160 KiB", lds);
-        return GP_ERR_UNSUPPORTED;
-    }
-    const int blocks = (a.cols + CT * 16 - 1) / (CT * 16);
+    a.buf1_off = (int)(buf0 / 4);
+    return (buf0 + buf1) * sizeof(float);
+}
+
+template <int CT>
+static int sa_span(const SAArgs& a) {
     const int tpc = a.ns / 16;
-    const int span = tpc < CT ? tpc : CT;
-    if (span == 1)
-        hipLaunchKernelGGL((sa_branch_kernel<CT, 4, 1>), dim3(blocks, B), dim3(SA_THREADS), lds, st, args);
-    else if (span == 2)
-        hipLaunchKernelGGL((sa_branch_kernel<CT, 4, 2>), dim3(blocks, B), dim3(SA_THREADS), lds, st, args);
-    else if (span == 4 && CT >= 4)
-        hipLaunchKernelGGL((sa_branch_kernel<(CT >= 4 ? CT : 4), 4, 4>), dim3(blocks, B), dim3(SA_THREADS), lds, st,
-                           args);
-    else {
-        gp_set_error("sa_branch_kernel: unsupported span %d", span);
+    return tpc < CT ? tpc : CT;
+}
+
+// One launch for a pair of branches (a0 on blockIdx.z = 0, a1 on 1).
+template <int CT>
+static int launch_pair(SAArgs a0, SAArgs a1, int B, hipStream_t st) {
+    const size_t lds = std::max(sa_lds<CT>(a0), sa_lds<CT>(a1));
+    if (lds > 160 * 1024) {
+        gp_set_error("sa_pair_kernel: LDS %zu bytes exceeds 160 KiB", lds);
         return GP_ERR_UNSUPPORTED;
     }
-    return gp_check_launch("sa_branch_kernel");
+    const int blocks = std::max((a0.cols + CT * 16 - 1) / (CT * 16), (a1.cols + CT * 16 - 1) / (CT * 16));
+    const int s0 = sa_span<CT>(a0), s1 = sa_span<CT>(a1);
+    const dim3 grid(blocks, B, 2), blk(SA_THREADS);
+#define GP_SA_PAIR(S0, S1)                                                                     \
+    if (s0 == S0 && s1 == S1) {                                                                \
+        hipLaunchKernelGGL((sa_pair_kernel<CT, S0, S1>), grid, blk, lds, st, a0, a1);          \
+        return gp_check_launch("sa_pair_kernel");                                              \
+    }
+    if constexpr (CT == 2) {
+        GP_SA_PAIR(1, 2) GP_SA_PAIR(2, 2) GP_SA_PAIR(1, 1)
+    } else {
+        GP_SA_PAIR(4, 4) GP_SA_PAIR(1, 2) GP_SA_PAIR(2, 2) GP_SA_PAIR(1, 1)
+    }
+#undef GP_SA_PAIR
+    gp_set_error("sa_pair_kernel: unsupported spans %d/%d", s0, s1);
+    return GP_ERR_UNSUPPORTED;
 }
 
 extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N,
@@ -552,8 +575,10 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
         float* qbuf = l < 4 ? reinterpret_cast<float*>(ws + L.proj[l]) : nullptr;
         if (l < 4) {
             int q_off = 0;
+            SAArgs pp[2];
             for (int br = 0; br < 2; ++br) {
-                SAArgs pa = {};
+                SAArgs& pa = pp[br];
+                pa = {};
                 pa.n_prev = n_prev;
                 pa.c_prev = l == 0 ? 0 : kCout[l - 1];
                 pa.m = 1;
@@ -573,9 +598,9 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                 pa.q_off = q_off;
                 pa.tag = 16 + l * 2 + br;
                 q_off += pad16(kWidths[l][br][1]);
-                rc = launch_sa<4>(pa, B, st);
-                if (rc) return rc;
             }
+            rc = launch_pair<4>(pp[0], pp[1], B, st);
+            if (rc) return rc;
         }
         float* out = l < 4 ? reinterpret_cast<float*>(ws + L.feat[l]) : feat;
         if (l == 4) {  // group-all pools with atomicMax when a centroid spans workgroups
@@ -630,8 +655,10 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
             continue;
         }
         int out_off = 0;
+        SAArgs sa[2];
         for (int br = 0; br < 2; ++br) {
-            SAArgs a = {};
+            SAArgs& a = sa[br];
+            a = {};
             a.n_prev = n_prev;
             a.c_prev = l == 0 ? 0 : kCout[l - 1];
             a.m = l < 4 ? kNpoint[l] : 1;
@@ -665,11 +692,11 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                 gp_set_error("encoder_forward: nsample %d not a multiple of 16", a.ns);
                 return GP_ERR_UNSUPPORTED;
             }
-            // levels 2-3 at 32 columns (LDS ping-pong <= 80 KiB: 2-3 workgroups per CU), GroupAll split over 2 workgroups
-            // per (object, branch) with atomicMax pooling (4x the workgroups of one per object)
-            rc = (l >= 2) ? launch_sa<2>(a, B, st) : launch_sa<4>(a, B, st);
-            if (rc) return rc;
         }
+        // levels 2-3 at 32 columns (LDS ping-pong <= 80 KiB: 2-3 workgroups per CU), GroupAll split
+        // over 2 workgroups per (object, branch) with atomicMax pooling; both branches per launch
+        rc = launch_pair<2>(sa[0], sa[1], B, st);
+        if (rc) return rc;
     }
     return GP_OK;
 }
