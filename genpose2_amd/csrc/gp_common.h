@@ -81,6 +81,33 @@ __device__ __forceinline__ float dist2_ref(float ax, float ay, float az, float b
     return (dx * dx + dy * dy) + dz * dz;
 }
 
+// --------------------------------------------------------------- cross-lane sums (no LDS)
+// DPP within 16-lane rows, then the gfx950 row swaps (v_permlane16_swap / v_permlane32_swap):
+// every lane ends with the same bits, and the summation order is fixed, so every workgroup that
+// runs the same code reduces identically.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// sum over lanes l, l^16, l^32, l^48 (the four rows' lane n)
+__device__ __forceinline__ float rows_sum(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float wave_sum(float v) {
+    v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
+    v = dpp_add<0x141>(v);   // row_half_mirror
+    v = dpp_add<0x140>(v);   // row_mirror
+    return rows_sum(v);
+}
+// value of lane 4*(l/4) (first lane of the quad)
+__device__ __forceinline__ float quad_bcast0(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x00, 0xF, 0xF, false));
+}
+
 // --------------------------------------------------------------- Philox4x32-10 + Box-Muller
 struct u32x4 { uint32_t x, y, z, w; };
 

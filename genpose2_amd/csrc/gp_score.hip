@@ -247,12 +247,9 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
                 p1 += u.x * w1.x + u.y * w1.y + u.z * w1.z + u.w * w1.w;
                 p2 += u.x * w2.x + u.y * w2.y + u.z * w2.z + u.w * w2.w;
             }
-#pragma unroll
-            for (int off = 16; off <= 32; off <<= 1) {
-                p0 += __shfl_xor(p0, off, 64);
-                p1 += __shfl_xor(p1, off, 64);
-                p2 += __shfl_xor(p2, off, 64);
-            }
+            p0 = rows_sum(p0);
+            p1 = rows_sum(p1);
+            p2 = rows_sum(p2);
             if (q == 0) {
                 sm.red[wid][h * 3 + 0][ct * 16 + n] = p0;
                 sm.red[wid][h * 3 + 1][ct * 16 + n] = p1;
@@ -299,8 +296,8 @@ __device__ __forceinline__ void gram_schmidt6_quad(float* v, int p, int lane) {
     float n1 = sqrtf((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
     n1 = n1 > 1e-12f ? n1 : 1e-12f;
     const float b0 = v[0] / n1, b1 = v[1] / n1, b2 = v[2] / n1;   // meaningful on p == 0
-    const int src = lane & ~3;
-    const float B0 = __shfl(b0, src, 64), B1 = __shfl(b1, src, 64), B2 = __shfl(b2, src, 64);
+    (void)lane;
+    const float B0 = quad_bcast0(b0), B1 = quad_bcast0(b1), B2 = quad_bcast0(b2);
     const float d = (B0 * v[0] + B1 * v[1]) + B2 * v[2];
     float c0 = v[0] - d * B0, c1 = v[1] - d * B1, c2 = v[2] - d * B2;
     float n2 = sqrtf((c0 * c0 + c1 * c1) + c2 * c2);
@@ -553,8 +550,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
         }
         // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); the same lane
         // order and xor tree in every workgroup, so all derive the identical value
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) gacc += __shfl_xor(gacc, off, 64);
+        gacc = wave_sum(gacc);
         wave_sync();
         PC_MARK(11);
         // four lanes per row: part p < 3 owns elements [3p, 3p+3) (rot6 columns a1, a2, translation)
@@ -673,8 +669,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             }
             nrm = sqrtf(ss);
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
+        nrm = wave_sum(nrm);
         if (lane == 0) a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = nrm;
     }
     PC_MARK(8);
