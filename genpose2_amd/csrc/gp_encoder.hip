@@ -18,6 +18,7 @@
 #include <algorithm>
 
 #include "gp_common.h"
+#include "gp_fps.h"
 
 int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const int* m, int* const* idx,
                         float* const* nxyz, hipStream_t st);
@@ -427,11 +428,60 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
     }
 }
 
-// Both branches of a narrow level in one launch: blockIdx.y = branch.
+// FPS levels run beside a narrow level's MLP as extra workgroups (blockIdx.y == 0, one per
+// object): the chain's later levels depend only on the previous level's centroids, so they need
+// not sit on the critical path. Level l+1 reads level l's sampled coordinates.
+struct FpsSide {
+    int nlev;               // 0: none
+    int n[2], m[2], nb[2], jbits[2];
+    const float* in;        // (B, n[0], 3)
+    int* idx[2];            // (B, m_l)
+    float* nxyz[2];         // (B, m_l, 3)
+    int nobj;
+};
+
+static size_t fps_side_lds(const FpsSide& f) {
+    return f.nlev ? FPS_RED_BYTES + sizeof(float) * 3 * ((size_t)f.n[0] + f.m[0]) + sizeof(int) * (size_t)f.m[0] : 0;
+}
+
+__device__ __forceinline__ void fps_side(const FpsSide& f, char* smem) {
+    const int b = blockIdx.x;
+    if (b >= f.nobj) return;
+    void* s_red = smem;
+    float* cur = reinterpret_cast<float*>(smem + FPS_RED_BYTES);
+    float* nxt = cur + 3 * f.n[0];
+    int* s_idx = reinterpret_cast<int*>(nxt + 3 * f.m[0]);
+    const float* src = f.in + (size_t)b * f.n[0] * 3;
+    for (int i = threadIdx.x; i < 3 * f.n[0]; i += FPS_THREADS) cur[i] = src[i];
+    __syncthreads();
+    for (int l = 0; l < f.nlev; ++l) {
+        if (f.n[l] <= FPS_THREADS)
+            fps_run<1>(cur, f.n[l], f.m[l], f.nb[l], f.jbits[l], s_red, s_idx, nxt);
+        else if (f.n[l] <= 2 * FPS_THREADS)
+            fps_run<2>(cur, f.n[l], f.m[l], f.nb[l], f.jbits[l], s_red, s_idx, nxt);
+        else
+            fps_run<4>(cur, f.n[l], f.m[l], f.nb[l], f.jbits[l], s_red, s_idx, nxt);
+        __syncthreads();
+        int* gi = f.idx[l] + (size_t)b * f.m[l];
+        float* gx = f.nxyz[l] + (size_t)b * f.m[l] * 3;
+        for (int i = threadIdx.x; i < f.m[l]; i += FPS_THREADS) gi[i] = s_idx[i];
+        for (int i = threadIdx.x; i < 3 * f.m[l]; i += FPS_THREADS) gx[i] = nxt[i];
+        __syncthreads();
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+}
+
+// Both branches of a narrow level in one launch (blockIdx.y = 1 + branch), plus FPS side work.
 template <int KG1a, int NT1a, int NT2a, int SPANa, int KG1b, int NT1b, int NT2b, int SPANb>
-__global__ __launch_bounds__(SA_THREADS) void sa_narrow_kernel(NarrowArgs a0, NarrowArgs a1) {
+__global__ __launch_bounds__(SA_THREADS) void sa_narrow_kernel(NarrowArgs a0, NarrowArgs a1, FpsSide f) {
     extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+    // FPS first (blockIdx.y == 0): the dispatcher issues workgroups in linear order, so the
+    // latency-bound FPS chain starts at once instead of behind the 1024 MLP workgroups
     if (blockIdx.y == 0)
+        fps_side(f, reinterpret_cast<char*>(lds));
+    else if (blockIdx.y == 1)
         narrow_branch<KG1a, NT1a, NT2a, SPANa>(a0, lds);
     else
         narrow_branch<KG1b, NT1b, NT2b, SPANb>(a1, lds);
@@ -557,7 +607,8 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
         nin[l] = l == 0 ? N : kNpoint[l - 1];
         mout[l] = kNpoint[l];
     }
-    int rc = gp_launch_fps_chain(pts, B, 4, nin, mout, fidx, nxyz, st);
+    // FPS level 0 here; levels 1-3 run beside the level-0 / level-1 MLP launches (FpsSide)
+    int rc = gp_launch_fps_chain(pts, B, 1, nin, mout, fidx, nxyz, st);
     if (rc) return rc;
     for (int l = 0; l < 5; ++l) {
         const float* xyz_prev = l == 0 ? pts : nxyz[l - 1];
@@ -640,15 +691,29 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                 n.out_off = out_off;
                 out_off += kWidths[l][br][3];
             }
-            const dim3 grid(512, 2);
+            FpsSide fs = {};
+            fs.nlev = l == 0 ? 1 : 2;          // level 0 launch: FPS level 1; level 1 launch: FPS levels 2, 3
+            fs.in = nxyz[l];
+            fs.nobj = B;
+            for (int k = 0; k < fs.nlev; ++k) {
+                const int lv = l == 0 ? 1 : 2 + k;
+                fs.n[k] = nin[lv];
+                fs.m[k] = mout[lv];
+                const FpsGeom g = fps_geom(nin[lv]);
+                fs.nb[k] = g.nb;
+                fs.jbits[k] = g.jbits;
+                fs.idx[k] = fidx[lv];
+                fs.nxyz[k] = nxyz[lv];
+            }
+            const dim3 grid(std::max(512, B), 3);
             if (l == 0) {
-                const size_t lds = std::max(narrow_lds(1, 1, 2), narrow_lds(2, 2, 4));
+                const size_t lds = std::max({narrow_lds(1, 1, 2), narrow_lds(2, 2, 4), fps_side_lds(fs)});
                 hipLaunchKernelGGL((sa_narrow_kernel<1, 1, 2, 1, 2, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
-                                   na[1]);
+                                   na[1], fs);
             } else {
-                const size_t lds = std::max(narrow_lds(4, 4, 8), narrow_lds(4, 6, 8));
+                const size_t lds = std::max({narrow_lds(4, 4, 8), narrow_lds(4, 6, 8), fps_side_lds(fs)});
                 hipLaunchKernelGGL((sa_narrow_kernel<4, 4, 8, 1, 4, 6, 8, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
-                                   na[1]);
+                                   na[1], fs);
             }
             rc = gp_check_launch("sa_narrow_kernel");
             if (rc) return rc;

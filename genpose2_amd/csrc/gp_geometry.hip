@@ -19,6 +19,7 @@
 #include <stdio.h>
 
 #include "gp_common.h"
+#include "gp_fps.h"
 
 // ============================================================================ error plumbing
 static thread_local char g_err[512];
@@ -42,126 +43,13 @@ int gp_check_launch(const char* what) {
 extern "C" const char* gp_last_error(void) { return g_err; }
 extern "C" int gp_abi_version(void) { return GP_ABI_VERSION; }
 
-// ============================================================================ FPS
-static int fps_block_log2(int n) {  // cuda_utils.h:9-13 (opt_n_threads), exact for n>=1
-    int p = 0;
-    while ((2 << p) <= n && p < 10) ++p;
-    return p;
-}
-
-struct FpsGeom {
-    int nb;      // log2 of the reference block size
-    int jbits;   // bits for k / bs
-};
-
-static FpsGeom fps_geom(int n) {
-    FpsGeom g;
-    g.nb = fps_block_log2(n);
-    const int jmax = (n - 1) >> g.nb;
-    g.jbits = 0;
-    while ((1 << g.jbits) <= jmax) ++g.jbits;
-    return g;
-}
-
-__device__ __forceinline__ uint32_t fps_key(int k, int nb, int jbits) {
-    const uint32_t t = (uint32_t)k & ((1u << nb) - 1u);
-    const uint32_t rt = nb ? (__brev(t) >> (32 - nb)) : 0u;
-    return (rt << jbits) | ((uint32_t)k >> nb);
-}
-
-__device__ __forceinline__ int fps_key_to_k(uint32_t key, int nb, int jbits) {
-    const uint32_t rt = key >> jbits;
-    const uint32_t t = nb ? (__brev(rt) >> (32 - nb)) : 0u;
-    return (int)(t + ((key & ((1u << jbits) - 1u)) << nb));
-}
-
-__device__ __forceinline__ unsigned long long fps_pack(float d2, uint32_t key) {
-    return ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned long long)(0xFFFFFFFFu - key);
-}
-
-constexpr int FPS_THREADS = 256;
-
-// Wave-wide max of a 64-bit key with DPP row operations (quad perms, half/full row mirror,
-// row_bcast15/31) instead of 6 ds_bpermute shuffle rounds; the result is read from lane 63.
-#define GP_DPP_MAX_STEP(CTRL, ROWMASK)                                                          \
-    {                                                                                           \
-        const uint32_t ohi = (uint32_t)__builtin_amdgcn_update_dpp((int)hi, (int)hi, CTRL, ROWMASK, 0xF, false); \
-        const uint32_t olo = (uint32_t)__builtin_amdgcn_update_dpp((int)lo, (int)lo, CTRL, ROWMASK, 0xF, false); \
-        const bool take = (ohi > hi) || (ohi == hi && olo > lo);                                 \
-        hi = take ? ohi : hi;                                                                   \
-        lo = take ? olo : lo;                                                                   \
-    }
-
-__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
-    uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-    GP_DPP_MAX_STEP(0xB1, 0xF)   // quad_perm [1,0,3,2]
-    GP_DPP_MAX_STEP(0x4E, 0xF)   // quad_perm [2,3,0,1]
-    GP_DPP_MAX_STEP(0x141, 0xF)  // row_half_mirror
-    GP_DPP_MAX_STEP(0x140, 0xF)  // row_mirror
-    GP_DPP_MAX_STEP(0x142, 0xA)  // row_bcast:15 -> rows 1, 3
-    GP_DPP_MAX_STEP(0x143, 0xC)  // row_bcast:31 -> rows 2, 3
-    const uint32_t rhi = (uint32_t)__builtin_amdgcn_readlane((int)hi, 63);
-    const uint32_t rlo = (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
-    return ((unsigned long long)rhi << 32) | rlo;
-}
-
-// One FPS run over `n` points held in LDS (s_xyz, xyz interleaved). Writes the m indices to
-// s_idx and the selected coordinates to s_out (both LDS; s_out may be null). Nothing touches
-// global memory inside the iteration loop, so the per-iteration barrier never waits on a store.
-// All 256 threads must call it.
-template <int PMAX>
-__device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits,
-                        unsigned long long* s_red /* [2][4] */, int* s_idx, float* s_out) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    float px[PMAX], py[PMAX], pz[PMAX], tmin[PMAX];
-    uint32_t key[PMAX];
-#pragma unroll
-    for (int p = 0; p < PMAX; ++p) {
-        const int k = tid + p * FPS_THREADS;
-        const bool ok = k < n;
-        px[p] = ok ? s_xyz[3 * k + 0] : 0.f;
-        py[p] = ok ? s_xyz[3 * k + 1] : 0.f;
-        pz[p] = ok ? s_xyz[3 * k + 2] : 0.f;
-        tmin[p] = 1e10f;                        // pointnet2_utils.py:32-34
-        key[p] = ok ? fps_key(k, nb, jbits) : 0u;
-    }
-    int old = 0;
-    if (m <= 0) return;
-    if (tid == 0) s_idx[0] = 0;
-    if (tid < 3 && s_out) s_out[tid] = s_xyz[tid];
-    for (int j = 1; j < m; ++j) {
-        const float x1 = s_xyz[3 * old + 0], y1 = s_xyz[3 * old + 1], z1 = s_xyz[3 * old + 2];
-        unsigned long long best = 0ull;
-#pragma unroll
-        for (int p = 0; p < PMAX; ++p) {
-            const int k = tid + p * FPS_THREADS;
-            if (k < n) {
-                const float d = dist2_ref(px[p], py[p], pz[p], x1, y1, z1);
-                const float d2 = fminf(d, tmin[p]);
-                tmin[p] = d2;
-                const unsigned long long c = fps_pack(d2, key[p]);
-                best = c > best ? c : best;
-            }
-        }
-        best = wave_max_u64(best);
-        unsigned long long* red = s_red + (j & 1) * 4;
-        if (lane == 0) red[wid] = best;
-        __syncthreads();
-        unsigned long long b = red[0];
-#pragma unroll
-        for (int w = 1; w < FPS_THREADS / 64; ++w) b = red[w] > b ? red[w] : b;
-        old = fps_key_to_k(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull), nb, jbits);
-        if (tid == 0) s_idx[j] = old;
-        if (tid < 3 && s_out) s_out[3 * j + tid] = s_xyz[3 * old + tid];
-    }
-}
-
+// ============================================================================ FPS (core in gp_fps.h)
 template <int PMAX>
 __global__ __launch_bounds__(FPS_THREADS) void fps_kernel(const float* __restrict__ xyz, int n, int m,
                                                           int nb, int jbits, int* __restrict__ idx) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(smem);
-    float* s_xyz = reinterpret_cast<float*>(smem + 64);
+    void* s_red = smem;
+    float* s_xyz = reinterpret_cast<float*>(smem + FPS_RED_BYTES);
     const int b = blockIdx.x;
     const float* src = xyz + (size_t)b * n * 3;
     int* s_idx = reinterpret_cast<int*>(s_xyz + 3 * n);
@@ -174,7 +62,7 @@ __global__ __launch_bounds__(FPS_THREADS) void fps_kernel(const float* __restric
 
 static int launch_fps(const float* xyz, int b, int n, int m, int* idx, hipStream_t st) {
     const FpsGeom g = fps_geom(n);
-    const size_t lds = 64 + sizeof(float) * 3 * (size_t)n + sizeof(int) * (size_t)m;
+    const size_t lds = FPS_RED_BYTES + sizeof(float) * 3 * (size_t)n + sizeof(int) * (size_t)m;
     if (lds > 160 * 1024) {
         gp_set_error("furthest_point_sampling: n=%d, m=%d exceed the LDS budget", n, m);
         return GP_ERR_UNSUPPORTED;
@@ -217,8 +105,8 @@ struct ChainArgs {
 template <int PMAX>
 __global__ __launch_bounds__(FPS_THREADS) void fps_chain_kernel(const float* __restrict__ xyz, ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(smem);
-    float* bufA = reinterpret_cast<float*>(smem + 64);
+    void* s_red = smem;
+    float* bufA = reinterpret_cast<float*>(smem + FPS_RED_BYTES);
     float* bufB = bufA + 3 * a.n[0];
     int* s_idx = reinterpret_cast<int*>(bufB + 3 * a.m[0]);
     const int b = blockIdx.x;
@@ -254,7 +142,7 @@ int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const i
         a.idx[l] = idx[l];
         a.nxyz[l] = nxyz[l];
     }
-    const size_t lds = 64 + sizeof(float) * 3 * ((size_t)n[0] + (size_t)m[0]) + sizeof(int) * (size_t)m[0];
+    const size_t lds = FPS_RED_BYTES + sizeof(float) * 3 * ((size_t)n[0] + (size_t)m[0]) + sizeof(int) * (size_t)m[0];
     const int p = (n[0] + FPS_THREADS - 1) / FPS_THREADS;
 #define GP_CHAIN_CASE(PM)                                                                       \
     if (p <= PM) {                                                                              \
