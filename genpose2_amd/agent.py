@@ -58,6 +58,7 @@ class PoseNet:
     def _build(self, sd: weights.StateDict) -> None:
         weights.check_keys(sd, self.cfg.agent_type)
         self.state_dict = sd
+        self._pc_cache = {}                        # T -> (step table, tproj) of these weights
         if self.cfg.agent_type in ("score", "energy"):
             self.encoder = dev.EncoderModel(sd, self.device)
             self.heads = dev.HeadModel(sd, self.device)
@@ -91,6 +92,17 @@ class PoseNet:
         if self.noise_feed is not None:
             return self.noise_feed.prior.to(self.device, torch.float32).reshape(R, arch.POSE_DIM)
         return torch.randn((R, arch.POSE_DIM), generator=self._gen, device=self.device, dtype=torch.float32)
+
+    def _pc_table(self, T: int):
+        """Step table and per-step head projections for T steps: fixed by T and the weights, so
+        built once (the H2D copy of the time grid would otherwise stall the host behind the
+        encoder on every call)."""
+        c = self._pc_cache.get(T)
+        if c is None:
+            tab = sde.pc_step_table(T)
+            c = (tab, self.heads.time_proj(torch.from_numpy(tab[:, 0]).to(self.device)))
+            self._pc_cache[T] = c
+        return c
 
     def _encode(self, data) -> torch.Tensor:
         return self.encoder.forward(data["pts"])
@@ -131,8 +143,7 @@ class PoseNet:
         self._calls += 1
         if mode == "pc":
             T = int(self.cfg.sampling_steps)
-            tab = sde.pc_step_table(T)
-            tproj = self.heads.time_proj(torch.from_numpy(tab[:, 0]).to(self.device))
+            tab, tproj = self._pc_table(T)
             if rep_init is None:   # prior((R,9)) at T=1 (sde.py:30-34); init_x used as-is (samplers.py:128)
                 x = (self._draw_prior(R) * sde.prior_sigma(arch.SDE_T)).contiguous()
             else:

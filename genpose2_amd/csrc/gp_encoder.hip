@@ -69,6 +69,9 @@ extern "C" int gp_debug_sa_trace(int sel, unsigned long long* host) {
 #endif
 
 constexpr int SA_THREADS = 256;
+#ifndef SA_RING
+#define SA_RING 2        // k-groups of operands in flight + 1
+#endif
 
 // One layer for the CTW column tiles [cbase, cbase+CTW) of this wave and the output tiles
 // wt*TC, wt*TC + WT*TC, ... (WT = waves sharing the columns). Layers narrower than 4*TC output
@@ -155,17 +158,22 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
 #pragma unroll
                     for (int c = 0; c < CTW; ++c) acc[t][c] = mfma4(af[t][j], bf[c][j], acc[t][c]);
         };
-        // two-slot ping-pong: the operands of k-group g+1 are in flight while g computes;
-        // sched_barrier keeps the compiler from sinking the loads back next to their MFMAs
-        f32x4 aA[TC], bA[CTW], aB[TC], bB[CTW];
-        fetch(0, aA, bA);
-        for (int g = 0; g < KG; g += 2) {
-            if (g + 1 < KG) fetch(g + 1, aB, bB);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(aA, bA);
-            if (g + 2 < KG) fetch(g + 2, aA, bA);
-            __builtin_amdgcn_sched_barrier(0);
-            if (g + 1 < KG) compute(aB, bB);
+        // SA_RING-slot ring: the operands of k-groups g+1 .. g+SA_RING-1 are in flight while g
+        // computes; sched_barrier keeps the compiler from sinking the loads next to their MFMAs
+        f32x4 ra[SA_RING][TC], rb[SA_RING][CTW];
+#pragma unroll
+        for (int u = 0; u < SA_RING - 1; ++u)
+            if (u < KG) fetch(u, ra[u], rb[u]);
+        for (int g = 0; g < KG; g += SA_RING) {
+#pragma unroll
+            for (int u = 0; u < SA_RING; ++u) {
+                if (g + u < KG) {
+                    if (g + u + SA_RING - 1 < KG)
+                        fetch(g + u + SA_RING - 1, ra[(u + SA_RING - 1) % SA_RING], rb[(u + SA_RING - 1) % SA_RING]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute(ra[u], rb[u]);
+                }
+            }
         }
 #pragma unroll
         for (int t = 0; t < TC; ++t) {
@@ -259,7 +267,26 @@ __device__ __forceinline__ void sa_gather0(const SAArgs& a, f32x4* lds, int b, i
     }
 }
 
-template <int CT, int TC, int SPAN>
+// A layer with exactly the wave's tile count per pass where an instantiation exists (a pass of TC
+// tiles computes all TC accumulators, so a short last pass would burn MFMAs on absent tiles).
+template <int CT, int CTW, int SPAN, int MAXTC>
+__device__ __forceinline__ void sa_layer_fit(const SAArgs& a, f32x4* lds, int L, int b, int col0, int cbase, int wt,
+                                             int WT) {
+    const int nt = a.nt[L];
+    const int cnt = nt > wt ? (nt - wt + WT - 1) / WT : 0;
+    if constexpr (MAXTC >= 8) {
+        if (cnt == 8) return sa_layer<CT, CTW, 8, SPAN>(a, lds, L, b, col0, cbase, wt, WT);
+    }
+    if constexpr (MAXTC >= 7) {
+        if (cnt == 7) return sa_layer<CT, CTW, 7, SPAN>(a, lds, L, b, col0, cbase, wt, WT);
+    }
+    if constexpr (MAXTC >= 6) {
+        if (cnt == 6) return sa_layer<CT, CTW, 6, SPAN>(a, lds, L, b, col0, cbase, wt, WT);
+    }
+    sa_layer<CT, CTW, 4, SPAN>(a, lds, L, b, col0, cbase, wt, WT);
+}
+
+template <int CT, int TC, int SPAN, int MAXTC>
 __device__ __forceinline__ void sa_body(const SAArgs& a, f32x4* lds) {
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.y;
@@ -283,12 +310,12 @@ __device__ __forceinline__ void sa_body(const SAArgs& a, f32x4* lds) {
             while (wc > 1 && CT / wc < SPAN) wc >>= 1;
         const int wt = wid / wc, WT = 4 / wc;
         if (wc == 1) {
-            sa_layer<CT, CT, TC, SPAN>(a, lds, L, b, col0, 0, wt, WT);
+            sa_layer_fit<CT, CT, SPAN, MAXTC>(a, lds, L, b, col0, 0, wt, WT);
         } else if (wc == 2) {
-            if constexpr (CT >= 2 && CT / 2 >= 1) sa_layer<CT, CT / 2, TC, (SPAN <= CT / 2 ? SPAN : 1)>(
+            if constexpr (CT >= 2 && CT / 2 >= 1) sa_layer_fit<CT, CT / 2, (SPAN <= CT / 2 ? SPAN : 1), MAXTC>(
                 a, lds, L, b, col0, (wid % 2) * (CT / 2), wt, WT);
         } else {
-            if constexpr (CT >= 4) sa_layer<CT, CT / 4, TC, 1>(a, lds, L, b, col0, (wid % 4) * (CT / 4), wt, WT);
+            if constexpr (CT >= 4) sa_layer_fit<CT, CT / 4, 1, MAXTC>(a, lds, L, b, col0, (wid % 4) * (CT / 4), wt, WT);
         }
         SA_MARK(1 + 2 * L);
         __syncthreads();
@@ -298,13 +325,13 @@ __device__ __forceinline__ void sa_body(const SAArgs& a, f32x4* lds) {
 
 // Both branches of a level (or both branch projections) in one launch: blockIdx.z = branch.
 // Each branch keeps its own column count, layer widths and pooling span.
-template <int CT, int SPAN0, int SPAN1>
+template <int CT, int SPAN0, int SPAN1, int MAXTC>
 __global__ __launch_bounds__(SA_THREADS, 2) void sa_pair_kernel(SAArgs a0, SAArgs a1) {
     extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
     if (blockIdx.z == 0) {
-        if ((int)blockIdx.x * CT * 16 < a0.cols) sa_body<CT, 4, SPAN0>(a0, lds);
+        if ((int)blockIdx.x * CT * 16 < a0.cols) sa_body<CT, 4, SPAN0, MAXTC>(a0, lds);
     } else {
-        if ((int)blockIdx.x * CT * 16 < a1.cols) sa_body<CT, 4, SPAN1>(a1, lds);
+        if ((int)blockIdx.x * CT * 16 < a1.cols) sa_body<CT, 4, SPAN1, MAXTC>(a1, lds);
     }
 }
 
@@ -565,7 +592,7 @@ static int sa_span(const SAArgs& a) {
 }
 
 // One launch for a pair of branches (a0 on blockIdx.z = 0, a1 on 1).
-template <int CT>
+template <int CT, int MAXTC = 4>
 static int launch_pair(SAArgs a0, SAArgs a1, int B, hipStream_t st) {
     const size_t lds = std::max(sa_lds<CT>(a0), sa_lds<CT>(a1));
     if (lds > 160 * 1024) {
@@ -577,7 +604,7 @@ static int launch_pair(SAArgs a0, SAArgs a1, int B, hipStream_t st) {
     const dim3 grid(blocks, B, 2), blk(SA_THREADS);
 #define GP_SA_PAIR(S0, S1)                                                                     \
     if (s0 == S0 && s1 == S1) {                                                                \
-        hipLaunchKernelGGL((sa_pair_kernel<CT, S0, S1>), grid, blk, lds, st, a0, a1);          \
+        hipLaunchKernelGGL((sa_pair_kernel<CT, S0, S1, MAXTC>), grid, blk, lds, st, a0, a1);   \
         return gp_check_launch("sa_pair_kernel");                                              \
     }
     if constexpr (CT == 2) {
@@ -760,7 +787,10 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
         }
         // levels 2-3 at 32 columns (LDS ping-pong <= 80 KiB: 2-3 workgroups per CU), GroupAll split
         // over 2 workgroups per (object, branch) with atomicMax pooling; both branches per launch
-        rc = launch_pair<2>(sa[0], sa[1], B, st);
+        // levels 3-4: one pass of up to 8 tiles per wave per layer (2 workgroups per CU either way);
+        // level 2 keeps 4-tile passes: its 131 VGPRs fit 3 workgroups per CU, a 7-tile pass's 191 only
+        // 2 (measured 725 vs 764 us)
+        rc = l == 2 ? launch_pair<2, 4>(sa[0], sa[1], B, st) : launch_pair<2, 8>(sa[0], sa[1], B, st);
         if (rc) return rc;
     }
     return GP_OK;

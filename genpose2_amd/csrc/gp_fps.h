@@ -67,15 +67,15 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     return ((unsigned long long)rhi << 32) | rlo;
 }
 
-constexpr int FPS_RED_BYTES = 2 * (FPS_THREADS / 64) * 8;   // double-buffered per-wave 64-bit maxima
+constexpr int FPS_RED_BYTES = 2 * 16 * 8;   // double-buffered per-wave 64-bit maxima, up to 16 waves
 
 // One FPS run over `n` points held in LDS (s_xyz, xyz interleaved). Writes the m indices to
 // s_idx and the selected coordinates to s_out (both LDS; s_out may be null). Nothing touches
 // global memory inside the iteration loop, so the per-iteration barrier never waits on a store.
-// All 256 threads must call it. s_red holds FPS_RED_BYTES.
+// All NTH threads must call it. s_red holds FPS_RED_BYTES.
 // (Carrying the winner's coordinates through the exchange instead of re-reading them from s_xyz
 // was measured slower: 411 vs 327 us for level 0 at B=64.)
-template <int PMAX>
+template <int PMAX, int NTH = FPS_THREADS>
 __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits, void* s_red_v, int* s_idx,
                         float* s_out) {
     unsigned long long* s_red = reinterpret_cast<unsigned long long*>(s_red_v);
@@ -84,7 +84,7 @@ __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits, voi
     uint32_t key[PMAX];
 #pragma unroll
     for (int p = 0; p < PMAX; ++p) {
-        const int k = tid + p * FPS_THREADS;
+        const int k = tid + p * NTH;
         const bool ok = k < n;
         px[p] = ok ? s_xyz[3 * k + 0] : 0.f;
         py[p] = ok ? s_xyz[3 * k + 1] : 0.f;
@@ -101,7 +101,7 @@ __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits, voi
         unsigned long long best = 0ull;
 #pragma unroll
         for (int p = 0; p < PMAX; ++p) {
-            const int k = tid + p * FPS_THREADS;
+            const int k = tid + p * NTH;
             if (k < n) {
                 const float d = dist2_ref(px[p], py[p], pz[p], x1, y1, z1);
                 const float d2 = fminf(d, tmin[p]);
@@ -111,12 +111,12 @@ __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits, voi
             }
         }
         best = wave_max_u64(best);
-        unsigned long long* red = s_red + (j & 1) * 4;
+        unsigned long long* red = s_red + (j & 1) * 16;
         if (lane == 0) red[wid] = best;
         __syncthreads();
         unsigned long long b = red[0];
 #pragma unroll
-        for (int w = 1; w < FPS_THREADS / 64; ++w) b = red[w] > b ? red[w] : b;
+        for (int w = 1; w < NTH / 64; ++w) b = red[w] > b ? red[w] : b;
         old = fps_key_to_k(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull), nb, jbits);
         if (tid == 0) s_idx[j] = old;
         if (tid < 3 && s_out) s_out[3 * j + tid] = s_xyz[3 * old + tid];
