@@ -73,8 +73,9 @@ constexpr int FPS_RED_BYTES = 2 * 16 * 8;   // double-buffered per-wave 64-bit m
 // s_idx and the selected coordinates to s_out (both LDS; s_out may be null). Nothing touches
 // global memory inside the iteration loop, so the per-iteration barrier never waits on a store.
 // All NTH threads must call it. s_red holds FPS_RED_BYTES.
-// (Carrying the winner's coordinates through the exchange instead of re-reading them from s_xyz
-// was measured slower: 411 vs 327 us for level 0 at B=64.)
+// Measured slower and not kept (level 0 at B=64): carrying the winner's coordinates through the
+// exchange instead of re-reading them from s_xyz (411 vs 327 us); two 32-bit DPP maxima (distance,
+// then key) instead of one 64-bit maximum of the packed pair (436 vs 309 us).
 template <int PMAX, int NTH = FPS_THREADS>
 __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits, void* s_red_v, int* s_idx,
                         float* s_out) {
