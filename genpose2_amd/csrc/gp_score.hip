@@ -60,7 +60,7 @@ struct HeadSmem {
     float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
     f32x4 act1[KG_HID * NT * 64];      // pose_encoder.0 output, accumulator-native [g][ct][lane]
     f32x4 act2[KG_HID * NT * 64];      // pose_encoder.2 output
-    float red[WV][9][NT * 16];         // per-wave head-layer-2 partials (head output: head_out())
+    float red[NT * 16][9][WV];         // per-wave head-layer-2 partials, wave-minor (head_out reads a row)
     float xu[NT * 16 * 9];             // PC update inputs: state x and score s of this tile's rows
     float su[NT * 16 * 9];
     float noise[NT * 16][2][12];       // PC corrector / predictor draws of this step
@@ -92,7 +92,7 @@ template <int NT, int WV>
 __device__ __forceinline__ float head_out(const HeadSmem<NT, WV>& sm, int c, int o) {
     float acc = 0.f;
 #pragma unroll
-    for (int v = 0; v < WV; ++v) acc += sm.red[v][o][c];
+    for (int v = 0; v < WV; ++v) acc += sm.red[c][o][v];
     return sm.h2b[o] + acc;
 }
 
@@ -204,19 +204,27 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
     __syncthreads();
     PC_MARK(2);
     // ---- pose_encoder.2 (256 -> 256): TPW output tiles per wave
-    stream_step<D2, KG_HID + D2, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
-    // ---- head layer 1 prologue, issued before the barrier: accumulator init with the hoisted
-    //      pts/t blocks, and the first DH k-groups of the pose-block weights
-    PC_MARK(3);
-    f32x4 acc[3 * TPW][NT];
+    // the last PE2_TAIL k-groups of pose_encoder.2 run after the head-layer-1 accumulator-init loads
+    // (hoisted pts/t blocks) are issued, so their latency hides behind MFMAs
+    constexpr int PE2_TAIL = 4;
+    stream_step<D2, KG_HID + D2 - PE2_TAIL, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
+    f32x4 tpv[3 * TPW], pov[3 * TPW][NT];
 #pragma unroll
     for (int i = 0; i < 3 * TPW; ++i) {
         const int T = TH[i];
-        const f32x4 tp = ld4(tproj + 16 * T + 4 * q);
+        tpv[i] = ld4(tproj + 16 * T + 4 * q);
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct)
-            acc[i][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q) + tp;
+        for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q);
     }
+    stream_step<KG_HID + D2 - PE2_TAIL, KG_HID + D2, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
+    // ---- head layer 1 prologue, issued before the barrier: the first DH k-groups of the pose-block
+    //      weights
+    PC_MARK(3);
+    f32x4 acc[3 * TPW][NT];
+#pragma unroll
+    for (int i = 0; i < 3 * TPW; ++i)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) acc[i][ct] = pov[i][ct] + tpv[i];
     f32x4 ringh[DH + 1][3 * TPW];
     stream_step<0, DH, 3 * TPW, NT, KG_HID, DH>(WH, TH, sm.act2, lane, voff, ringh, acc);
 #pragma unroll
@@ -251,9 +259,9 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
             p1 = rows_sum(p1);
             p2 = rows_sum(p2);
             if (q == 0) {
-                sm.red[wid][h * 3 + 0][ct * 16 + n] = p0;
-                sm.red[wid][h * 3 + 1][ct * 16 + n] = p1;
-                sm.red[wid][h * 3 + 2][ct * 16 + n] = p2;
+                sm.red[ct * 16 + n][h * 3 + 0][wid] = p0;
+                sm.red[ct * 16 + n][h * 3 + 1][wid] = p1;
+                sm.red[ct * 16 + n][h * 3 + 2][wid] = p2;
             }
         }
     }
@@ -470,7 +478,9 @@ struct PCArgs {
     float* x;             // (R, 9) state
     float* s;             // (R, 9) score of the previous step
     float* part;          // (2, nwg) per-workgroup sums of row score norms
-    float* zbuf;          // (2, R, 9) Philox draws for the update of the current step
+    float* zbuf;          // (2 slots, 2 streams, R, 9) Philox draws: launch i writes step i's into slot
+                          // i&1 while its wave 0 reads step i-1's from the other slot (no ordering
+                          // between the waves of a workgroup is needed)
     const float* z1;      // (T, R, 9) or null -> Philox
     const float* z2;
     uint64_t seed;
@@ -505,8 +515,9 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
         float xr[NLD], sr[NLD], z1r[NLD], z2r[NLD];
         const size_t base = (size_t)r0 * 9;
         const bool inj = a.z1 != nullptr;
-        const float* z1p = inj ? a.z1 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : a.zbuf;
-        const float* z2p = inj ? a.z2 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : a.zbuf + (size_t)a.rows * 9;
+        const float* zslot = a.zbuf + (size_t)((i - 1) & 1) * 2 * a.rows * 9;
+        const float* z1p = inj ? a.z1 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : zslot;
+        const float* z2p = inj ? a.z2 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : zslot + (size_t)a.rows * 9;
 #pragma unroll
         for (int j = 0; j < NLD; ++j) {
             const int e = lane + 64 * j;
@@ -643,7 +654,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             const int r = r0 + c;
             if (r < a.rows) {
                 const f32x4 v = philox_normal4(a.seed, (uint32_t)(st + 2 * i), (uint32_t)r, (uint32_t)blk);
-                float* dst = a.zbuf + ((size_t)st * a.rows + r) * 9 + blk * 4;
+                float* dst = a.zbuf + ((size_t)((i & 1) * 2 + st) * a.rows + r) * 9 + blk * 4;
                 dst[0] = v.x;
                 if (blk < 2) {
                     dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
@@ -700,8 +711,8 @@ extern "C" int gp_randn(uint64_t seed, uint32_t stream, int rows, int cols, floa
 
 extern "C" size_t gp_pc_workspace_size(int rows) {
     const size_t ntiles = ((size_t)rows + 15) / 16;
-    // s (R,9) | grad-norm partials (2, ntiles) | next step's Philox draws (2, R, 9)
-    return sizeof(float) * ((size_t)rows * 9 * 3 + 2 * ntiles) + 256;
+    // s (R,9) | grad-norm partials (2, ntiles) | Philox draws (2 slots, 2 streams, R, 9)
+    return sizeof(float) * ((size_t)rows * 9 * 5 + 2 * ntiles) + 256;
 }
 
 static int pc_pick_nt(int rows) {

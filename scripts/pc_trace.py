@@ -52,6 +52,14 @@ def main():
            "wg_start_spread_cycles": float(tr[:, :, 0].min(1).max() - t0),
            "wg_end_max_cycles": float(tr[:, :, 8].max() - t0),
            "wg_lifetime_mean_cycles": float((tr[:, :, 8].max(1) - tr[:, :, 0].min(1)).mean())}
+    # workgroup critical path: the last wave past each barrier
+    st = tr[:, :, 0].min(1)
+    crit = {"update+bar1": tr[:, :, 1].max(1) - st,
+            "pe0+bar2": tr[:, :, 2].max(1) - tr[:, :, 1].max(1),
+            "pe2+epi+bar4": tr[:, :, 4].max(1) - tr[:, :, 2].max(1),
+            "h1 (last wave)": tr[:, :, 5].max(1) - tr[:, :, 4].max(1),
+            "tail (l2, bar, s)": tr[:, :, 8].max(1) - tr[:, :, 5].max(1)}
+    out["critical_path_mean"] = {k: float(v.mean()) for k, v in crit.items()}
     w0 = buf.reshape(2, 256, 8, 16)[(T - 1) & 1, :nwg, 0, :].astype(np.int64)
     seq = [0, 9, 10, 11, 12, 1]
     out["wave0_update_cycles_mean"] = {f"{a}->{b}": float((w0[:, b] - w0[:, a]).mean()) for a, b in zip(seq, seq[1:])}
