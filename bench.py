@@ -72,10 +72,20 @@ def cpu_baseline(cfg, threads):
                      np.zeros((R, 3), np.float32), ts_sample, z, z)
     t_step = (time.perf_counter() - t0) / ts_sample
     total = t_enc_obj * B + t_step * T
-    return {"value": B * K * T / total, "unit": "pose-candidate-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (numpy fp32, reference unhoisted score form) encoder on 2 objects "
-                      f"({t_enc_obj*1e3:.0f} ms/object) + PC sampler at R={R} rows for {ts_sample} steps "
-                      f"({t_step*1e3:.0f} ms/step), extrapolated to B={B}, T={T}"}
+    out = {"value": B * K * T / total, "unit": "pose-candidate-steps/s", "cores": threads, "kind": "port",
+           "sample": f"oracle (numpy fp32, reference unhoisted score form) encoder on 2 objects "
+                     f"({t_enc_obj*1e3:.0f} ms/object) + PC sampler at R={R} rows for {ts_sample} steps "
+                     f"({t_step*1e3:.0f} ms/step), extrapolated to B={B}, T={T}"}
+    # the oracle/reference time ratio measured in the build container on identical
+    # inputs and threads (oracle/calibrate_cpu.py); converts the port figure to reference terms
+    cal = os.path.join(REPO, "profiles", "r1", "cpu_calibration.json")
+    if os.path.exists(cal):
+        with open(cal) as f:
+            c = json.load(f)
+        out["calibration"] = {"oracle_over_reference": round(c["oracle_over_reference"], 3),
+                              "threads": c["threads"], "source": "profiles/r1/cpu_calibration.json"}
+        out["reference_equivalent_value"] = out["value"] * c["oracle_over_reference"]
+    return out
 
 
 def load_traffic(rows):
