@@ -305,8 +305,59 @@ def gen_pipeline(get_config, PoseNet):
     np.savez_compressed(os.path.join(HERE, "golden_pipeline.npz"), **out)
 
 
+def gen_tracking(get_config, PoseNet):
+    """Warm start as runners/evaluation_tracking.py:110-127 calls it: init_x = previous pose with
+    pts_center subtracted from its translation, small T0. PC uses init_x as-is
+    and ignores T0 (posenet.py:241-253); ODE starts at prior(sigma(T0)) + init_x (samplers.py:197-201)."""
+    from utils.misc import get_pose_representation
+    B, K, T, T0 = 2, 5, 20, 0.2
+    d = batch(41, B, 1024)
+    rng = np.random.Generator(np.random.PCG64(400))
+    prev = torch.zeros(B, 9)
+    for j in range(B):
+        Rj = torch.from_numpy(synthetic._random_rotation(rng)).float()
+        prev[j, :6] = get_pose_representation(Rj[None], "rot_matrix")[0]
+        prev[j, 6:] = d["pts_center"][j] + torch.from_numpy(rng.normal(scale=0.01, size=3)).float()
+    init_x = prev.clone()
+    init_x[:, -3:] -= d["pts_center"]
+    prior = rng.standard_normal((B * K, 9)).astype(np.float32)
+    zs = rng.standard_normal((2 * T, B * K, 9)).astype(np.float32)
+    out = dict(pts=d["pts"].numpy(), pts_center=d["pts_center"].numpy(), init_x=init_x.numpy(),
+               prior=prior, z1=zs[0::2], z2=zs[1::2], K=K, T=T, T0=T0)
+    agent = make_agent(get_config, PoseNet, "score", "pc", T)
+    with NoiseFeed(prior, zs) as nf:
+        pose, q = agent.pred_func(dict(d), repeat_num=K, T0=T0, init_x=init_x.clone())
+        assert nf.i == 2 * T
+    out.update(pc_pred_pose=pose.numpy(), pc_pred_q=q.numpy())
+    agent = make_agent(get_config, PoseNet, "score", "ode", None)
+    import scipy.integrate as si
+    calls = {"n": 0}
+    orig = si.solve_ivp
+
+    def counting(fun, *a, **k):
+        def f(t, y):
+            calls["n"] += 1
+            return fun(t, y)
+        return orig(f, *a, **k)
+
+    import networks.gf_algorithms.samplers as smp
+    smp.integrate.solve_ivp = counting
+    try:
+        with NoiseFeed(prior, np.zeros((0,), np.float32)):
+            pose, q = agent.pred_func(dict(d), repeat_num=K, T0=T0, init_x=init_x.clone())
+    finally:
+        smp.integrate.solve_ivp = orig
+    out.update(ode_pred_pose=pose.numpy(), ode_pred_q=q.numpy(), ode_nfev=np.int64(calls["n"]))
+    np.savez_compressed(os.path.join(HERE, "golden_tracking.npz"), **out)
+
+
 def main():
+    only = sys.argv[1] if len(sys.argv) > 1 else None      # e.g. "tracking": that fixture only
     get_config, PoseNet = import_reference("pc", 20)
+    if only == "tracking":
+        gen_tracking(get_config, PoseNet)
+        print("tracking done")
+        return
     gen_encoder(get_config, PoseNet)
     print("encoder done")
     gen_heads(get_config, PoseNet)

@@ -196,6 +196,26 @@ def test_ode_pred_func_vs_golden(tag, rot_tol, tr_rel):
     assert np.abs(q.cpu().numpy()[..., :4] - g[f"{tag}_pred_q"][..., :4]).max() < rot_tol * 10
 
 
+@pytest.mark.parametrize("mode", ["pc", "ode"])
+def test_tracking_warm_start_vs_golden(mode):
+    """init_x + T0=0.2 as the tracking runner calls pred_func."""
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("tracking")
+    K, T, T0 = int(g["K"]), int(g["T"]), float(g["T0"])
+    agent = PoseNet(GenPoseConfig(device=DEV, sampler_mode=[mode], sampling_steps=T if mode == "pc" else None))
+    agent.noise_feed = NoiseFeed(*(torch.from_numpy(g[k]) for k in ("prior", "z1", "z2")))
+    data = {"pts": torch.from_numpy(g["pts"]).to(DEV), "pts_center": torch.from_numpy(g["pts_center"]).to(DEV)}
+    pose, q = agent.pred_func(data, repeat_num=K, T0=T0, init_x=torch.from_numpy(g["init_x"]).to(DEV))
+    ref = g[f"{mode}_pred_pose"]
+    p = pose.cpu().numpy()
+    assert np.abs(p[..., :6] - ref[..., :6]).max() < 1e-4
+    assert rel(p[..., 6:], ref[..., 6:]) < 1e-5
+    assert np.abs(q.cpu().numpy()[..., :4] - g[f"{mode}_pred_q"][..., :4]).max() < 1e-3
+    if mode == "ode":
+        assert agent.last_nfev == int(g["ode_nfev"])
+
+
 # ---------------------------------------------------------------- energy / ranking / scale
 def test_energy_ranking_aggregate_scale_vs_golden():
     from genpose2_amd import aggregate

@@ -77,6 +77,21 @@ def test_ode_pred_func(tag, rot_tol, tr_rel, score_sd):
         assert np.abs(xs - g[f"{tag}_xs"]).max() < 1e-5 * np.abs(g[f"{tag}_xs"]).max()
 
 
+def test_tracking_warm_start(score_sd):
+    """init_x + small T0 (runners/evaluation_tracking.py:110-127)."""
+    g = golden("tracking")
+    K, T, T0 = int(g["K"]), int(g["T"]), float(g["T0"])
+    pose, q, _, _ = oracle.pred_func(score_sd, g["pts"], g["pts_center"], K, T, "pc", g["prior"], g["z1"], g["z2"],
+                                     T0=T0, init_x=g["init_x"])
+    assert np.abs(pose[..., :6] - g["pc_pred_pose"][..., :6]).max() < 1e-4
+    assert rel(pose[..., 6:], g["pc_pred_pose"][..., 6:]) < 1e-5
+    pose, q, _, ex = oracle.pred_func(score_sd, g["pts"], g["pts_center"], K, None, "ode", g["prior"], T0=T0,
+                                      init_x=g["init_x"])
+    assert np.abs(pose[..., :6] - g["ode_pred_pose"][..., :6]).max() < 1e-4
+    assert rel(pose[..., 6:], g["ode_pred_pose"][..., 6:]) < 1e-5
+    assert ex["nfev"] == int(g["ode_nfev"])
+
+
 def test_energy_sort_aggregate_scale(energy_sd, scale_sd):
     g = golden("pipeline")
     e = oracle.get_energy(energy_sd, g["pts"], g["pts_center"], g["pred_pose"], 1e-5)
