@@ -25,7 +25,12 @@ int gp_check_launch(const char* what);
 // D = A(16x4) * B(4x16) + C.  Lane l supplies A[l&15][l>>4] and B[l>>4][l&15]; C/D lane l
 // holds rows 4*(l>>4)+j, column l&15 (j = register 0..3).
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+#ifdef GP_DIAG_NO_MFMA   // diagnostic builds only: one VALU FMA instead (results are meaningless)
+    c.x = __builtin_fmaf(a, b, c.x);
+    return c;
+#else
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+#endif
 }
 
 // One 16-deep k-group: 4 MFMAs with the lane's A float4 / B float4 (k = 16g + 4q + j).
@@ -49,7 +54,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
 }
 // 16-byte buffer load: voffset per lane (VGPR), soffset wave-uniform (SGPR).
 __device__ __forceinline__ f32x4 ldbuf4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+#ifdef GP_DIAG_NO_WLOAD   // diagnostic builds only: no weight stream (results are meaningless)
+    (void)r;
+    const float v = (float)(voff + soff) * 1e-9f;
+    return f32x4{v, v, v, v};
+#else
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+#endif
 }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 

@@ -33,6 +33,9 @@ constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
 #ifndef EVAL_WV
 #define EVAL_WV 8                // waves per workgroup, score/energy evaluation
 #endif
+#ifndef PC_D2
+#define PC_D2 3                  // k-groups of pose_encoder.2 weights kept in flight
+#endif
 #ifndef HEAD_PREFETCH
 #define HEAD_PREFETCH 2          // k-groups of head-layer-1 weights kept in flight
 #endif
@@ -168,7 +171,7 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
     const int voff = lane * 16;
     const __amdgpu_buffer_rsrc_t W2 = make_rsrc(w.pe2_w, HID * HID * 4);
     const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_w, 3 * HID * HID * 4);
-    constexpr int D2 = 3, DH = HEAD_PREFETCH;
+    constexpr int D2 = PC_D2, DH = HEAD_PREFETCH;
     int T2[TPW], TH[3 * TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) T2[t] = wid * TPW + t;
