@@ -78,7 +78,7 @@ constexpr int SA_THREADS = 256;
 // tiles split the workgroup's columns over waves instead of leaving waves idle.
 template <int CT, int CTW, int TC, int SPAN>
 __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int b, int col0, int cbase,
-                                         int wt, int WT) {
+                                         int wt, int WT, int ibeg, int iend) {
     const int lane = threadIdx.x & 63;
     const int q = lane >> 4, nn = lane & 15;
     const int KG = a.kg[L], NT = a.nt[L];
@@ -116,13 +116,12 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
             bx[c] = v;
         }
     }
-    // this wave's output tiles wt, wt+WT, wt+2WT, ... (round robin keeps waves within one tile
-    // of each other), TC of them per pass
-    const int cnt = NT > wt ? (NT - wt + WT - 1) / WT : 0;
-    for (int i0 = 0; i0 < cnt; i0 += TC) {
+    // entries [ibeg, iend) of this wave's output tiles wt, wt+WT, wt+2WT, ... (round robin keeps
+    // waves within one tile of each other), TC of them per pass
+    for (int i0 = ibeg; i0 < iend; i0 += TC) {
         int Tt[TC];
 #pragma unroll
-        for (int t = 0; t < TC; ++t) Tt[t] = (i0 + t < cnt) ? wt + (i0 + t) * WT : NT;   // NT = none
+        for (int t = 0; t < TC; ++t) Tt[t] = (i0 + t < iend) ? wt + (i0 + t) * WT : NT;   // NT = none
         f32x4 acc[TC][CTW];
 #pragma unroll
         for (int t = 0; t < TC; ++t)
@@ -267,23 +266,28 @@ __device__ __forceinline__ void sa_gather0(const SAArgs& a, f32x4* lds, int b, i
     }
 }
 
-// A layer with exactly the wave's tile count per pass where an instantiation exists (a pass of TC
-// tiles computes all TC accumulators, so a short last pass would burn MFMAs on absent tiles).
+// A layer in passes whose tile counts match the wave's tiles exactly (a pass of TC tiles computes
+// all TC accumulators, so a short last pass would burn MFMAs on absent tiles).
 template <int CT, int CTW, int SPAN, int MAXTC>
 __device__ __forceinline__ void sa_layer_fit(const SAArgs& a, f32x4* lds, int L, int b, int col0, int cbase, int wt,
                                              int WT) {
     const int nt = a.nt[L];
     const int cnt = nt > wt ? (nt - wt + WT - 1) / WT : 0;
     if constexpr (MAXTC >= 8) {
-        if (cnt == 8) return sa_layer<CT, CTW, 8, SPAN>(a, lds, L, b, col0, cbase, wt, WT);
+        if (cnt == 8) return sa_layer<CT, CTW, 8, SPAN>(a, lds, L, b, col0, cbase, wt, WT, 0, cnt);
     }
     if constexpr (MAXTC >= 7) {
-        if (cnt == 7) return sa_layer<CT, CTW, 7, SPAN>(a, lds, L, b, col0, cbase, wt, WT);
+        if (cnt == 7) return sa_layer<CT, CTW, 7, SPAN>(a, lds, L, b, col0, cbase, wt, WT, 0, cnt);
     }
     if constexpr (MAXTC >= 6) {
-        if (cnt == 6) return sa_layer<CT, CTW, 6, SPAN>(a, lds, L, b, col0, cbase, wt, WT);
+        if (cnt == 6) return sa_layer<CT, CTW, 6, SPAN>(a, lds, L, b, col0, cbase, wt, WT, 0, cnt);
     }
-    sa_layer<CT, CTW, 4, SPAN>(a, lds, L, b, col0, cbase, wt, WT);
+    // passes of 4 tiles, then the remainder as one exact pass
+    const int full = cnt & ~3, rem = cnt - full;
+    if (full) sa_layer<CT, CTW, 4, SPAN>(a, lds, L, b, col0, cbase, wt, WT, 0, full);
+    if (rem == 1) sa_layer<CT, CTW, 1, SPAN>(a, lds, L, b, col0, cbase, wt, WT, full, cnt);
+    else if (rem == 2) sa_layer<CT, CTW, 2, SPAN>(a, lds, L, b, col0, cbase, wt, WT, full, cnt);
+    else if (rem == 3) sa_layer<CT, CTW, 3, SPAN>(a, lds, L, b, col0, cbase, wt, WT, full, cnt);
 }
 
 template <int CT, int TC, int SPAN, int MAXTC>
