@@ -79,7 +79,7 @@ def test_encoder_levels_vs_golden(tag, score_agent):
     assert rel(feat, g[f"{tag}_feat"]) < 1e-5
 
 
-@pytest.mark.parametrize("n,grid", [(1024, True), (2048, True), (1500, False), (600, True)])
+@pytest.mark.parametrize("n,grid", [(1024, True), (2048, True), (1500, False), (600, True), (4096, True)])
 def test_encoder_fps_chain_vs_oracle(n, grid, score_agent):
     """The encoder's per-object FPS chain (one wave per object) vs the serialized oracle, level by
     level, on tie-heavy integer grids and ragged sizes."""
