@@ -43,27 +43,36 @@ __device__ __forceinline__ unsigned long long fps_pack(float d2, uint32_t key) {
 
 constexpr int FPS_THREADS = 256;
 
-// Wave-wide max of a 64-bit key with DPP row operations (quad perms, half/full row mirror,
-// row_bcast15/31) instead of 6 ds_bpermute shuffle rounds; the result is read from lane 63.
-#define GP_DPP_MAX_STEP(CTRL, ROWMASK)                                                          \
+// Wave-wide max of a 64-bit key: DPP steps within each 16-lane row (quad perms, half/full row
+// mirror), then the gfx950 row swaps (v_permlane16_swap / v_permlane32_swap) across rows. Every
+// lane ends with the maximum; one 64-bit compare per step.
+#define GP_DPP_MAX_STEP(CTRL)                                                                   \
     {                                                                                           \
-        const uint32_t ohi = (uint32_t)__builtin_amdgcn_update_dpp((int)hi, (int)hi, CTRL, ROWMASK, 0xF, false); \
-        const uint32_t olo = (uint32_t)__builtin_amdgcn_update_dpp((int)lo, (int)lo, CTRL, ROWMASK, 0xF, false); \
-        const bool take = (ohi > hi) || (ohi == hi && olo > lo);                                 \
+        const uint32_t ohi = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xF, 0xF, false); \
+        const uint32_t olo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xF, 0xF, false); \
+        const bool take = (((unsigned long long)ohi << 32) | olo) > (((unsigned long long)hi << 32) | lo); \
         hi = take ? ohi : hi;                                                                   \
         lo = take ? olo : lo;                                                                   \
+    }
+#define GP_SWAP_MAX_STEP(SWAP)                                                                  \
+    {                                                                                           \
+        const auto h = SWAP(hi, hi, false, false);                                              \
+        const auto l = SWAP(lo, lo, false, false);                                              \
+        const bool take = (((unsigned long long)h[1] << 32) | l[1]) > (((unsigned long long)h[0] << 32) | l[0]); \
+        hi = take ? h[1] : h[0];                                                                \
+        lo = take ? l[1] : l[0];                                                                \
     }
 
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
     uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-    GP_DPP_MAX_STEP(0xB1, 0xF)   // quad_perm [1,0,3,2]
-    GP_DPP_MAX_STEP(0x4E, 0xF)   // quad_perm [2,3,0,1]
-    GP_DPP_MAX_STEP(0x141, 0xF)  // row_half_mirror
-    GP_DPP_MAX_STEP(0x140, 0xF)  // row_mirror
-    GP_DPP_MAX_STEP(0x142, 0xA)  // row_bcast:15 -> rows 1, 3
-    GP_DPP_MAX_STEP(0x143, 0xC)  // row_bcast:31 -> rows 2, 3
-    const uint32_t rhi = (uint32_t)__builtin_amdgcn_readlane((int)hi, 63);
-    const uint32_t rlo = (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+    GP_DPP_MAX_STEP(0xB1)   // quad_perm [1,0,3,2]
+    GP_DPP_MAX_STEP(0x4E)   // quad_perm [2,3,0,1]
+    GP_DPP_MAX_STEP(0x141)  // row_half_mirror
+    GP_DPP_MAX_STEP(0x140)  // row_mirror
+    GP_SWAP_MAX_STEP(__builtin_amdgcn_permlane16_swap)
+    GP_SWAP_MAX_STEP(__builtin_amdgcn_permlane32_swap)
+    const uint32_t rhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
+    const uint32_t rlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
     return ((unsigned long long)rhi << 32) | rlo;
 }
 
