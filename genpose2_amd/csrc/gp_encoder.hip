@@ -233,10 +233,20 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
 template <int CT>
 __device__ __forceinline__ void sa_gather0(const SAArgs& a, f32x4* lds, int b, int col0) {
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int q = lane >> 4, nn = lane & 15;
-    const int NT0 = a.nt[0], KG0 = a.kg[0], gx = a.c_prev >> 4;
+    const int NT0 = a.nt[0], KG0 = a.kg[0], gx = a.c_prev >> 4, H0p = NT0 * 16;
     const f32x4* w0 = reinterpret_cast<const f32x4*>(a.w[0]);
+    // W0_xyz . x_c for this workgroup's centroids, once, into the (still unused) second buffer
+    const int mfirst = col0 / a.ns;
+    const int mlast = min((col0 + CT * 16 - 1) / a.ns, a.m - 1);
+    float* cx = reinterpret_cast<float*>(lds + a.buf1_off);
+    for (int e = tid; e < (mlast - mfirst + 1) * H0p; e += SA_THREADS) {
+        const int c = e / H0p, ch = e - (e / H0p) * H0p;
+        const float* cc = a.cent + ((size_t)b * a.m + mfirst + c) * 3;
+        const f32x4 w = w0[((ch >> 4) * KG0 + gx) * 64 + (ch & 15)];   // W0[ch][c_prev + 0..2]
+        cx[e] = (w.x * cc[0] + w.y * cc[1]) + w.z * cc[2];
+    }
     int pcol[CT], mcol[CT];
     bool ok[CT];
 #pragma unroll
@@ -244,25 +254,35 @@ __device__ __forceinline__ void sa_gather0(const SAArgs& a, f32x4* lds, int b, i
         const int col = col0 + ct * 16 + nn;
         ok[ct] = col < a.cols;
         const int m = ok[ct] ? col / a.ns : 0, s = ok[ct] ? col - (col / a.ns) * a.ns : 0;
-        mcol[ct] = m;
+        mcol[ct] = m - mfirst;
         pcol[ct] = ok[ct] ? a.nbr[((size_t)b * a.m + m) * a.ns + s] : 0;
     }
-    for (int pr = wid; pr < NT0 * CT; pr += 4) {
-        const int T = pr / CT, ct = pr - (pr / CT) * CT;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (ok[ct]) {
-            const f32x4 qv = ld4(a.qin + ((size_t)b * a.n_prev + pcol[ct]) * a.q_stride + a.q_off + 16 * T + 4 * q);
-            const float* cc = a.cent + ((size_t)b * a.m + mcol[ct]) * 3;
-            const float cx = cc[0], cy = cc[1], cz = cc[2];
-            float r[4];
+    __syncthreads();
+    // this wave's (output tile, column tile) pairs, 8 at a time: all Q gathers in flight first
+    constexpr int PB = 8;
+    for (int p0 = wid; p0 < NT0 * CT; p0 += 4 * PB) {
+        f32x4 qv[PB];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const f32x4 wx = w0[(T * KG0 + gx) * 64 + 4 * q + j];   // W0[16T+4q+j][c_prev + 0..2]
-                r[j] = fmaxf(qv[j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
-            }
-            v = f32x4{r[0], r[1], r[2], r[3]};
+        for (int u = 0; u < PB; ++u) {
+            const int pr = p0 + 4 * u;
+            const int T = pr / CT, ct = pr - (pr / CT) * CT;
+            qv[u] = (pr < NT0 * CT && ok[ct])
+                        ? ld4(a.qin + ((size_t)b * a.n_prev + pcol[ct]) * a.q_stride + a.q_off + 16 * T + 4 * q)
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        lds[(T * CT + ct) * 64 + lane] = v;
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+            const int pr = p0 + 4 * u;
+            if (pr >= NT0 * CT) break;
+            const int T = pr / CT, ct = pr - (pr / CT) * CT;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (ok[ct]) {
+                const f32x4 c4 = ld4(cx + mcol[ct] * H0p + 16 * T + 4 * q);
+                v = f32x4{fmaxf(qv[u].x - c4.x, 0.f), fmaxf(qv[u].y - c4.y, 0.f), fmaxf(qv[u].z - c4.z, 0.f),
+                          fmaxf(qv[u].w - c4.w, 0.f)};
+            }
+            lds[(T * CT + ct) * 64 + lane] = v;
+        }
     }
 }
 
