@@ -37,61 +37,72 @@ __device__ __forceinline__ int fps_key_to_k(uint32_t key, int nb, int jbits) {
     return (int)(t + ((key & ((1u << jbits) - 1u)) << nb));
 }
 
-__device__ __forceinline__ unsigned long long fps_pack(float d2, uint32_t key) {
-    return ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned long long)(0xFFFFFFFFu - key);
-}
-
 constexpr int FPS_THREADS = 256;
-
-// Wave-wide max of a 64-bit key: DPP steps within each 16-lane row (quad perms, half/full row
-// mirror), then the gfx950 row swaps (v_permlane16_swap / v_permlane32_swap) across rows. Every
-// lane ends with the maximum; one 64-bit compare per step.
-#define GP_DPP_MAX_STEP(CTRL)                                                                   \
-    {                                                                                           \
-        const uint32_t ohi = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xF, 0xF, false); \
-        const uint32_t olo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xF, 0xF, false); \
-        const bool take = (((unsigned long long)ohi << 32) | olo) > (((unsigned long long)hi << 32) | lo); \
-        hi = take ? ohi : hi;                                                                   \
-        lo = take ? olo : lo;                                                                   \
-    }
-#define GP_SWAP_MAX_STEP(SWAP)                                                                  \
-    {                                                                                           \
-        const auto h = SWAP(hi, hi, false, false);                                              \
-        const auto l = SWAP(lo, lo, false, false);                                              \
-        const bool take = (((unsigned long long)h[1] << 32) | l[1]) > (((unsigned long long)h[0] << 32) | l[0]); \
-        hi = take ? h[1] : h[0];                                                                \
-        lo = take ? l[1] : l[0];                                                                \
-    }
-
-__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
-    uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-    GP_DPP_MAX_STEP(0xB1)   // quad_perm [1,0,3,2]
-    GP_DPP_MAX_STEP(0x4E)   // quad_perm [2,3,0,1]
-    GP_DPP_MAX_STEP(0x141)  // row_half_mirror
-    GP_DPP_MAX_STEP(0x140)  // row_mirror
-    GP_SWAP_MAX_STEP(__builtin_amdgcn_permlane16_swap)
-    GP_SWAP_MAX_STEP(__builtin_amdgcn_permlane32_swap)
-    const uint32_t rhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
-    const uint32_t rlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
-    return ((unsigned long long)rhi << 32) | rlo;
-}
 
 constexpr int FPS_RED_BYTES = 2 * 16 * 8;   // double-buffered per-wave 64-bit maxima, up to 16 waves
 
+// The packed (distance, ~key) pair read as an f64. Its high word is a finite non-negative f32, so
+// the pattern is a finite non-negative double (exponent field <= 0x7F7, never NaN/Inf) and f64
+// order equals the unsigned order of the 64-bit pattern, denormals included (the kernels run with
+// f64 denormals preserved: float_denorm_mode_16_64 = 3). One v_max_f64 therefore does the work of
+// a 64-bit compare plus two selects. Inline asm keeps LLVM from canonicalising the DPP'd inputs.
+__device__ __forceinline__ double fps_pack_f64(float d2, uint32_t low) {
+    return __hiloint2double(__float_as_int(d2), (int)low);
+}
+
+__device__ __forceinline__ double fps_max(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double fps_dpp(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// Wave-wide max (every lane ends with it): DPP within each 16-lane row, then the gfx950 row
+// swaps (v_permlane16_swap / v_permlane32_swap) across rows.
+__device__ __forceinline__ double fps_wave_max(double v) {
+    v = fps_max(v, fps_dpp<0xB1>(v));    // quad_perm [1,0,3,2]
+    v = fps_max(v, fps_dpp<0x4E>(v));    // quad_perm [2,3,0,1]
+    v = fps_max(v, fps_dpp<0x141>(v));   // row_half_mirror
+    v = fps_max(v, fps_dpp<0x140>(v));   // row_mirror
+    {
+        const auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+        const auto l = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+        v = fps_max(__hiloint2double(h[0], l[0]), __hiloint2double(h[1], l[1]));
+    }
+    {
+        const auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+        const auto l = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+        v = fps_max(__hiloint2double(h[0], l[0]), __hiloint2double(h[1], l[1]));
+    }
+    return v;
+}
+
 // One FPS run over `n` points held in LDS (s_xyz, xyz interleaved). Writes the m indices to
-// s_idx and the selected coordinates to s_out (both LDS; s_out may be null). Nothing touches
-// global memory inside the iteration loop, so the per-iteration barrier never waits on a store.
-// All NTH threads must call it. s_red holds FPS_RED_BYTES.
+// s_idx and, after the loop, the selected coordinates to s_out (both LDS; s_out may be null).
+// Nothing touches global memory inside the iteration loop, so the per-iteration barrier never
+// waits on a store. All NTH threads must call it. s_red holds FPS_RED_BYTES.
+// Per iteration: distance update + local max of packed pairs, a wave max (6 DPP/swap steps),
+// one barrier, then a DPP tree over the per-wave maxima (lane i reads wave i % NW) and the key
+// decode on the scalar unit. Points past n carry the packed value 0 (distance 0, low word 0), which
+// never beats a real point, so the loop has no bounds branches.
 // Measured slower and not kept (level 0 at B=64): carrying the winner's coordinates through the
 // exchange instead of re-reading them from s_xyz (411 vs 327 us); two 32-bit DPP maxima (distance,
 // then key) instead of one 64-bit maximum of the packed pair (436 vs 309 us).
 template <int PMAX, int NTH = FPS_THREADS>
 __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits, void* s_red_v, int* s_idx,
                         float* s_out) {
-    unsigned long long* s_red = reinterpret_cast<unsigned long long*>(s_red_v);
+    constexpr int NW = NTH / 64;
+    static_assert(NW >= 1 && NW <= 16 && (NW & (NW - 1)) == 0, "NTH must be 64 * 2^k, at most 1024");
+    double* s_red = reinterpret_cast<double*>(s_red_v);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     float px[PMAX], py[PMAX], pz[PMAX], tmin[PMAX];
-    uint32_t key[PMAX];
+    uint32_t low[PMAX];
 #pragma unroll
     for (int p = 0; p < PMAX; ++p) {
         const int k = tid + p * NTH;
@@ -99,37 +110,43 @@ __device__ void fps_run(const float* s_xyz, int n, int m, int nb, int jbits, voi
         px[p] = ok ? s_xyz[3 * k + 0] : 0.f;
         py[p] = ok ? s_xyz[3 * k + 1] : 0.f;
         pz[p] = ok ? s_xyz[3 * k + 2] : 0.f;
-        tmin[p] = 1e10f;                        // pointnet2_utils.py:32-34
-        key[p] = ok ? fps_key(k, nb, jbits) : 0u;
+        tmin[p] = ok ? 1e10f : 0.f;             // pointnet2_utils.py:32-34
+        low[p] = ok ? 0xFFFFFFFFu - fps_key(k, nb, jbits) : 0u;
     }
-    int old = 0;
     if (m <= 0) return;
     if (tid == 0) s_idx[0] = 0;
-    if (tid < 3 && s_out) s_out[tid] = s_xyz[tid];
+    const uint32_t kmask = (1u << jbits) - 1u;
+    int old = 0;
     for (int j = 1; j < m; ++j) {
         const float x1 = s_xyz[3 * old + 0], y1 = s_xyz[3 * old + 1], z1 = s_xyz[3 * old + 2];
-        unsigned long long best = 0ull;
+        double best;
 #pragma unroll
         for (int p = 0; p < PMAX; ++p) {
-            const int k = tid + p * NTH;
-            if (k < n) {
-                const float d = dist2_ref(px[p], py[p], pz[p], x1, y1, z1);
-                const float d2 = fminf(d, tmin[p]);
-                tmin[p] = d2;
-                const unsigned long long c = fps_pack(d2, key[p]);
-                best = c > best ? c : best;
-            }
+            const float d = dist2_ref(px[p], py[p], pz[p], x1, y1, z1);
+            const float d2 = fminf(d, tmin[p]);
+            tmin[p] = d2;
+            best = p ? fps_max(best, fps_pack_f64(d2, low[p])) : fps_pack_f64(d2, low[p]);
         }
-        best = wave_max_u64(best);
-        unsigned long long* red = s_red + (j & 1) * 16;
+        best = fps_wave_max(best);
+        double* red = s_red + (j & 1) * 16;
         if (lane == 0) red[wid] = best;
         __syncthreads();
-        unsigned long long b = red[0];
-#pragma unroll
-        for (int w = 1; w < NTH / 64; ++w) b = red[w] > b ? red[w] : b;
-        old = fps_key_to_k(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull), nb, jbits);
+        double v = red[lane & (NW - 1)];
+        if constexpr (NW >= 2) v = fps_max(v, fps_dpp<0xB1>(v));
+        if constexpr (NW >= 4) v = fps_max(v, fps_dpp<0x4E>(v));
+        if constexpr (NW >= 8) v = fps_max(v, fps_dpp<0x141>(v));
+        if constexpr (NW >= 16) v = fps_max(v, fps_dpp<0x140>(v));
+        const uint32_t key = 0xFFFFFFFFu - (uint32_t)__builtin_amdgcn_readfirstlane(__double2loint(v));
+        const uint32_t rt = key >> jbits;
+        const uint32_t t = nb ? (__builtin_bitreverse32(rt) >> (32 - nb)) : 0u;
+        old = (int)(t + ((key & kmask) << nb));
         if (tid == 0) s_idx[j] = old;
-        if (tid < 3 && s_out) s_out[3 * j + tid] = s_xyz[3 * old + tid];
+    }
+    if (s_out) {
+        __syncthreads();
+        for (int i = tid; i < 3 * m; i += NTH) {
+            const int j = i / 3;
+            s_out[i] = s_xyz[3 * s_idx[j] + (i - 3 * j)];
+        }
     }
 }
-
