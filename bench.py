@@ -103,6 +103,28 @@ def load_traffic(rows):
     return None
 
 
+def report_ode(args, B, N, K, ws, rank, elapsed, nfevs, cfgd):
+    """ODE sampler line (report nfev and B*K*nfev/s). The whole pred_func is timed
+    (encoder + RK45 on device + host step controller, one 8-byte read per attempted step)."""
+    from genpose2_amd import arch
+    nfev = float(np.mean(nfevs))
+    units = B * K * ws * float(np.sum(nfevs))
+    per_call = elapsed / args.steps
+    flop = B * K * arch.score_flops_per_candidate_step() * float(np.sum(nfevs))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "pose candidate-RHS evaluations/sec (B objs x K cands x nfev, ODE sampler)",
+            "value": units / elapsed, "unit": "pose-candidate-evals/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": per_call * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64 state / f32 score", "data": "synthetic",
+            "config": {"workload": f"config{args.config} shape, ODE sampler: B={B} objects/GPU, N={N} pts, K={K}, "
+                                   f"T0={args.t0}, RK45 rtol=atol=1e-5 (encoder + sampler per step)",
+                       "global_batch": B * ws, "seq_len": nfev, "parallelism": f"dp{ws} (object shards)"},
+            "nfev": nfev, "poses_per_s": B * K * ws / per_call,
+            "effective_score_tflops": flop / ws / elapsed / 1e12 * ws,
+        }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,6 +133,10 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sampler", choices=["pc", "ode"], default="pc",
+                    help="ode: the shipped evaluation's sampler (scripts/eval_single.sh: --sampler_mode ode "
+                         "--T0 0.55, sampling_steps unset); reports B*K*nfev/s")
+    ap.add_argument("--t0", type=float, default=0.55)
     args = ap.parse_args()
     cfgd = CONFIGS[args.config]
     ws, rank, local = dist_env()
@@ -125,7 +151,9 @@ def main():
     from genpose2_amd.config import GenPoseConfig
 
     B, N, K, T = cfgd["B"], cfgd["N"], cfgd["K"], cfgd["T"]
-    cfg = GenPoseConfig(device=str(dev), sampling_steps=T, eval_repeat_num=K, noise_seed=1234 + rank)
+    ode = args.sampler == "ode"
+    cfg = GenPoseConfig(device=str(dev), sampling_steps=None if ode else T, eval_repeat_num=K,
+                        noise_seed=1234 + rank, sampler_mode=[args.sampler])
     score = PoseNet(cfg).eval()
     broadcast_weights(score, ws)
     energy = PoseNet(cfg.copy(agent_type="energy")).eval() if cfgd["energy"] else None
@@ -139,6 +167,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(device=dev)
     samp_ev = []
+    nfevs = []
 
     def one_step(record=False):
         data = dict(data0)
@@ -153,7 +182,7 @@ def main():
                 with torch.cuda.stream(side):
                     energy.encode_func(edata)
             score.after_encode = start_energy_encoder
-        if record:
+        if record and not ode:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             # bracket only the PC sampler launches (pc_step_kernel x (T+1)) on the launch stream
@@ -165,8 +194,10 @@ def main():
                 e1.record(stream)
                 return out
             score.heads.pc_sample = timed
-        pose, _ = score.pred_func(data, repeat_num=K)
-        if record:
+        pose, _ = score.pred_func(data, repeat_num=K, T0=args.t0 if ode else None)
+        if ode:
+            nfevs.append(score.last_nfev)
+        if record and not ode:
             score.heads.pc_sample = orig
             samp_ev.append((e0, e1))
         if energy is not None:
@@ -201,6 +232,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if ode:
+        report_ode(args, B, N, K, ws, rank, elapsed, nfevs[-args.steps:], cfgd)
+        if ws > 1:
+            dist.destroy_process_group()
+        return
     units = B * K * T * ws * args.steps
     samp_ms = float(np.mean([a.elapsed_time(b) for a, b in samp_ev]))
     per_launch_s = samp_ms / 1e3 / (T + 1)

@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GENPOSE_HIP_LIB", os.path.join(_HERE, "libgenpose_hip.so"))
 
 c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+c_double = ctypes.c_double
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
 c_uint64 = ctypes.c_uint64
 
@@ -54,6 +55,18 @@ _SIGS: Dict[str, tuple] = {
                              c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_float, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_size_t, c_void_p]),
     "gp_pose_epilogue_f64": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "gp_ode_workspace_size": (c_size_t, [c_int]),
+    "gp_ode_rhs": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_float, c_float, c_double, c_void_p, c_void_p,
+                           c_void_p, c_int, c_double, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gp_ode_attempt": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_double, c_double, c_int, c_int,
+                               c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gp_ode_init_norms": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_double, c_double, c_void_p,
+                                  c_void_p]),
+    "gp_ode_dense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_double, c_double,
+                             ctypes.c_longlong, c_void_p, c_void_p]),
+    "gp_ode_denoise": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_float, c_float, c_float, c_float, c_void_p,
+                               c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "gp_scale_forward": (c_int, [ctypes.POINTER(ScaleWeights), c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "gp_randn": (c_int, [c_uint64, ctypes.c_uint32, c_int, c_int, c_void_p, c_void_p]),
     "gp_rank_aggregate": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p,

@@ -17,7 +17,7 @@ import torch
 
 from . import aggregate, arch, device as dev, sde, weights
 from .config import GenPoseConfig
-from .ode import rk45_solve
+from .ode import DeviceRk45, rk45_drive, time_scalars
 
 
 def _as_config(cfg) -> GenPoseConfig:
@@ -159,7 +159,8 @@ class PoseNet:
             pred_q = q.view(bs, K, -1)
             in_process = xs.view(bs, K, T, -1) if xs is not None else None
         elif mode == "ode":
-            pred_pose, pred_q, in_process = self._ode(pobj, center, bs, K, rep_init, T0)
+            pred_pose, pred_q, in_process = self._ode(pobj, center, bs, K, rep_init, T0,
+                                                      bool(return_process or self.cfg.save_video))
         else:
             raise NotImplementedError(mode)
         self.pts_feature = False
@@ -174,8 +175,10 @@ class PoseNet:
             return [pred_pose, in_process]
         return pred_pose, pred_q
 
-    def _ode(self, pobj, center, bs, K, rep_init, T0):
-        """cond_ode_sampler (samplers.py:180-258) on device."""
+    def _ode(self, pobj, center, bs, K, rep_init, T0, want_process=False):
+        """cond_ode_sampler (samplers.py:180-258) on device: RK45 stages, error norms and dense
+        output are HIP launches (genpose2_amd/ode.py DeviceRk45); the controller runs scipy's step
+        logic on host scalars. Returns (pose (B,K,9) fp64, q (B,K,7) fp64, process or None)."""
         R = bs * K
         T0 = arch.SDE_T if T0 is None else float(T0)
         eps = arch.SAMPLING_EPS
@@ -183,36 +186,25 @@ class PoseNet:
         x0 = self._draw_prior(R) * sde.prior_sigma(T0)
         if rep_init is not None:
             x0 = rep_init.to(torch.float32) + x0
-        cache = {}
-        buf = torch.empty((R, arch.POSE_DIM), dtype=torch.float32, device=self.device)
-
-        def fun(t: float, y: torch.Tensor) -> torch.Tensor:
-            t32 = float(np.float32(t))
-            if t32 not in cache:
-                cache.clear()
-                cache[t32] = self._time_row_and_sigma(self.heads, t32)
-            trow, sig32 = cache[t32]
-            s = self.heads.score(pobj, trow, sig32, y.view(R, -1).to(torch.float32), K, out=buf)
-            g = float(sde.diffusion(torch.tensor(t, dtype=torch.float64)))
-            return -((0.5 * g * g) * s.to(torch.float64)).view(-1)
-
+        be = DeviceRk45(self.heads, pobj, x0.to(self.device), K)
         t_eval = None if steps is None else np.linspace(T0, eps, steps)
-        _, ys, nfev = rk45_solve(fun, T0, x0.reshape(-1).to(torch.float64), eps, t_eval=t_eval)
+        ts, nfev, _ = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process)
         self.last_nfev = nfev
-        n_t = ys.shape[0]
-        x = ys[-1].view(R, -1).clone()
-        # denoise with the PC predictor step (samplers.py:240-249)
-        trow, sig32 = self._time_row_and_sigma(self.heads, eps)
+        ys = be.outputs()                      # (n_t or 1, R*9) fp64
+        x = ys[-1]
+        # denoise with the PC predictor step (samplers.py:240-249), GS, + pts_center, quaternion
+        t32, sig, _ = time_scalars(eps)
         vec_eps = torch.full((1,), eps, dtype=torch.float32)
-        g32 = sde.diffusion(vec_eps).to(self.device)
-        grad = self.heads.score(pobj, trow, sig32, x.to(torch.float32).contiguous(), K)
-        drift = 0 - g32 ** 2 * grad
-        x = x + drift * ((1 - eps) / (1000 if steps is None else steps))
-        xs = ys.view(n_t * R, -1).clone()
-        xs, _ = dev.pose_epilogue_f64(xs, K, center.repeat(n_t, 1))  # row r -> object (r % R) // K
-        x, q = dev.pose_epilogue_f64(x.contiguous(), K, center)
-        in_process = xs.view(n_t, R, -1).permute(1, 0, 2).reshape(bs, K, n_t, -1)
-        return x.view(bs, K, -1), q.view(bs, K, -1), in_process
+        g2 = float(sde.diffusion(vec_eps).to(torch.float32) ** 2)
+        step = float(np.float32((1 - eps) / (1000 if steps is None else steps)))
+        pose, q = self.heads.ode_denoise(pobj, t32, sig, g2, step, x, K, center, be.ws)
+        in_process = None
+        if want_process:
+            n_t = ys.shape[0]
+            xs = ys.reshape(n_t * R, -1).clone()
+            xs, _ = dev.pose_epilogue_f64(xs, K, center.repeat(n_t, 1))  # row r -> object (r % R) // K
+            in_process = xs.view(n_t, R, -1).permute(1, 0, 2).reshape(bs, K, n_t, -1)
+        return pose.view(bs, K, -1), q.view(bs, K, -1), in_process
 
     # ------------------------------------------------------------------ get_energy
     @torch.no_grad()

@@ -1,0 +1,357 @@
+// Shared score-head trunk for gfx950: LDS layout, streamed-weight MFMA layers, and pose helpers.
+// Used by the PC sampler / score / energy kernels (gp_score.hip) and the ODE stage kernels
+// (gp_ode.hip). Reference: PoseScoreNet.forward (networks/gf_algorithms/scorenet.py:215-275).
+#pragma once
+#include "gp_common.h"
+
+constexpr int HT = 256;          // threads per workgroup
+constexpr int HID = 256;         // pose/head hidden width
+constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
+#ifndef PC_WV1
+#define PC_WV1 8                 // waves per workgroup, 16-candidate PC tiles
+#endif
+#ifndef PC_WV2
+#define PC_WV2 4                 // waves per workgroup, 32-candidate PC tiles
+#endif
+#ifndef EVAL_WV
+#define EVAL_WV 8                // waves per workgroup, score/energy evaluation
+#endif
+#ifndef PC_D2
+#define PC_D2 3                  // k-groups of pose_encoder.2 weights kept in flight
+#endif
+#ifndef HEAD_PREFETCH
+#define HEAD_PREFETCH 2          // k-groups of head-layer-1 weights kept in flight
+#endif
+
+
+// Phase stamps (PC_MARK) are defined by the including file; no-op by default.
+#ifndef PC_MARK
+#define PC_MARK(k) ((void)trace_slot)
+#endif
+
+
+// ============================================================================ shared head trunk
+// NT = column tiles (16 candidates each) per workgroup.
+template <int NT, int WV>
+struct HeadSmem {
+    float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
+    f32x4 act1[KG_HID * NT * 64];      // pose_encoder.0 output, accumulator-native [g][ct][lane]
+    f32x4 act2[KG_HID * NT * 64];      // pose_encoder.2 output
+    float red[NT * 16][9][WV];         // per-wave head-layer-2 partials, wave-minor (head_out reads a row)
+    float xu[NT * 16 * 9];             // PC update inputs: state x and score s of this tile's rows
+    float su[NT * 16 * 9];
+    float noise[NT * 16][2][12];       // PC corrector / predictor draws of this step
+    float scratch[WV * 64];
+    // small per-launch weights staged once per workgroup (their loads overlap the PC update)
+    f32x4 pe0w[16 * 64];               // pose_encoder.0 packed A fragments
+    float pe0b[HID], pe2b[HID];
+    float h2w[9 * HID];                // head layer 2, [head*3 + out][256]
+    float h2b[12];
+};
+
+// Threads [FIRST, WV*64) copy the small weights into LDS.
+template <int NT, int WV, int FIRST = 0>
+__device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, HeadSmem<NT, WV>& sm) {
+    constexpr int NTH = WV * 64 - FIRST;
+    const int t0 = (int)threadIdx.x - FIRST;
+    if (t0 < 0) return;
+    for (int i = t0; i < 16 * 64; i += NTH) sm.pe0w[i] = ld4(w.pe0_w + (size_t)i * 4);
+    for (int i = t0; i < HID; i += NTH) {
+        sm.pe0b[i] = w.pe0_b[i];
+        sm.pe2b[i] = w.pe2_b[i];
+    }
+    for (int i = t0; i < 9 * HID / 4; i += NTH) st4(&sm.h2w[i * 4], ld4(w.h2_w + (size_t)i * 4));
+    if (t0 < 9) sm.h2b[t0] = w.h2_b[t0];
+}
+
+// Head output o of column c (valid after head_trunk): bias + the per-wave partials in wave order.
+template <int NT, int WV>
+__device__ __forceinline__ float head_out(const HeadSmem<NT, WV>& sm, int c, int o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int v = 0; v < WV; ++v) acc += sm.red[c][o][v];
+    return sm.h2b[o] + acc;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// acc[t][ct] += sum_g A(tile T[t], k-group g) . B(k-group g, column tile ct) over KG k-groups.
+// A fragments stream from global (L2-resident packed weights) through a (D+1)-slot register ring
+// so that the loads of k-group g+D are in flight while k-group g feeds the MFMAs; B fragments
+// come from LDS. Loads are raw buffer loads: the tile/k-group offset is a wave-uniform SGPR
+// (soffset) and the only per-lane address is lane*16 (voffset), so the fully unrolled ring needs
+// no 64-bit address registers. Every ring index is a compile-time constant.
+// Steps G..GEND-1 of the pipelined stream (step G issues k-group G's loads and computes k-group
+// G-D). Steps 0..D-1 only prime the ring, so they can be issued early (before a barrier).
+template <int G, int GEND, int TT, int NT, int KG, int D>
+__device__ __forceinline__ void stream_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f32x4* __restrict__ B,
+                                            int lane, int voff, f32x4 (&ring)[D + 1][TT], f32x4 (&acc)[TT][NT]) {
+    if constexpr (G < GEND) {
+        if constexpr (G < KG) {
+#pragma unroll
+            for (int t = 0; t < TT; ++t) ring[G % (D + 1)][t] = ldbuf4(W, voff, (T[t] * KG + G) * 1024);
+        }
+        // keep the prefetch where it is: without this fence the scheduler sinks every load next to
+        // its MFMAs and waits vmcnt(0) per k-group (checked in the .s)
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (G >= D) {
+            constexpr int GG = G - D;
+            f32x4 bf[NT];
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) bf[ct] = B[(GG * NT + ct) * 64 + lane];
+            // k-step outermost: consecutive MFMAs hit different accumulators (16x16x4 f32 has a
+            // 40-cycle dependent latency vs a 32-cycle issue interval)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int t = 0; t < TT; ++t)
+#pragma unroll
+                    for (int ct = 0; ct < NT; ++ct)
+                        acc[t][ct] = mfma4(ring[GG % (D + 1)][t][j], bf[ct][j], acc[t][ct]);
+        }
+        stream_step<G + 1, GEND, TT, NT, KG, D>(W, T, B, lane, voff, ring, acc);
+    }
+}
+
+// acc[t][ct] += sum_g A(tile T[t], k-group g) . B(k-group g, column tile ct) over KG k-groups.
+// A fragments stream from global (L2-resident packed weights) through a (D+1)-slot register ring
+// so that the loads of k-group g+D are in flight while k-group g feeds the MFMAs; B fragments
+// come from LDS. Loads are raw buffer loads: the tile/k-group offset is a wave-uniform SGPR
+// (soffset) and the only per-lane address is lane*16 (voffset). The k-group loop is unrolled by
+// template recursion, so every ring index is a compile-time constant (no scratch).
+template <int TT, int NT, int KG, int D>
+__device__ __forceinline__ void stream_layer(__amdgpu_buffer_rsrc_t W, const int (&T)[TT],
+                                             const f32x4* __restrict__ B, int lane, f32x4 (&acc)[TT][NT]) {
+    f32x4 ring[D + 1][TT];
+    stream_step<0, KG + D, TT, NT, KG, D>(W, T, B, lane, lane * 16, ring, acc);
+}
+
+// Computes the head outputs (read with head_out) for the candidates of this workgroup. Starts with
+// the workgroup barrier that publishes sm.xin, obj_of_col and the staged weights (callers write
+// them before the call without a barrier of their own; the first weight loads are issued before it).
+// `obj_of_col` maps column -> object row of pobj; `tproj` is the 768-vector of this time value.
+template <int NT, int WV>
+__device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float* __restrict__ pobj,
+                           const float* __restrict__ tproj, const int* obj_of_col, HeadSmem<NT, WV>& sm,
+                           int trace_slot = 0) {
+    constexpr int TPW = 16 / WV;   // output tiles per wave and per 256-wide layer
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
+    const int q = lane >> 4, n = lane & 15;
+    const int voff = lane * 16;
+    const __amdgpu_buffer_rsrc_t W2 = make_rsrc(w.pe2_w, HID * HID * 4);
+    const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_w, 3 * HID * HID * 4);
+    constexpr int D2 = PC_D2, DH = HEAD_PREFETCH;
+    int T2[TPW], TH[3 * TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) T2[t] = wid * TPW + t;
+#pragma unroll
+    for (int h = 0; h < 3; ++h)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) TH[h * TPW + t] = h * 16 + wid * TPW + t;
+    f32x4 acc2[TPW][NT];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) acc2[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 ring2[D2 + 1][TPW];
+    // prime pose_encoder.2's weight ring before pose_encoder.0 (no B operand read yet)
+    stream_step<0, D2, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
+    __syncthreads();
+    PC_MARK(1);
+    // ---- pose_encoder.0 (9 -> 256), one k-group
+    {
+        f32x4 bf[NT];
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) bf[ct] = ld4(&sm.xin[(ct * 16 + n) * 16 + 4 * q]);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const int T = wid * TPW + t;
+            const f32x4 a = sm.pe0w[T * 64 + lane];
+            const f32x4 bias = ld4(&sm.pe0b[16 * T + 4 * q]);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct)
+                sm.act1[(T * NT + ct) * 64 + lane] = relu4(mfma_kgroup(a, bf[ct], f32x4{0.f, 0.f, 0.f, 0.f}) + bias);
+        }
+    }
+    __syncthreads();
+    PC_MARK(2);
+    // ---- pose_encoder.2 (256 -> 256): TPW output tiles per wave
+    // the last PE2_TAIL k-groups of pose_encoder.2 run after the head-layer-1 accumulator-init loads
+    // (hoisted pts/t blocks) are issued, so their latency hides behind MFMAs
+    constexpr int PE2_TAIL = 4;
+    stream_step<D2, KG_HID + D2 - PE2_TAIL, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
+    f32x4 tpv[3 * TPW], pov[3 * TPW][NT];
+#pragma unroll
+    for (int i = 0; i < 3 * TPW; ++i) {
+        const int T = TH[i];
+        tpv[i] = ld4(tproj + 16 * T + 4 * q);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q);
+    }
+    stream_step<KG_HID + D2 - PE2_TAIL, KG_HID + D2, TPW, NT, KG_HID, D2>(W2, T2, sm.act1, lane, voff, ring2, acc2);
+    // ---- head layer 1 prologue, issued before the barrier: the first DH k-groups of the pose-block
+    //      weights
+    PC_MARK(3);
+    f32x4 acc[3 * TPW][NT];
+#pragma unroll
+    for (int i = 0; i < 3 * TPW; ++i)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) acc[i][ct] = pov[i][ct] + tpv[i];
+    f32x4 ringh[DH + 1][3 * TPW];
+    stream_step<0, DH, 3 * TPW, NT, KG_HID, DH>(WH, TH, sm.act2, lane, voff, ringh, acc);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const f32x4 bias = ld4(&sm.pe2b[16 * T2[t] + 4 * q]);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) sm.act2[(T2[t] * NT + ct) * 64 + lane] = relu4(acc2[t][ct] + bias);
+    }
+    __syncthreads();
+    PC_MARK(4);
+    // ---- head layer 1 (pose block 256 -> 3x256): 3*TPW output tiles per wave
+    stream_step<DH, KG_HID + DH, 3 * TPW, NT, KG_HID, DH>(WH, TH, sm.act2, lane, voff, ringh, acc);
+    PC_MARK(5);
+    // ---- ReLU -> head layer 2 (block diagonal 3 x (256 -> 3)) partial dot products
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+            float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                const f32x4 u = relu4(acc[h * TPW + t][ct]);
+                const int ch = 16 * (wid * TPW + t) + 4 * q;
+                const f32x4 w0 = ld4(&sm.h2w[(h * 3 + 0) * HID + ch]);
+                const f32x4 w1 = ld4(&sm.h2w[(h * 3 + 1) * HID + ch]);
+                const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
+                p0 += u.x * w0.x + u.y * w0.y + u.z * w0.z + u.w * w0.w;
+                p1 += u.x * w1.x + u.y * w1.y + u.z * w1.z + u.w * w1.w;
+                p2 += u.x * w2.x + u.y * w2.y + u.z * w2.z + u.w * w2.w;
+            }
+            p0 = rows_sum(p0);
+            p1 = rows_sum(p1);
+            p2 = rows_sum(p2);
+            if (q == 0) {
+                sm.red[ct * 16 + n][h * 3 + 0][wid] = p0;
+                sm.red[ct * 16 + n][h * 3 + 1][wid] = p1;
+                sm.red[ct * 16 + n][h * 3 + 2][wid] = p2;
+            }
+        }
+    }
+    __syncthreads();
+    PC_MARK(6);
+}
+
+// ============================================================================ pose helpers
+template <typename T>
+__device__ __forceinline__ T tsqrt(T v);
+template <>
+__device__ __forceinline__ float tsqrt<float>(float v) { return sqrtf(v); }
+template <>
+__device__ __forceinline__ double tsqrt<double>(double v) { return sqrt(v); }
+
+// normalize_rotation(.., 'rot_matrix') (misc.py:327-344): rotation_6d_to_matrix GS with
+// F.normalize's eps 1e-12 (rotation_conversions.py:571-575).
+template <typename T>
+__device__ __forceinline__ void gram_schmidt6(T* v) {
+#pragma clang fp contract(off)
+    T n1 = tsqrt<T>((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+    n1 = n1 > (T)1e-12 ? n1 : (T)1e-12;
+    const T b0 = v[0] / n1, b1 = v[1] / n1, b2 = v[2] / n1;
+    const T d = (b0 * v[3] + b1 * v[4]) + b2 * v[5];
+    T c0 = v[3] - d * b0, c1 = v[4] - d * b1, c2 = v[5] - d * b2;
+    T n2 = tsqrt<T>((c0 * c0 + c1 * c1) + c2 * c2);
+    n2 = n2 > (T)1e-12 ? n2 : (T)1e-12;
+    v[0] = b0;
+    v[1] = b1;
+    v[2] = b2;
+    v[3] = c0 / n2;
+    v[4] = c1 / n2;
+    v[5] = c2 / n2;
+}
+
+// gram_schmidt6 spread over the four lanes of a row (lane part p: 0 -> v[0:3], 1 -> v[3:6],
+// 2 -> translation, untouched; 3 idle). Same operations and order as gram_schmidt6<float>.
+__device__ __forceinline__ void gram_schmidt6_quad(float* v, int p, int lane) {
+#pragma clang fp contract(off)
+    float n1 = sqrtf((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+    n1 = n1 > 1e-12f ? n1 : 1e-12f;
+    const float b0 = v[0] / n1, b1 = v[1] / n1, b2 = v[2] / n1;   // meaningful on p == 0
+    (void)lane;
+    const float B0 = quad_bcast0(b0), B1 = quad_bcast0(b1), B2 = quad_bcast0(b2);
+    const float d = (B0 * v[0] + B1 * v[1]) + B2 * v[2];
+    float c0 = v[0] - d * B0, c1 = v[1] - d * B1, c2 = v[2] - d * B2;
+    float n2 = sqrtf((c0 * c0 + c1 * c1) + c2 * c2);
+    n2 = n2 > 1e-12f ? n2 : 1e-12f;
+    if (p == 0) {
+        v[0] = b0; v[1] = b1; v[2] = b2;
+    } else if (p == 1) {
+        v[0] = c0 / n2; v[1] = c1 / n2; v[2] = c2 / n2;
+    }
+}
+
+// matrix_to_quaternion (rotation_conversions.py:102-161) of R = [b1 b2 b1xb2] (columns), input
+// already Gram-Schmidt'ed; returns wxyz.
+template <typename T>
+__device__ __forceinline__ void quat_from_gs(const T* v, T* qo) {
+#pragma clang fp contract(off)
+    // second GS pass as get_rot_matrix applies rotation_6d_to_matrix again (posenet_agent.py:554)
+    T g[6] = {v[0], v[1], v[2], v[3], v[4], v[5]};
+    gram_schmidt6<T>(g);
+    const T b3x = g[1] * g[5] - g[2] * g[4];
+    const T b3y = g[2] * g[3] - g[0] * g[5];
+    const T b3z = g[0] * g[4] - g[1] * g[3];
+    const T m00 = g[0], m01 = g[3], m02 = b3x;
+    const T m10 = g[1], m11 = g[4], m12 = b3y;
+    const T m20 = g[2], m21 = g[5], m22 = b3z;
+    const T one = (T)1;
+    T qa[4] = {((one + m00) + m11) + m22, ((one + m00) - m11) - m22, ((one - m00) + m11) - m22,
+               ((one - m00) - m11) + m22};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qa[i] = qa[i] > (T)0 ? tsqrt<T>(qa[i]) : (T)0;
+    int best = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+        if (qa[i] > qa[best]) best = i;
+    T c[4];
+    if (best == 0) {
+        c[0] = qa[0] * qa[0]; c[1] = m21 - m12; c[2] = m02 - m20; c[3] = m10 - m01;
+    } else if (best == 1) {
+        c[0] = m21 - m12; c[1] = qa[1] * qa[1]; c[2] = m10 + m01; c[3] = m02 + m20;
+    } else if (best == 2) {
+        c[0] = m02 - m20; c[1] = m10 + m01; c[2] = qa[2] * qa[2]; c[3] = m12 + m21;
+    } else {
+        c[0] = m10 - m01; c[1] = m20 + m02; c[2] = m21 + m12; c[3] = qa[3] * qa[3];
+    }
+    const T den = (T)2 * (qa[best] > (T)0.1 ? qa[best] : (T)0.1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qo[i] = c[i] / den;
+}
+
+// Head layer-1 t block for one time value (HT threads): tproj = W1_t . relu(W_te . [sin, cos](GFP(t)) + b_te)
+// (scorenet.py:77-88 GaussianFourierProjection + t_encoder, the t columns of the first head layer).
+__device__ __forceinline__ void time_row(const gp_head_weights& w, float t, float* emb, float* tf,
+                                         float* __restrict__ out) {
+    const int i = threadIdx.x;
+    if (i < 64) {  // x_proj = x[:, None] * W[None, :] * 2 * np.pi (scorenet.py:87)
+        const float a = fmul(fmul(fmul(t, w.gfp_w[i]), 2.0f), 3.14159265358979323846f);
+        emb[i] = sinf(a);
+        emb[64 + i] = cosf(a);
+    }
+    __syncthreads();
+    if (i < 128) {
+        float acc = 0.f;
+        for (int c = 0; c < 128; ++c) acc += w.te_w_t[c * 128 + i] * emb[c];
+        tf[i] = fmaxf(acc + w.te_b[i], 0.f);
+    }
+    __syncthreads();
+    for (int o = i; o < 768; o += HT) {
+        float acc = 0.f;
+        for (int c = 0; c < 128; ++c) acc += w.h1t_t[c * 768 + o] * tf[c];
+        out[o] = acc;
+    }
+}

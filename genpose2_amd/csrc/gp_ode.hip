@@ -1,0 +1,424 @@
+// Probability-flow ODE sampler on device: Dormand-Prince 5(4) stages fused with the score heads.
+//
+// Reference: cond_ode_sampler (networks/gf_algorithms/samplers.py:180-258) hands the float64 state
+// to scipy solve_ivp(method="RK45") and pays a device->host and host->device copy per right-hand
+// side. Here every RK45 stage is one launch: the stage combination y + (sum_j a_j K_j) * h (fp64,
+// scipy rk.py rk_step order) is formed in the prologue, cast to the fp32 pose the score model sees
+// (samplers.py:210), the head trunk evaluates the score, and the epilogue writes
+// K_s = -(0.5 g(t)^2) * score in fp64 (samplers.py:216). The last stage of an attempted step also
+// writes y_new and the per-workgroup sum of (err / scale)^2 of scipy's error estimator
+// (_estimate_error_norm, rk.py); ode_norm_kernel reduces it in a fixed order. The step
+// controller's scalars stay on the host (genpose2_amd/ode.py): one 8-byte read per attempt.
+#include "gp_head.h"
+
+#define ODE_NK 7   // Dormand-Prince stages incl. the FSAL derivative
+
+struct OdeStageArgs {
+    gp_head_weights w;
+    const float* pobj;
+    const float* tproj;          // (768) time row of this stage's t
+    float sigma;                 // sigma(t32), fp32 (score = f / (sigma + 1e-7))
+    double coef;                 // -(0.5 * g(t)^2)
+    const double* y;             // (R,9) state at the step's start
+    const double* k[ODE_NK];     // stage derivatives combined into this stage's input
+    double a[ODE_NK];            // y_in = y + (sum_{j<nk} a_j K_j) * h
+    int nk;
+    double h;
+    double* kout;                // (R,9) this stage's derivative
+    // final stage of an attempt (MODE 1): y_new out and the error-estimator partials
+    double* ynew;
+    double e[ODE_NK];            // error weights over K_0..K_6 (K_6 = this stage)
+    double rtol, atol;
+    double* part;                // (nwg) sum over the workgroup's elements of (err/scale)^2
+    int rows, kper;
+};
+
+// MODE 0: stage derivative. MODE 1: last stage of an attempt (y_new, K_6, error partials).
+template <int MODE>
+__global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a) {
+    __shared__ HeadSmem<1, EVAL_WV> sm;
+    __shared__ int obj[16];
+    __shared__ double y0s[16 * 9], y1s[16 * 9], esq[16 * 9];
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * 16;
+    stage_small_weights<1, EVAL_WV>(a.w, sm);
+    for (int i = tid; i < 256; i += EVAL_WV * 64) {
+        const int c = i >> 4, j = i & 15;
+        const int r = r0 + c;
+        float xv = 0.f;
+        if (r < a.rows && j < 9) {
+#pragma clang fp contract(off)
+            const size_t e = (size_t)r * 9 + j;
+            const double y = a.y[e];
+            double yi = y;
+            if (a.nk > 0) {
+                double acc = a.k[0][e] * a.a[0];
+                for (int s = 1; s < a.nk; ++s) acc = acc + a.k[s][e] * a.a[s];
+                yi = y + acc * a.h;
+            }
+            xv = (float)yi;   // torch.tensor(x, dtype=torch.float32) (samplers.py:210)
+            if (MODE == 1) {
+                y0s[c * 9 + j] = y;
+                y1s[c * 9 + j] = yi;
+                a.ynew[e] = yi;
+            }
+        }
+        sm.xin[i] = xv;
+    }
+    if (tid < 16) {
+        const int r = r0 + tid;
+        obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
+    }
+    head_trunk<1, EVAL_WV>(a.w, a.pobj, a.tproj, obj, sm);
+    if (tid < 144) {
+#pragma clang fp contract(off)
+        const int c = tid / 9, o = tid - c * 9;
+        const int r = r0 + c;
+        double sq = 0.0;
+        if (r < a.rows) {
+            const size_t e = (size_t)r * 9 + o;
+            const float s = fdiv(head_out(sm, c, o), fadd(a.sigma, 1e-7f));
+            const double kv = a.coef * (double)s;
+            a.kout[e] = kv;
+            if (MODE == 1) {
+                // scipy: err = (K^T E) * h / scale, scale = atol + max(|y|, |y_new|) * rtol
+                double acc = a.k[0][e] * a.e[0];
+                for (int s2 = 1; s2 < ODE_NK - 1; ++s2) acc = acc + a.k[s2][e] * a.e[s2];
+                acc = acc + kv * a.e[ODE_NK - 1];
+                const double y0 = y0s[c * 9 + o], y1 = y1s[c * 9 + o];
+                const double sc = a.atol + fmax(fabs(y0), fabs(y1)) * a.rtol;
+                const double er = (acc * a.h) / sc;
+                sq = er * er;
+            }
+        }
+        if (MODE == 1) esq[tid] = sq;
+    }
+    if (MODE == 1) {
+        __syncthreads();
+        if (tid == 0) {
+            double t = 0.0;
+            for (int i = 0; i < 144; ++i) t += esq[i];
+            a.part[blockIdx.x] = t;
+        }
+    }
+}
+
+// out[slot] = sqrt(sum(part[0..n))) / sqrt(count): scipy's RMS norm over the reduced partials in a
+// fixed order (one workgroup).
+__global__ __launch_bounds__(256) void ode_norm_kernel(const double* __restrict__ part, int n, double count,
+                                                       double* __restrict__ out) {
+    __shared__ double red[256];
+    double t = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) t += part[i];
+    red[threadIdx.x] = t;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = sqrt(red[0]) / sqrt(count);
+}
+
+// select_initial_step norms (scipy _ivp/common.py): scale = atol + |y0| rtol;
+// f1 == NULL: out[0] = rms(y0 / scale), out[1] = rms(f0 / scale); else out[2] = rms((f1 - f0) / scale).
+__global__ __launch_bounds__(1024) void ode_init_norms_kernel(const double* __restrict__ y0,
+                                                              const double* __restrict__ f0,
+                                                              const double* __restrict__ f1, long long n,
+                                                              double atol, double rtol, double* __restrict__ out) {
+#pragma clang fp contract(off)
+    __shared__ double r0[1024], r1[1024];
+    double s0 = 0.0, s1 = 0.0;
+    for (long long i = threadIdx.x; i < n; i += 1024) {
+        const double sc = atol + fabs(y0[i]) * rtol;
+        if (f1 == nullptr) {
+            const double u = y0[i] / sc, v = f0[i] / sc;
+            s0 += u * u;
+            s1 += v * v;
+        } else {
+            const double v = (f1[i] - f0[i]) / sc;
+            s0 += v * v;
+        }
+    }
+    r0[threadIdx.x] = s0;
+    r1[threadIdx.x] = s1;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            r0[threadIdx.x] += r0[threadIdx.x + s];
+            r1[threadIdx.x] += r1[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double rn = sqrt((double)n);
+        if (f1 == nullptr) {
+            out[0] = sqrt(r0[0]) / rn;
+            out[1] = sqrt(r1[0]) / rn;
+        } else {
+            out[2] = sqrt(r0[0]) / rn;
+        }
+    }
+}
+
+// Dense output of an accepted step (scipy RkDenseOutput, rk.py): for each requested t_eval point
+// te = tev[i], x = (te - t_old) / h, p = cumprod([x, x, x, x]), y = h * (Q p) + y_old with
+// Q = K^T P. Writes out[(i - i_base) * n + e] for i in [i0, i1).
+struct OdeDenseArgs {
+    const double* k[ODE_NK];
+    double P[ODE_NK][4];
+    const double* y_old;
+    const double* tev;
+    int i0, i1, i_base;
+    double t_old, h;
+    double* out;
+    long long n;
+    int reverse;   // out row = (i_base - i) instead of (i - i_base)
+};
+
+__global__ __launch_bounds__(256) void ode_dense_kernel(OdeDenseArgs a) {
+#pragma clang fp contract(off)
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= a.n) return;
+    double Q[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        double acc = a.k[0][e] * a.P[0][m];
+        for (int j = 1; j < ODE_NK; ++j) acc = acc + a.k[j][e] * a.P[j][m];
+        Q[m] = acc;
+    }
+    const double yo = a.y_old[e];
+    for (int i = a.i0; i < a.i1; ++i) {
+        const double x = (a.tev[i] - a.t_old) / a.h;
+        const double p1 = x, p2 = p1 * x, p3 = p2 * x, p4 = p3 * x;
+        const double d = ((Q[0] * p1 + Q[1] * p2) + Q[2] * p3) + Q[3] * p4;
+        const long long row = a.reverse ? (long long)(a.i_base - i) : (long long)(i - a.i_base);
+        a.out[row * a.n + e] = a.h * d + yo;
+    }
+}
+
+// Final denoise (samplers.py:240-249) + epilogue: grad = score(float(x), eps) in fp32,
+// mean_x = x + (0 - g^2 grad) * c (fp32 product, fp64 sum), then GS of [:6], + pts_center, quaternion
+// (posenet_agent.py:554-556). Writes pose (R,9) fp64 and q (R,7) fp64.
+struct OdeDenoiseArgs {
+    gp_head_weights w;
+    const float* pobj;
+    const float* tproj;
+    float sigma;
+    float g2;        // diffusion(eps)^2 in fp32
+    float step;      // (1 - eps) / num_steps as fp32
+    const double* x;
+    const float* center;
+    double* pose;
+    double* q;
+    int rows, kper;
+};
+
+__global__ __launch_bounds__(EVAL_WV * 64) void ode_denoise_kernel(OdeDenoiseArgs a) {
+    __shared__ HeadSmem<1, EVAL_WV> sm;
+    __shared__ int obj[16];
+    __shared__ double xm[16 * 9];
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * 16;
+    stage_small_weights<1, EVAL_WV>(a.w, sm);
+    for (int i = tid; i < 256; i += EVAL_WV * 64) {
+        const int c = i >> 4, j = i & 15;
+        const int r = r0 + c;
+        sm.xin[i] = (r < a.rows && j < 9) ? (float)a.x[(size_t)r * 9 + j] : 0.f;
+    }
+    if (tid < 16) {
+        const int r = r0 + tid;
+        obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
+    }
+    head_trunk<1, EVAL_WV>(a.w, a.pobj, a.tproj, obj, sm);
+    if (tid < 144) {
+#pragma clang fp contract(off)
+        const int c = tid / 9, o = tid - c * 9;
+        const int r = r0 + c;
+        if (r < a.rows) {
+            const float grad = fdiv(head_out(sm, c, o), fadd(a.sigma, 1e-7f));
+            const float drift = 0.0f - a.g2 * grad;
+            xm[tid] = a.x[(size_t)r * 9 + o] + (double)(drift * a.step);
+        }
+    }
+    __syncthreads();
+    if (tid < 16 && r0 + tid < a.rows) {
+        const int r = r0 + tid;
+        double v[9], qq[4];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) v[j] = xm[tid * 9 + j];
+        gram_schmidt6<double>(v);
+        const float* cen = a.center + (size_t)obj[tid] * 3;
+        v[6] += (double)cen[0];
+        v[7] += (double)cen[1];
+        v[8] += (double)cen[2];
+        quat_from_gs<double>(v, qq);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) a.pose[(size_t)r * 9 + j] = v[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a.q[(size_t)r * 7 + j] = qq[j];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a.q[(size_t)r * 7 + 4 + j] = v[6 + j];
+    }
+}
+
+// Time rows of up to 6 stage times passed by value (no host->device copy per attempt).
+struct OdeTimes {
+    float t[6];
+};
+__global__ __launch_bounds__(HT) void ode_time_rows_kernel(gp_head_weights w, OdeTimes tv, float* __restrict__ out) {
+    __shared__ float emb[128];
+    __shared__ float tf[128];
+    time_row(w, tv.t[blockIdx.x], emb, tf, out + (size_t)blockIdx.x * 768);
+}
+
+// ------------------------------------------------------------------------------ C ABI
+// Workspace: 6 time rows (6 x 768 fp32) | per-workgroup error partials (fp64).
+static size_t ode_part_offset() { return 6 * 768 * sizeof(float); }
+
+extern "C" size_t gp_ode_workspace_size(int rows) {
+    return ode_part_offset() + sizeof(double) * (((size_t)rows + 15) / 16) + 256;
+}
+
+static int ode_launch_times(const gp_head_weights* w, const float* t32, int nt, void* ws, hipStream_t stream) {
+    OdeTimes tv = {};
+    for (int i = 0; i < nt; ++i) tv.t[i] = t32[i];
+    hipLaunchKernelGGL(ode_time_rows_kernel, dim3(nt), dim3(HT), 0, stream, *w, tv, static_cast<float*>(ws));
+    return gp_check_launch("ode_time_rows_kernel");
+}
+
+extern "C" int gp_ode_rhs(const gp_head_weights* w, const float* pobj, float t32, float sigma, double coef,
+                          const double* y, const double* const* kin, const double* acoef, int nk, double h, int rows,
+                          int k, double* kout, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    GP_REQUIRE(w && pobj && y && kout && workspace && rows >= 1 && k >= 1, "ode_rhs: bad arguments");
+    GP_REQUIRE(nk >= 0 && nk < ODE_NK && (nk == 0 || (kin && acoef)), "ode_rhs: nk must be in [0, 6]");
+    GP_REQUIRE(workspace_bytes >= gp_ode_workspace_size(rows), "ode_rhs: workspace too small");
+    OdeStageArgs a = {};
+    a.w = *w;
+    a.pobj = pobj;
+    a.tproj = static_cast<const float*>(workspace);
+    a.sigma = sigma;
+    a.coef = coef;
+    a.y = y;
+    for (int j = 0; j < nk; ++j) {
+        GP_REQUIRE(kin[j] != nullptr, "ode_rhs: null stage pointer");
+        a.k[j] = kin[j];
+        a.a[j] = acoef[j];
+    }
+    a.nk = nk;
+    a.h = h;
+    a.kout = kout;
+    a.rows = rows;
+    a.kper = k;
+    int rc = ode_launch_times(w, &t32, 1, workspace, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(ode_stage_kernel<0>, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
+    return gp_check_launch("ode_stage_kernel");
+}
+
+extern "C" int gp_ode_attempt(const gp_head_weights* w, const float* pobj, const float* t32_6, const float* sigma_6,
+                              const double* coef_6, const double* y, double* const* kslots, const double* tableau_a,
+                              const double* b, const double* e, double h, double rtol, double atol, int rows, int k,
+                              double* ynew, double* err_out, void* workspace, size_t workspace_bytes,
+                              hipStream_t stream) {
+    GP_REQUIRE(w && pobj && t32_6 && sigma_6 && coef_6 && y && kslots && tableau_a && b && e && ynew && err_out &&
+                   workspace && rows >= 1 && k >= 1,
+               "ode_attempt: bad arguments");
+    GP_REQUIRE(workspace_bytes >= gp_ode_workspace_size(rows), "ode_attempt: workspace too small");
+    for (int j = 0; j < ODE_NK; ++j) GP_REQUIRE(kslots[j] != nullptr, "ode_attempt: null K slot");
+    const int nwg = (rows + 15) / 16;
+    const float* tproj = static_cast<const float*>(workspace);
+    double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + ode_part_offset());
+    int rc = ode_launch_times(w, t32_6, 6, workspace, stream);
+    if (rc) return rc;
+    OdeStageArgs a = {};
+    a.w = *w;
+    a.pobj = pobj;
+    a.y = y;
+    a.h = h;
+    a.rows = rows;
+    a.kper = k;
+    a.rtol = rtol;
+    a.atol = atol;
+    for (int j = 0; j < ODE_NK; ++j) a.k[j] = kslots[j];
+    // stages 1..5: K_s = f(t + c_s h, y + (sum_{j<s} A[s][j] K_j) h)   (tableau_a: 6x6 row-major)
+    for (int s = 1; s < 6; ++s) {
+        a.tproj = tproj + (size_t)(s - 1) * 768;
+        a.sigma = sigma_6[s - 1];
+        a.coef = coef_6[s - 1];
+        a.nk = s;
+        for (int j = 0; j < s; ++j) a.a[j] = tableau_a[s * 6 + j];
+        a.kout = kslots[s];
+        hipLaunchKernelGGL(ode_stage_kernel<0>, dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    }
+    // y_new = y + (sum_{j<6} B_j K_j) h ; K_6 = f(t + h, y_new) ; error partials
+    a.tproj = tproj + (size_t)5 * 768;
+    a.sigma = sigma_6[5];
+    a.coef = coef_6[5];
+    a.nk = 6;
+    for (int j = 0; j < 6; ++j) a.a[j] = b[j];
+    for (int j = 0; j < ODE_NK; ++j) a.e[j] = e[j];
+    a.kout = kslots[6];
+    a.ynew = ynew;
+    a.part = part;
+    hipLaunchKernelGGL(ode_stage_kernel<1>, dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    hipLaunchKernelGGL(ode_norm_kernel, dim3(1), dim3(256), 0, stream, (const double*)part, nwg,
+                       (double)rows * 9.0, err_out);
+    return gp_check_launch("ode_stage_kernel<final>");
+}
+
+extern "C" int gp_ode_init_norms(const double* y0, const double* f0, const double* f1, long long n, double atol,
+                                 double rtol, double* out, hipStream_t stream) {
+    GP_REQUIRE(y0 && f0 && out && n >= 1, "ode_init_norms: bad arguments");
+    hipLaunchKernelGGL(ode_init_norms_kernel, dim3(1), dim3(1024), 0, stream, y0, f0, f1, n, atol, rtol, out);
+    return gp_check_launch("ode_init_norms_kernel");
+}
+
+extern "C" int gp_ode_dense(const double* const* kslots, const double* P7x4, const double* y_old,
+                            const double* t_eval, int i0, int i1, int i_base, int reverse, double t_old, double h,
+                            long long n, double* out, hipStream_t stream) {
+    GP_REQUIRE(kslots && P7x4 && y_old && t_eval && out && n >= 1 && i1 >= i0, "ode_dense: bad arguments");
+    if (i1 == i0) return GP_OK;
+    OdeDenseArgs a = {};
+    for (int j = 0; j < ODE_NK; ++j) {
+        GP_REQUIRE(kslots[j] != nullptr, "ode_dense: null K slot");
+        a.k[j] = kslots[j];
+        for (int m = 0; m < 4; ++m) a.P[j][m] = P7x4[j * 4 + m];
+    }
+    a.y_old = y_old;
+    a.tev = t_eval;
+    a.i0 = i0;
+    a.i1 = i1;
+    a.i_base = i_base;
+    a.reverse = reverse;
+    a.t_old = t_old;
+    a.h = h;
+    a.out = out;
+    a.n = n;
+    hipLaunchKernelGGL(ode_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
+    return gp_check_launch("ode_dense_kernel");
+}
+
+extern "C" int gp_ode_denoise(const gp_head_weights* w, const float* pobj, float t32, float sigma, float g2,
+                              float step, const double* x, int rows, int k, const float* pts_center, double* pose,
+                              double* q, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    GP_REQUIRE(w && pobj && x && pts_center && pose && q && workspace && rows >= 1 && k >= 1,
+               "ode_denoise: bad arguments");
+    GP_REQUIRE(workspace_bytes >= gp_ode_workspace_size(rows), "ode_denoise: workspace too small");
+    int rc = ode_launch_times(w, &t32, 1, workspace, stream);
+    if (rc) return rc;
+    OdeDenoiseArgs a = {};
+    a.w = *w;
+    a.pobj = pobj;
+    a.tproj = static_cast<const float*>(workspace);
+    a.sigma = sigma;
+    a.g2 = g2;
+    a.step = step;
+    a.x = x;
+    a.center = pts_center;
+    a.pose = pose;
+    a.q = q;
+    a.rows = rows;
+    a.kper = k;
+    hipLaunchKernelGGL(ode_denoise_kernel, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
+    return gp_check_launch("ode_denoise_kernel");
+}

@@ -160,6 +160,20 @@ class HeadModel:
         return res, q, xs
 
 
+    def ode_denoise(self, pobj, t32: float, sigma: float, g2: float, step: float, x: torch.Tensor, k: int,
+                    pts_center: torch.Tensor, ws: torch.Tensor):
+        """cond_ode_sampler's final denoise + epilogue (gp_ode_denoise) -> pose (R,9), q (R,7) fp64."""
+        R = x.numel() // arch.POSE_DIM
+        pose = torch.empty((R, arch.POSE_DIM), dtype=torch.float64, device=self.device)
+        q = torch.empty((R, 7), dtype=torch.float64, device=self.device)
+        check(self.lib.gp_ode_denoise(
+            ctypes.byref(self.w), ctypes.c_void_p(pobj.data_ptr()), t32, sigma, g2, step,
+            ctypes.c_void_p(x.data_ptr()), R, k, ctypes.c_void_p(require_device_tensor(pts_center, "pts_center").data_ptr()),
+            ctypes.c_void_p(pose.data_ptr()), ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+            ws.numel(), self._s()), "ode_denoise")
+        return pose, q
+
+
 class ScaleModel:
     def __init__(self, sd: weights.StateDict, device: torch.device):
         self.lib = _lib.load()

@@ -3,29 +3,43 @@ Dormand-Prince 5(4) integrator.
 
 The reference hands the float64 state to scipy ``solve_ivp(method="RK45")`` on the host and pays
 one device->host and one host->device copy per right-hand-side evaluation (samplers.py:207-219).
-Here the state, the 7 stages and every stage combination stay in HBM (float64); the score is the
-HIP head kernel; only the step controller's scalars (one RMS error norm per attempted step) cross
-to the host. The controller restates scipy's published RK45 (scipy 1.15 ``_ivp/rk.py``:
-``rk_step``, ``_step_impl``, ``RkDenseOutput``; ``_ivp/common.py``: ``select_initial_step``,
-RMS ``norm``; ``_ivp/ivp.py`` t_eval handling), which the reference pins only as
-``scipy`` (requirements.txt:2, commented ``scipy==1.12.0``).
+Here the state, the 7 stage derivatives and every stage combination stay in HBM (float64): one
+HIP launch per stage (``gp_ode_attempt`` fuses the stage combination, the score heads and the
+error estimate). Only the step controller's scalars cross to the host: one 8-byte error norm per
+attempted step.
+
+The controller (``rk45_drive``) restates scipy's published RK45 line by line, with the same
+Python/NumPy scalar types (scipy 1.15 ``_ivp/rk.py``: ``RK45``, ``rk_step``, ``_step_impl``,
+``RkDenseOutput``; ``_ivp/common.py``: ``select_initial_step``, RMS ``norm``; ``_ivp/base.py``:
+``OdeSolver.step``; ``_ivp/ivp.py``: ``solve_ivp`` t_eval handling). The reference pins scipy only as
+``scipy`` (requirements.txt:2, commented ``scipy==1.12.0``). The arithmetic lives in a backend:
+``DeviceRk45`` (HIP, the product path) or ``NumpyRk45`` (scipy's own NumPy expressions; used by the
+CPU tests to hold the controller to ``solve_ivp`` exactly).
 """
 from __future__ import annotations
 
-import math
-from typing import Callable, Optional, Tuple
+import ctypes
+import warnings
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
 
-# Dormand-Prince tableau as in scipy RK45
-_C = [0.0, 1 / 5, 3 / 10, 4 / 5, 8 / 9, 1.0]
-_A = [[], [1 / 5], [3 / 40, 9 / 40], [44 / 45, -56 / 15, 32 / 9],
-      [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729],
-      [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656]]
-_B = [35 / 384, 0.0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84]
-_E = [-71 / 57600, 0.0, 71 / 16695, -71 / 1920, 17253 / 339200, -22 / 525, 1 / 40]
-_P = np.array([
+from . import _lib, arch, sde
+from ._lib import check
+
+# Dormand-Prince tableau exactly as scipy's RK45 class attributes
+C = np.array([0, 1 / 5, 3 / 10, 4 / 5, 8 / 9, 1])
+A = np.array([
+    [0, 0, 0, 0, 0],
+    [1 / 5, 0, 0, 0, 0],
+    [3 / 40, 9 / 40, 0, 0, 0],
+    [44 / 45, -56 / 15, 32 / 9, 0, 0],
+    [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729, 0],
+    [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656]])
+B = np.array([35 / 384, 0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84])
+E = np.array([-71 / 57600, 0, 71 / 16695, -71 / 1920, 17253 / 339200, -22 / 525, 1 / 40])
+P = np.array([
     [1, -8048581381 / 2820520608, 8663915743 / 2820520608, -12715105075 / 11282082432],
     [0, 0, 0, 0],
     [0, 131558114200 / 32700410799, -68118460800 / 10900136933, 87487479700 / 32700410799],
@@ -33,115 +47,334 @@ _P = np.array([
     [0, 127303824393 / 49829197408, -318862633887 / 49829197408, 701980252875 / 199316789632],
     [0, -282668133 / 205662961, 2019193451 / 616988883, -1453857185 / 822651844],
     [0, 40617522 / 29380423, -110615467 / 29380423, 69997945 / 29380423]])
-SAFETY, MIN_FACTOR, MAX_FACTOR = 0.9, 0.2, 10.0
-ERR_EXP = -1.0 / 5.0
+N_STAGES = 6
+ERROR_ESTIMATOR_ORDER = 4
+SAFETY, MIN_FACTOR, MAX_FACTOR = 0.9, 0.2, 10
+ERROR_EXPONENT = -1 / (ERROR_ESTIMATOR_ORDER + 1)
 
 
-def _rms(x: torch.Tensor) -> float:
-    return float(torch.linalg.vector_norm(x).item()) / math.sqrt(x.numel())
+# ============================================================================ controller
+def rk45_drive(be, t0: float, t_bound: float, rtol: float = 1e-5, atol: float = 1e-5,
+               t_eval: Optional[np.ndarray] = None, keep_all: bool = True):
+    """solve_ivp(fun, (t0, t_bound), y0, method="RK45", rtol, atol, t_eval) over backend `be`.
 
-
-def _lin(coefs, ks, h=None):
-    acc = None
-    for c, k in zip(coefs, ks):
-        if c == 0.0:
-            continue
-        acc = k * c if acc is None else acc + k * c
-    if acc is None:
-        acc = torch.zeros_like(ks[0])
-    return acc * h if h is not None else acc
-
-
-def rk45_solve(fun: Callable[[float, torch.Tensor], torch.Tensor], t0: float, y0: torch.Tensor, t_bound: float,
-               rtol: float = 1e-5, atol: float = 1e-5, t_eval: Optional[np.ndarray] = None):
-    """Integrate y' = fun(t, y) from t0 to t_bound. Returns (ts (n,), ys (n, *y.shape), nfev)."""
-    nfev = [0]
-
-    def f(t, y):
-        nfev[0] += 1
-        return fun(t, y)
-
-    direction = 1.0 if t_bound > t0 else -1.0
-    t, y = float(t0), y0.clone()
-    fy = f(t, y)
-    # select_initial_step (order = error_estimator_order = 4)
-    interval = abs(t_bound - t0)
-    scale = atol + y.abs() * rtol
-    d0, d1 = _rms(y / scale), _rms(fy / scale)
-    h0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
-    h0 = min(h0, interval)
-    y1 = y + (h0 * direction) * fy
-    f1 = f(t + h0 * direction, y1)
-    d2 = _rms((f1 - fy) / scale) / h0
-    h1 = max(1e-6, h0 * 1e-3) if (d1 <= 1e-15 and d2 <= 1e-15) else (0.01 / max(d1, d2)) ** (1 / 5)
-    h_abs = min(100 * h0, h1, interval)
-
-    ts, ys = [], []
-    if t_eval is None:
-        ts.append(t)
-        ys.append(y.clone())
-    else:
-        t_eval = np.asarray(t_eval, dtype=np.float64)
-        if direction < 0:
+    `be` holds y0 and provides: set_t_eval, rhs0(t), init_norms(), rhs_euler(t, h), diff_norm(),
+    attempt(t, h) -> error norm, dense(t_old, t, lo, hi), accept(t_old, t), keep_y(keep, first).
+    Returns (ts, nfev, status); the outputs stay in the backend (``be.ys`` for t_eval=None, the
+    dense rows otherwise). With keep_all=False
+    only the final output is kept (the value ``res.y[:, -1]`` that pred_func uses).
+    """
+    t0, tf = map(float, (t0, t_bound))                          # ivp.py: t0, tf = map(float, t_span)
+    direction = np.sign(tf - t0) if tf != t0 else 1             # base.py OdeSolver.__init__
+    if t_eval is not None:
+        t_eval = np.asarray(t_eval)
+        if np.any(t_eval < min(t0, tf)) or np.any(t_eval > max(t0, tf)):
+            raise ValueError("Values in `t_eval` are not within `t_span`.")
+        if tf > t0:
+            t_eval_i = 0
+        else:
             t_eval = t_eval[::-1]
             t_eval_i = t_eval.shape[0]
-        else:
-            t_eval_i = 0
-    K = [None] * 7
+        be.set_t_eval(np.ascontiguousarray(t_eval), direction, keep_all)
+    interval_length = abs(tf - t0)
+    if interval_length == 0.0:
+        raise ValueError("RK45: empty integration interval (T0 == eps)")
+    # ---- RK45.__init__: f = fun(t0, y0); h_abs = select_initial_step(...)
+    nfev = 1
+    be.rhs0(t0)
+    d0, d1 = be.init_norms()
+    if d0 < 1e-5 or d1 < 1e-5:
+        h0 = 1e-6
+    else:
+        h0 = 0.01 * d0 / d1
+    h0 = min(h0, interval_length)
+    be.rhs_euler(t0 + h0 * direction, h0 * direction)
+    nfev += 1
+    d2 = be.diff_norm() / h0
+    if d1 <= 1e-15 and d2 <= 1e-15:
+        h1 = max(1e-6, h0 * 1e-3)
+    else:
+        h1 = (0.01 / max(d1, d2)) ** (1 / (ERROR_ESTIMATOR_ORDER + 1))
+    h_abs = min(100 * h0, h1, interval_length, np.inf)
+    ts: List[float] = [t0] if t_eval is None else []
+    if t_eval is None:
+        be.keep_y(keep_all, first=True)
+    t = t0
     status = None
     while status is None:
-        # ---- OdeSolver.step -> _step_impl
-        min_step = 10 * abs(np.nextafter(t, direction * np.inf) - t)
-        h_abs = min(max(h_abs, min_step), np.inf)
-        accepted, rejected = False, False
-        while not accepted:
+        # ---- OdeSolver.step (t == t_bound cannot hold here: the loop ends when t reaches it)
+        # ---- RK45._step_impl
+        min_step = 10 * np.abs(np.nextafter(t, direction * np.inf) - t)
+        if h_abs > np.inf:
+            h_abs = np.inf
+        elif h_abs < min_step:
+            h_abs = min_step
+        step_accepted = False
+        step_rejected = False
+        failed = False
+        while not step_accepted:
             if h_abs < min_step:
-                raise RuntimeError("RK45: required step size is less than spacing between numbers")
+                failed = True
+                break
             h = h_abs * direction
             t_new = t + h
-            if direction * (t_new - t_bound) > 0:
-                t_new = t_bound
+            if direction * (t_new - tf) > 0:
+                t_new = tf
             h = t_new - t
-            h_abs = abs(h)
-            K[0] = fy
-            for s in range(1, 6):
-                K[s] = f(t + _C[s] * h, y + _lin(_A[s], K[:s], h))
-            y_new = y + _lin(_B, K[:6]) * h
-            f_new = f(t + h, y_new)
-            K[6] = f_new
-            scale = atol + torch.maximum(y.abs(), y_new.abs()) * rtol
-            err = _rms(_lin(_E, K) * h / scale)
-            if err < 1:
-                factor = MAX_FACTOR if err == 0 else min(MAX_FACTOR, SAFETY * err ** ERR_EXP)
-                if rejected:
-                    factor = min(1.0, factor)
+            h_abs = np.abs(h)
+            error_norm = be.attempt(t, h)
+            nfev += N_STAGES
+            if error_norm < 1:
+                if error_norm == 0:
+                    factor = MAX_FACTOR
+                else:
+                    factor = min(MAX_FACTOR, SAFETY * error_norm ** ERROR_EXPONENT)
+                if step_rejected:
+                    factor = min(1, factor)
                 h_abs *= factor
-                accepted = True
+                step_accepted = True
             else:
-                h_abs *= max(MIN_FACTOR, SAFETY * err ** ERR_EXP)
-                rejected = True
-        t_old, y_old = t, y
-        t, y, fy = t_new, y_new, f_new
-        if direction * (t - t_bound) >= 0:
+                h_abs *= max(MIN_FACTOR, SAFETY * error_norm ** ERROR_EXPONENT)
+                step_rejected = True
+        if failed:
+            # solve_ivp returns (status -1) with the outputs collected so far; the reference then
+            # uses res.y[:, -1] as is
+            warnings.warn("RK45: required step size is less than spacing between numbers.")
+            status = -1
+            if t_eval is None and not keep_all:
+                be.keep_y(True, first=False)
+            break
+        t_old = t
+        t = t_new
+        if direction * (t - tf) >= 0:
             status = 0
         # ---- solve_ivp output collection
         if t_eval is None:
             ts.append(t)
-            ys.append(y.clone())
+            be.accept(t_old, t)
+            be.keep_y(keep_all or status is not None, first=False)
         else:
             if direction > 0:
-                new_i = int(np.searchsorted(t_eval, t, side="right"))
-                step_t = t_eval[t_eval_i:new_i]
+                t_eval_i_new = int(np.searchsorted(t_eval, t, side="right"))
+                lo, hi = t_eval_i, t_eval_i_new
             else:
-                new_i = int(np.searchsorted(t_eval, t, side="left"))
-                step_t = t_eval[new_i:t_eval_i][::-1]
-            if step_t.size > 0:
-                Q = torch.stack(K, -1) @ torch.from_numpy(_P).to(y.device)        # (n, 4)
-                hh = t - t_old
-                for te in step_t:
-                    x = (te - t_old) / hh
-                    p = torch.tensor(np.cumprod(np.tile(x, 4)), dtype=torch.float64, device=y.device)
-                    ts.append(float(te))
-                    ys.append(hh * (Q @ p) + y_old)
-                t_eval_i = new_i
-    return np.asarray(ts), torch.stack(ys, 0), nfev[0]
+                t_eval_i_new = int(np.searchsorted(t_eval, t, side="left"))
+                lo, hi = t_eval_i_new, t_eval_i
+            if hi > lo:
+                be.dense(t_old, t, lo, hi)
+                ts.extend(t_eval[lo:hi][::-1] if direction < 0 else t_eval[lo:hi])
+                t_eval_i = t_eval_i_new
+            be.accept(t_old, t)
+    return np.asarray(ts, dtype=np.float64), nfev, status
+
+
+# ============================================================================ NumPy backend
+class NumpyRk45:
+    """scipy's own expressions (rk.py rk_step, _estimate_error_norm, RkDenseOutput; common.py norm)
+    over an arbitrary fun(t, y). Used by the CPU tests to hold the controller to solve_ivp."""
+
+    def __init__(self, fun, y0: np.ndarray, rtol: float = 1e-5, atol: float = 1e-5):
+        self.fun = fun
+        self.y = np.asarray(y0, dtype=float)
+        self.rtol, self.atol = rtol, atol
+        self.K = np.empty((N_STAGES + 1, self.y.shape[0]), dtype=self.y.dtype)
+        self.ys: List[np.ndarray] = []
+        self.dense_rows: List[Tuple[float, np.ndarray]] = []
+
+    @staticmethod
+    def _norm(x):
+        return np.linalg.norm(x) / x.size ** 0.5
+
+    def set_t_eval(self, t_eval, direction, keep_all):
+        self.t_eval, self.direction = t_eval, direction
+
+    def rhs0(self, t):
+        self.f = self.fun(t, self.y)
+
+    def init_norms(self):
+        self.scale0 = self.atol + np.abs(self.y) * self.rtol
+        return self._norm(self.y / self.scale0), self._norm(self.f / self.scale0)
+
+    def rhs_euler(self, t, h):
+        y1 = self.y + h * self.f
+        self.f1 = self.fun(t, y1)
+
+    def diff_norm(self):
+        return self._norm((self.f1 - self.f) / self.scale0)
+
+    def attempt(self, t, h):
+        K, y = self.K, self.y
+        K[0] = self.f
+        for s, (a, c) in enumerate(zip(A[1:], C[1:]), start=1):
+            dy = np.dot(K[:s].T, a[:s]) * h
+            K[s] = self.fun(t + c * h, y + dy)
+        y_new = y + h * np.dot(K[:-1].T, B)
+        f_new = self.fun(t + h, y_new)
+        K[-1] = f_new
+        self.y_new, self.f_new = y_new, f_new
+        scale = self.atol + np.maximum(np.abs(y), np.abs(y_new)) * self.rtol
+        return self._norm(np.dot(K.T, E) * h / scale)
+
+    def accept(self, t_old, t):
+        self.y_old = self.y
+        self.y, self.f = self.y_new, self.f_new
+
+    def keep_y(self, keep, first):
+        if keep:
+            self.ys.append(self.y.copy())
+
+    def dense(self, t_old, t, lo, hi):
+        Q = self.K.T.dot(P)
+        h = t - t_old
+        te = self.t_eval[lo:hi][::-1] if self.direction < 0 else self.t_eval[lo:hi]
+        x = (te - t_old) / h
+        p = np.cumprod(np.tile(x, (Q.shape[1], 1)), axis=0)
+        y = h * np.dot(Q, p)
+        y += self.y[:, None]
+        for j in range(te.shape[0]):
+            self.dense_rows.append((float(te[j]), y[:, j]))
+
+
+# ============================================================================ HIP backend
+def _ptr_array(ts) -> ctypes.Array:
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+_A6 = np.zeros((6, 6), dtype=np.float64)
+_A6[:, :5] = A
+_A6 = np.ascontiguousarray(_A6)
+_B6 = np.ascontiguousarray(B, dtype=np.float64)
+_E7 = np.ascontiguousarray(E, dtype=np.float64)
+_P74 = np.ascontiguousarray(P, dtype=np.float64)
+
+
+def time_scalars(t):
+    """Per-RHS scalars exactly as ode_func forms them (samplers.py:209-216): the score model sees
+    t32 = float32(t) and sigma(t32) in fp32; the coefficient is -(0.5 * g^2) with
+    g = sde_coeff(torch.tensor(t)) -- float32 when t is a Python float (the first evaluation at
+    t0, ivp.py maps t_span to float), float64 for the NumPy scalars of every later evaluation."""
+    t32 = float(np.float32(t))
+    sig = float(sde.sigma(torch.tensor([t32], dtype=torch.float32))[0])
+    g = sde.diffusion(torch.tensor(t)).numpy()
+    coef = -(0.5 * (g ** 2))
+    return t32, sig, float(coef)
+
+
+def stage_scalars(ts: List[float]):
+    """time_scalars for the 6 stage times of one attempt in one vectorised pass (the stage times
+    are NumPy float64, so g is float64). Bitwise equal to per-value time_scalars
+    (tests/test_cpu_host.py::test_ode_stage_scalars_vectorised)."""
+    tt = np.asarray(ts, dtype=np.float64)
+    t32 = tt.astype(np.float32)
+    sig = sde.sigma(torch.from_numpy(t32)).numpy().astype(np.float32)
+    g = sde.diffusion(torch.from_numpy(tt)).numpy()
+    coef = -(0.5 * (g ** 2))
+    return (np.ascontiguousarray(t32), np.ascontiguousarray(sig), np.ascontiguousarray(coef, dtype=np.float64))
+
+
+class DeviceRk45:
+    """State y, K_0..K_6 and y_new as fp64 (R*9) device tensors; every RHS is a HIP launch."""
+
+    def __init__(self, heads, pobj: torch.Tensor, y0: torch.Tensor, k: int, rtol: float = 1e-5,
+                 atol: float = 1e-5):
+        self.lib = _lib.load()
+        self.h = heads
+        self.dev = heads.device
+        self.pobj = pobj
+        self.R = y0.numel() // arch.POSE_DIM
+        self.n = self.R * arch.POSE_DIM
+        self.k = int(k)
+        self.rtol, self.atol = float(rtol), float(atol)
+        self.y = y0.reshape(-1).to(self.dev, torch.float64).contiguous()
+        self.K = [torch.empty(self.n, dtype=torch.float64, device=self.dev) for _ in range(N_STAGES + 1)]
+        self.f1 = torch.empty(self.n, dtype=torch.float64, device=self.dev)
+        nb = int(self.lib.gp_ode_workspace_size(self.R))
+        self.ws = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+        self.scal = torch.zeros(8, dtype=torch.float64, device=self.dev)   # [d0, d1, d2, err]
+        self.ys: List[torch.Tensor] = []
+        self.dense_out: Optional[torch.Tensor] = None
+        self.t_eval_dev = None
+
+    def _s(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _rhs(self, t, kin, acoef, h, kout):
+        t32, sig, coef = time_scalars(t)
+        nk = len(kin)
+        karr = _ptr_array(kin) if nk else None
+        aarr = (ctypes.c_double * nk)(*acoef) if nk else None
+        check(self.lib.gp_ode_rhs(ctypes.byref(self.h.w), ctypes.c_void_p(self.pobj.data_ptr()), t32, sig, coef,
+                                  ctypes.c_void_p(self.y.data_ptr()), karr, aarr, nk, float(h), self.R, self.k,
+                                  ctypes.c_void_p(kout.data_ptr()), ctypes.c_void_p(self.ws.data_ptr()),
+                                  self.ws.numel(), self._s()), "ode_rhs")
+
+    def set_t_eval(self, t_eval, direction, keep_all):
+        self.t_eval = t_eval
+        self.direction = direction
+        self.keep_all = keep_all
+        self.t_eval_dev = torch.from_numpy(np.ascontiguousarray(t_eval, dtype=np.float64)).to(self.dev)
+        rows = t_eval.shape[0] if keep_all else 1
+        self.dense_out = torch.empty((rows, self.n), dtype=torch.float64, device=self.dev)
+
+    def rhs0(self, t):
+        self._rhs(t, [], [], 0.0, self.K[0])
+
+    def init_norms(self):
+        check(self.lib.gp_ode_init_norms(ctypes.c_void_p(self.y.data_ptr()), ctypes.c_void_p(self.K[0].data_ptr()),
+                                         None, self.n, self.atol, self.rtol, ctypes.c_void_p(self.scal.data_ptr()),
+                                         self._s()), "ode_init_norms")
+        v = self.scal[:2].cpu().numpy()
+        return v[0], v[1]
+
+    def rhs_euler(self, t, h):
+        self._rhs(t, [self.K[0]], [1.0], h, self.f1)
+
+    def diff_norm(self):
+        check(self.lib.gp_ode_init_norms(ctypes.c_void_p(self.y.data_ptr()), ctypes.c_void_p(self.K[0].data_ptr()),
+                                         ctypes.c_void_p(self.f1.data_ptr()), self.n, self.atol, self.rtol,
+                                         ctypes.c_void_p(self.scal.data_ptr()), self._s()), "ode_init_norms")
+        return self.scal[2:3].cpu().numpy()[0]
+
+    def attempt(self, t, h):
+        stage_t = [t + c * h for c in C[1:]] + [t + h]   # rk_step: fun(t + c * h, ...) for s = 1..5, then t + h
+        t32, sig, coef = stage_scalars(stage_t)
+        self.y_new = torch.empty(self.n, dtype=torch.float64, device=self.dev)
+        check(self.lib.gp_ode_attempt(
+            ctypes.byref(self.h.w), ctypes.c_void_p(self.pobj.data_ptr()), t32.ctypes.data_as(ctypes.c_void_p),
+            sig.ctypes.data_as(ctypes.c_void_p), coef.ctypes.data_as(ctypes.c_void_p),
+            ctypes.c_void_p(self.y.data_ptr()), _ptr_array(self.K), _A6.ctypes.data_as(ctypes.c_void_p),
+            _B6.ctypes.data_as(ctypes.c_void_p), _E7.ctypes.data_as(ctypes.c_void_p), float(h), self.rtol,
+            self.atol, self.R, self.k, ctypes.c_void_p(self.y_new.data_ptr()),
+            ctypes.c_void_p(self.scal[3:].data_ptr()), ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel(),
+            self._s()), "ode_attempt")
+        return self.scal[3:4].cpu().numpy()[0]
+
+    def accept(self, t_old, t):
+        self.y_old = self.y
+        self.y = self.y_new
+        self.K[0], self.K[N_STAGES] = self.K[N_STAGES], self.K[0]   # FSAL: f = f_new
+
+    def keep_y(self, keep, first):
+        if keep:
+            self.ys.append(self.y)
+
+    def dense(self, t_old, t, lo, hi):
+        """Called before accept(): self.y is still the step's y_old, K the step's stages."""
+        h = t - t_old
+        if self.keep_all:
+            i0, i1, base, rev = lo, hi, (self.t_eval.shape[0] - 1 if self.direction < 0 else 0), int(self.direction < 0)
+        else:   # only the final t_eval point (t_bound side) is kept
+            last = 0 if self.direction < 0 else self.t_eval.shape[0] - 1
+            if not (lo <= last < hi):
+                return
+            i0, i1, base, rev = last, last + 1, last, 0
+        check(self.lib.gp_ode_dense(_ptr_array(self.K), _P74.ctypes.data_as(ctypes.c_void_p),
+                                    ctypes.c_void_p(self.y.data_ptr()), ctypes.c_void_p(self.t_eval_dev.data_ptr()),
+                                    i0, i1, base, rev, float(t_old), float(h), self.n,
+                                    ctypes.c_void_p(self.dense_out.data_ptr()), self._s()), "ode_dense")
+
+    def outputs(self) -> torch.Tensor:
+        """(n_t, R*9) fp64 outputs in solve_ivp order (all kept, or only the last)."""
+        if self.dense_out is not None:
+            return self.dense_out
+        return torch.stack(self.ys, 0)

@@ -30,7 +30,7 @@ enum { GP_OK = 0, GP_ERR_INVALID = -1, GP_ERR_LAUNCH = -2, GP_ERR_UNSUPPORTED = 
 const char *gp_last_error(void);
 /* ABI version of this header. */
 int gp_abi_version(void);
-#define GP_ABI_VERSION 1
+#define GP_ABI_VERSION 2
 
 /* ===================================================================== operator level
  * Drop-in forward ops of `pointnet2_cuda` (same argument meaning and layouts). */
@@ -135,6 +135,49 @@ int gp_randn(uint64_t seed, uint32_t stream, int rows, int cols, float *out, hip
  * + pts_center on [6:], and q (R,7) fp64. */
 int gp_pose_epilogue_f64(double *pose, int rows, int k, const float *pts_center, double *q,
                          hipStream_t stream);
+
+/* ===================================================================== ODE sampler
+ * cond_ode_sampler (samplers.py:180-258): the probability-flow ODE dx/dt = -0.5 g(t)^2 score
+ * integrated by a Dormand-Prince 5(4) pair whose controller restates scipy solve_ivp RK45
+ * (samplers.py:226-234; the controller's scalars run on the host, genpose2_amd/ode.py).
+ * The state y, the stage derivatives K_0..K_6 and y_new are fp64 (R,9) device arrays; the score
+ * model sees float(y) (samplers.py:210) at t32 = float(t) with sigma = sigma(t32) in fp32, and a
+ * derivative is K = coef * double(score) with coef = -(0.5 g(t)^2) formed on the host.
+ * Every call needs gp_ode_workspace_size(rows) bytes of workspace (time rows + error partials). */
+size_t gp_ode_workspace_size(int rows);
+/* One right-hand side: kout = coef * score(float(y + (sum_{j<nk} acoef[j] kin[j]) * h), t32).
+ * kin (HOST array of nk device pointers) and acoef (HOST, nk) may be NULL when nk == 0. */
+int gp_ode_rhs(const gp_head_weights *w, const float *pobj, float t32, float sigma, double coef,
+               const double *y, const double *const *kin, const double *acoef, int nk, double h,
+               int rows, int k, double *kout, void *workspace, size_t workspace_bytes,
+               hipStream_t stream);
+/* One attempted step (scipy rk.py rk_step + _estimate_error_norm): for s = 1..5
+ * K_s = f(t_s, y + (sum_{j<s} A[s][j] K_j) h); y_new = y + (sum_{j<6} B_j K_j) h;
+ * K_6 = f(t + h, y_new); err_out[0] = rms((sum_j E_j K_j) h / (atol + max(|y|,|y_new|) rtol)).
+ * t32_6 / sigma_6 / coef_6 (HOST, 6 each): stage times 1..5 and t + h. kslots (HOST, 7 device
+ * pointers) holds K_0 = f(t, y) on entry. tableau_a (HOST 6x6 row-major), b (HOST 6), e (HOST 7). */
+int gp_ode_attempt(const gp_head_weights *w, const float *pobj, const float *t32_6,
+                   const float *sigma_6, const double *coef_6, const double *y,
+                   double *const *kslots, const double *tableau_a, const double *b, const double *e,
+                   double h, double rtol, double atol, int rows, int k, double *ynew, double *err_out,
+                   void *workspace, size_t workspace_bytes, hipStream_t stream);
+/* select_initial_step norms (scipy _ivp/common.py) over n elements, scale = atol + |y0| rtol:
+ * f1 == NULL -> out[0] = rms(y0/scale), out[1] = rms(f0/scale); else out[2] = rms((f1-f0)/scale). */
+int gp_ode_init_norms(const double *y0, const double *f0, const double *f1, long long n,
+                      double atol, double rtol, double *out, hipStream_t stream);
+/* Dense output of an accepted step (scipy RkDenseOutput): for i in [i0, i1),
+ * x = (t_eval[i] - t_old)/h, out[row] = h * (K^T P) cumprod([x,x,x,x]) + y_old with
+ * row = reverse ? i_base - i : i - i_base. P7x4 (HOST 7x4), kslots (HOST, 7 device pointers). */
+int gp_ode_dense(const double *const *kslots, const double *P7x4, const double *y_old,
+                 const double *t_eval, int i0, int i1, int i_base, int reverse, double t_old,
+                 double h, long long n, double *out, hipStream_t stream);
+/* Final denoise (samplers.py:240-249) + epilogue: grad = score(float(x), t32) fp32,
+ * x + (0 - g2 * grad) * step (fp32 product, fp64 sum), GS of [:6], + pts_center, quaternion
+ * (posenet_agent.py:554-556) -> pose (R,9) fp64, q (R,7) fp64. */
+int gp_ode_denoise(const gp_head_weights *w, const float *pobj, float t32, float sigma, float g2,
+                   float step, const double *x, int rows, int k, const float *pts_center,
+                   double *pose, double *q, void *workspace, size_t workspace_bytes,
+                   hipStream_t stream);
 
 /* ===================================================================== ScaleNet
  * ScaleNet.forward (scalenet.py:33-49): axes (b,3,3), pts_feat (b,1024) -> length (b,3). */

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     from genpose2_amd import _lib
     assert set(_lib.EXPORTED) == declared   # the ctypes binding covers exactly the header
     lib = _lib.load()
-    assert lib.gp_abi_version() == 1
+    assert lib.gp_abi_version() == 2
     assert lib.gp_encoder_workspace_size(64, 1024) > 0 and lib.gp_pc_workspace_size(3200) >= 3200 * 36
 
 
@@ -73,25 +73,50 @@ def test_pc_step_table_matches_reference_formula():
     assert tab[0, 4] == np.sqrt(np.float32(ts[0] - ts[1]))
 
 
-@pytest.mark.parametrize("t_eval", [None, 15])
-def test_rk45_restatement_matches_scipy(t_eval):
+@pytest.mark.parametrize("t_eval", [None, 15, 400])
+@pytest.mark.parametrize("t0", [1.0, 0.55])
+def test_rk45_controller_matches_scipy(t_eval, t0):
+    """The RK45 controller (rk45_drive) over scipy's own NumPy stage arithmetic (NumpyRk45)
+    reproduces solve_ivp bit for bit: accept/reject sequence, times, outputs, nfev."""
     from scipy.integrate import solve_ivp
-    from genpose2_amd.ode import rk45_solve
+    from genpose2_amd.ode import NumpyRk45, rk45_drive
     A = np.array([[-0.5, 2.0, 0.0], [-2.0, -0.5, 0.3], [0.0, -0.3, -0.1]])
 
     def f_np(t, y):
         return A @ y + np.sin(3 * t) * y ** 2 * 0.1
 
     y0 = np.array([1.0, -0.5, 2.0])
-    te = None if t_eval is None else np.linspace(1.0, 1e-5, t_eval)
-    ref = solve_ivp(f_np, (1.0, 1e-5), y0, method="RK45", rtol=1e-5, atol=1e-5, t_eval=te)
-    ts, ys, nfev = rk45_solve(lambda t, y: torch.from_numpy(f_np(t, y.numpy())), 1.0, torch.from_numpy(y0), 1e-5,
-                              t_eval=te)
-    # same accept/reject sequence; the error estimate sum_i E_i K_i cancels catastrophically, so
-    # BLAS vs torch summation order moves step sizes at ~1e-9 relative
-    assert nfev == ref.nfev
-    np.testing.assert_allclose(ts, ref.t, rtol=1e-7, atol=1e-12)
-    np.testing.assert_allclose(ys.numpy().T, ref.y, rtol=1e-7, atol=1e-10)
+    te = None if t_eval is None else np.linspace(t0, 1e-5, t_eval)
+    ref = solve_ivp(f_np, (t0, 1e-5), y0, method="RK45", rtol=1e-5, atol=1e-5, t_eval=te)
+    be = NumpyRk45(f_np, y0)
+    ts, nfev, status = rk45_drive(be, t0, 1e-5, t_eval=te)
+    assert status == 0 and nfev == ref.nfev
+    np.testing.assert_array_equal(ts, ref.t)
+    ys = np.stack(be.ys, 1) if te is None else np.stack([v for _, v in be.dense_rows], 1)
+    np.testing.assert_array_equal(ys, ref.y)
+
+
+def test_ode_stage_scalars_vectorised():
+    """stage_scalars (one vectorised pass per attempt) == time_scalars per value, which forms the
+    scalars as ode_func does (samplers.py:209-216)."""
+    from genpose2_amd.ode import stage_scalars, time_scalars
+    rng = np.random.default_rng(3)
+    ts = [np.float64(v) for v in np.concatenate([rng.uniform(1e-5, 1.0, 3000), [1.0, 0.55, 1e-5, 0.2]])]
+    for i in range(0, len(ts) - 6, 6):
+        t32, sig, coef = stage_scalars(ts[i:i + 6])
+        for j in range(6):
+            a, b, c = time_scalars(ts[i + j])
+            assert (float(t32[j]), float(sig[j]), float(coef[j])) == (a, b, c)
+
+
+def test_ode_first_rhs_uses_float32_diffusion():
+    """solve_ivp passes t0 as a Python float, so ode_func's torch.tensor(t) is float32 for the first
+    evaluation only (ivp.py map(float, t_span); sde.py:22-27)."""
+    from genpose2_amd.ode import time_scalars
+    a = time_scalars(0.55)[2]
+    b = time_scalars(np.float64(0.55))[2]
+    g32 = 0.01 * (50.0 / 0.01) ** torch.tensor(0.55)
+    assert g32.dtype == torch.float32 and a != b
 
 
 def test_dbscan_restatement_matches_sklearn():

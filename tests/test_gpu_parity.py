@@ -194,6 +194,17 @@ def test_ode_pred_func_vs_golden(tag, rot_tol, tr_rel):
     assert np.abs(p[..., :6] - ref[..., :6]).max() < rot_tol
     assert rel(p[..., 6:], ref[..., 6:]) < tr_rel
     assert np.abs(q.cpu().numpy()[..., :4] - g[f"{tag}_pred_q"][..., :4]).max() < rot_tol * 10
+    if tag == "t055_s20":   # the shipped T0; at T0=1 the controller may branch on ~1e-7 score differences
+        assert agent.last_nfev == int(g[f"{tag}_nfev"])
+    # return_process: the whole trajectory (solve_ivp outputs, GS'ed, + pts_center)
+    agent.noise_feed = NoiseFeed(torch.from_numpy(g[f"{tag}_prior"]))
+    pose2, xs = agent.pred_func(data, repeat_num=5, T0=float(g[f"{tag}_T0"]), return_process=True)
+    assert torch.equal(pose2, pose)   # the trajectory bookkeeping does not change the result
+    xr = g[f"{tag}_xs"]
+    if agent.last_nfev == int(g[f"{tag}_nfev"]):
+        assert xs.shape == xr.shape
+        assert np.abs(xs.cpu().numpy()[..., :6] - xr[..., :6]).max() < rot_tol
+        assert rel(xs.cpu().numpy()[..., 6:], xr[..., 6:]) < tr_rel
 
 
 @pytest.mark.parametrize("mode", ["pc", "ode"])
