@@ -17,7 +17,7 @@ import torch
 
 from . import aggregate, arch, device as dev, sde, weights
 from .config import GenPoseConfig
-from .ode import DeviceRk45, rk45_drive, time_scalars
+from .ode import DeviceRk45, rk45_device, rk45_drive, time_scalars
 
 
 def _as_config(cfg) -> GenPoseConfig:
@@ -49,6 +49,7 @@ class PoseNet:
         self.noise_feed: Optional[NoiseFeed] = None
         self._calls = 0
         self.after_encode = None                   # optional callable run by pred_func after the encoder
+        self.ode_host_control = False              # ODE: True runs the RK45 controller on the host
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(self.cfg.noise_seed)
         self.weights_source = f"synthetic(seed={self.cfg.seed})"
@@ -188,10 +189,15 @@ class PoseNet:
             x0 = rep_init.to(torch.float32) + x0
         be = DeviceRk45(self.heads, pobj, x0.to(self.device), K)
         t_eval = None if steps is None else np.linspace(T0, eps, steps)
-        ts, nfev, _ = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process)
+        if want_process or self.ode_host_control:
+            # every solve_ivp output is kept: host-side controller, one error norm read per attempt
+            _, nfev, _ = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process)
+            ys = be.outputs()                  # (n_t or 1, R*9) fp64
+            x = ys[-1]
+        else:
+            # default: the step controller runs on the device (no host round trip per attempt)
+            x, nfev, _ = rk45_device(be, T0, eps, t_eval=t_eval)
         self.last_nfev = nfev
-        ys = be.outputs()                      # (n_t or 1, R*9) fp64
-        x = ys[-1]
         # denoise with the PC predictor step (samplers.py:240-249), GS, + pts_center, quaternion
         t32, sig, _ = time_scalars(eps)
         vec_eps = torch.full((1,), eps, dtype=torch.float32)

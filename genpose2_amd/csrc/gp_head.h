@@ -334,8 +334,9 @@ __device__ __forceinline__ void quat_from_gs(const T* v, T* qo) {
 
 // Head layer-1 t block for one time value (HT threads): tproj = W1_t . relu(W_te . [sin, cos](GFP(t)) + b_te)
 // (scorenet.py:77-88 GaussianFourierProjection + t_encoder, the t columns of the first head layer).
+// Writes out[o] for o in [o0, o1) (the caller's slice of the 768-row).
 __device__ __forceinline__ void time_row(const gp_head_weights& w, float t, float* emb, float* tf,
-                                         float* __restrict__ out) {
+                                         float* __restrict__ out, int o0 = 0, int o1 = 768) {
     const int i = threadIdx.x;
     if (i < 64) {  // x_proj = x[:, None] * W[None, :] * 2 * np.pi (scorenet.py:87)
         const float a = fmul(fmul(fmul(t, w.gfp_w[i]), 2.0f), 3.14159265358979323846f);
@@ -349,7 +350,7 @@ __device__ __forceinline__ void time_row(const gp_head_weights& w, float t, floa
         tf[i] = fmaxf(acc + w.te_b[i], 0.f);
     }
     __syncthreads();
-    for (int o = i; o < 768; o += HT) {
+    for (int o = o0 + i; o < o1; o += HT) {
         float acc = 0.f;
         for (int c = 0; c < 128; ++c) acc += w.h1t_t[c * 768 + o] * tf[c];
         out[o] = acc;

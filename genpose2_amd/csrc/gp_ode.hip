@@ -13,10 +13,28 @@
 
 #define ODE_NK 7   // Dormand-Prince stages incl. the FSAL derivative
 
+// Device-resident RK45 controller state (the device-controlled path, gp_ode_auto_*). One copy per
+// attempt parity: the control kernel of attempt n reads ctl[n & 1] and writes ctl[(n + 1) & 1], the
+// stage kernels of attempt n read ctl[(n + 1) & 1]. Field order fixed (doubles, floats, ints) so the
+// host mirror (genpose2_amd/ode.py OdeCtl) has the same layout.
+struct OdeCtl {
+    double t, h_abs;              // solver time; step size carried to the next step (scipy self.h_abs)
+    double t_old, h_last;         // last accepted step (dense output)
+    double h, t_new, h_abs_loc;   // the prepared attempt (scipy _step_impl locals h, t_new, h_abs)
+    double coef[6];               // -(0.5 g(t_s)^2) of the attempt's 6 stage times
+    float t32[6], sig[6];         // float32(t_s), sigma(t32)
+    int status;                   // 0 running, 1 finished, -1 step size below spacing (scipy failure)
+    int active;                   // the prepared attempt runs
+    int rejected;                 // scipy step_rejected within the current step
+    int nfev, n_acc, yi;          // RHS evaluations, accepted steps, y buffer holding the state
+    int kidx[ODE_NK];             // K slot permutation (FSAL swaps slots 0 and 6 on acceptance)
+};
+static_assert(sizeof(OdeCtl) == 208, "OdeCtl layout is mirrored on the host");
+
 struct OdeStageArgs {
     gp_head_weights w;
     const float* pobj;
-    const float* tproj;          // (768) time row of this stage's t
+    const float* tproj;          // (768) time row of this stage's t (host-controlled calls)
     float sigma;                 // sigma(t32), fp32 (score = f / (sigma + 1e-7))
     double coef;                 // -(0.5 * g(t)^2)
     const double* y;             // (R,9) state at the step's start
@@ -31,6 +49,12 @@ struct OdeStageArgs {
     double rtol, atol;
     double* part;                // (nwg) sum over the workgroup's elements of (err/scale)^2
     int rows, kper;
+    // device-controlled attempts: state, time rows and buffers resolved from ctl
+    const OdeCtl* ctl;           // null for host-controlled calls
+    const float* tproj6;         // (6,768) rows of the prepared attempt
+    double* ybuf[2];
+    double* kbuf[ODE_NK];
+    int stage;                   // 1..6
 };
 
 // MODE 0: stage derivative. MODE 1: last stage of an attempt (y_new, K_6, error partials).
@@ -41,6 +65,28 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
     __shared__ double y0s[16 * 9], y1s[16 * 9], esq[16 * 9];
     const int tid = threadIdx.x;
     const int r0 = blockIdx.x * 16;
+    const double* y = a.y;
+    const double* kin[ODE_NK];
+#pragma unroll
+    for (int j = 0; j < ODE_NK; ++j) kin[j] = a.k[j];
+    double h = a.h, coef = a.coef;
+    float sigma = a.sigma;
+    const float* tproj = a.tproj;
+    double* kout = a.kout;
+    double* ynew = a.ynew;
+    if (a.ctl != nullptr) {   // device-controlled: skip when no attempt was prepared
+        const OdeCtl* c = a.ctl;
+        if (!c->active) return;
+        y = a.ybuf[c->yi];
+#pragma unroll
+        for (int j = 0; j < ODE_NK; ++j) kin[j] = a.kbuf[c->kidx[j]];
+        h = c->h;
+        coef = c->coef[a.stage - 1];
+        sigma = c->sig[a.stage - 1];
+        tproj = a.tproj6 + (size_t)(a.stage - 1) * 768;
+        kout = a.kbuf[c->kidx[a.stage]];
+        ynew = a.ybuf[c->yi ^ 1];
+    }
     stage_small_weights<1, EVAL_WV>(a.w, sm);
     for (int i = tid; i < 256; i += EVAL_WV * 64) {
         const int c = i >> 4, j = i & 15;
@@ -49,18 +95,18 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         if (r < a.rows && j < 9) {
 #pragma clang fp contract(off)
             const size_t e = (size_t)r * 9 + j;
-            const double y = a.y[e];
-            double yi = y;
+            const double yv = y[e];
+            double yi = yv;
             if (a.nk > 0) {
-                double acc = a.k[0][e] * a.a[0];
-                for (int s = 1; s < a.nk; ++s) acc = acc + a.k[s][e] * a.a[s];
-                yi = y + acc * a.h;
+                double acc = kin[0][e] * a.a[0];
+                for (int s = 1; s < a.nk; ++s) acc = acc + kin[s][e] * a.a[s];
+                yi = yv + acc * h;
             }
             xv = (float)yi;   // torch.tensor(x, dtype=torch.float32) (samplers.py:210)
             if (MODE == 1) {
-                y0s[c * 9 + j] = y;
+                y0s[c * 9 + j] = yv;
                 y1s[c * 9 + j] = yi;
-                a.ynew[e] = yi;
+                ynew[e] = yi;
             }
         }
         sm.xin[i] = xv;
@@ -69,7 +115,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         const int r = r0 + tid;
         obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
     }
-    head_trunk<1, EVAL_WV>(a.w, a.pobj, a.tproj, obj, sm);
+    head_trunk<1, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
     if (tid < 144) {
 #pragma clang fp contract(off)
         const int c = tid / 9, o = tid - c * 9;
@@ -77,17 +123,17 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         double sq = 0.0;
         if (r < a.rows) {
             const size_t e = (size_t)r * 9 + o;
-            const float s = fdiv(head_out(sm, c, o), fadd(a.sigma, 1e-7f));
-            const double kv = a.coef * (double)s;
-            a.kout[e] = kv;
+            const float s = fdiv(head_out(sm, c, o), fadd(sigma, 1e-7f));
+            const double kv = coef * (double)s;
+            kout[e] = kv;
             if (MODE == 1) {
                 // scipy: err = (K^T E) * h / scale, scale = atol + max(|y|, |y_new|) * rtol
-                double acc = a.k[0][e] * a.e[0];
-                for (int s2 = 1; s2 < ODE_NK - 1; ++s2) acc = acc + a.k[s2][e] * a.e[s2];
+                double acc = kin[0][e] * a.e[0];
+                for (int s2 = 1; s2 < ODE_NK - 1; ++s2) acc = acc + kin[s2][e] * a.e[s2];
                 acc = acc + kv * a.e[ODE_NK - 1];
                 const double y0 = y0s[c * 9 + o], y1 = y1s[c * 9 + o];
                 const double sc = a.atol + fmax(fabs(y0), fabs(y1)) * a.rtol;
-                const double er = (acc * a.h) / sc;
+                const double er = (acc * h) / sc;
                 sq = er * er;
             }
         }
@@ -421,4 +467,163 @@ extern "C" int gp_ode_denoise(const gp_head_weights* w, const float* pobj, float
     a.kper = k;
     hipLaunchKernelGGL(ode_denoise_kernel, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
     return gp_check_launch("ode_denoise_kernel");
+}
+
+// ============================================================================ device-controlled RK45
+// The host-controlled path above reads one error norm per attempt (a device->host round trip per
+// attempt, ~30% of the sampler's wall time at config 2). Here the step controller itself runs on
+// the device: ode_control_kernel of attempt n decides attempt n-1 (scipy _step_impl's
+// accept/reject and step-size update from its error norm) and prepares attempt n (min_step check,
+// h, t_new, the 6 stage times and their scalars, and their time rows), so the host only enqueues
+// attempts one ahead and reads a status word. Stage scalars use device pow(); the host path uses
+// glibc's through torch: the two can differ in the last bit (tests/test_gpu_parity.py compares
+// the two paths).
+struct OdeConsts {
+    double t_bound, direction, rtol, atol;
+    double sig_min, base, diff_scale;   // sigma(t) = sig_min * base^t; g = sigma(t) * diff_scale
+    double count;                       // elements of the state (R*9) for the RMS norm
+    int nwg;                            // error partials
+};
+
+#define ODE_CTL_CHUNKS 4   // workgroups per stage time row (768 / 4 outputs each)
+
+__global__ __launch_bounds__(HT) void ode_control_kernel(gp_head_weights w, const OdeCtl* __restrict__ cin,
+                                                         OdeCtl* __restrict__ cout, const double* __restrict__ part,
+                                                         int decide, OdeConsts k, float* __restrict__ tproj6) {
+#pragma clang fp contract(off)
+    __shared__ double red[HT];
+    __shared__ OdeCtl s;
+    __shared__ float emb[128], tf[128];
+    const int tid = threadIdx.x;
+    // error norm of attempt n-1 (same fixed order in every workgroup)
+    double v = 0.0;
+    if (decide)
+        for (int i = tid; i < k.nwg; i += HT) v += part[i];
+    red[tid] = v;
+    __syncthreads();
+    for (int st = HT / 2; st > 0; st >>= 1) {
+        if (tid < st) red[tid] += red[tid + st];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        OdeCtl c = *cin;
+        const double dir = k.direction;
+        if (decide && c.active) {   // scipy RK45._step_impl, after rk_step / _estimate_error_norm
+            const double err = sqrt(red[0]) / sqrt(k.count);
+            c.nfev += 6;
+            if (err < 1.0) {
+                double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * pow(err, -0.2));
+                if (c.rejected) factor = fmin(1.0, factor);
+                c.h_abs = c.h_abs_loc * factor;
+                c.t_old = c.t;
+                c.h_last = c.h;
+                c.t = c.t_new;
+                c.yi ^= 1;
+                const int k0 = c.kidx[0];
+                c.kidx[0] = c.kidx[ODE_NK - 1];
+                c.kidx[ODE_NK - 1] = k0;
+                c.n_acc += 1;
+                c.rejected = 0;
+                if (dir * (c.t - k.t_bound) >= 0.0) c.status = 1;
+            } else {
+                c.h_abs_loc *= fmax(0.2, 0.9 * pow(err, -0.2));
+                c.rejected = 1;
+            }
+        }
+        c.active = 0;
+        if (c.status == 0) {   // prepare the next attempt
+            const double min_step = 10.0 * fabs(nextafter(c.t, dir * INFINITY) - c.t);
+            double ha = c.rejected ? c.h_abs_loc : (c.h_abs < min_step ? min_step : c.h_abs);
+            if (ha < min_step) {
+                c.status = -1;
+            } else {
+                double h = ha * dir;
+                double t_new = c.t + h;
+                if (dir * (t_new - k.t_bound) > 0.0) t_new = k.t_bound;
+                h = t_new - c.t;
+                c.h = h;
+                c.t_new = t_new;
+                c.h_abs_loc = fabs(h);
+                c.active = 1;
+                const double cs[6] = {1.0 / 5.0, 3.0 / 10.0, 4.0 / 5.0, 8.0 / 9.0, 1.0, 0.0};
+                for (int st = 0; st < 6; ++st) {
+                    const double ts = st < 5 ? c.t + cs[st] * h : c.t + h;
+                    const float t32 = (float)ts;
+                    c.t32[st] = t32;
+                    c.sig[st] = fmul((float)k.sig_min, (float)pow(k.base, (double)t32));
+                    const double g = (k.sig_min * pow(k.base, ts)) * k.diff_scale;
+                    c.coef[st] = -(0.5 * (g * g));
+                }
+            }
+        }
+        s = c;
+        if (blockIdx.x == 0 && blockIdx.y == 0) *cout = c;
+    }
+    __syncthreads();
+    if (!s.active) return;
+    // time row slice of stage blockIdx.x: outputs [chunk * 192, chunk * 192 + 192)
+    constexpr int PER = 768 / ODE_CTL_CHUNKS;
+    time_row(w, s.t32[blockIdx.x], emb, tf, tproj6 + (size_t)blockIdx.x * 768, blockIdx.y * PER, blockIdx.y * PER + PER);
+}
+
+// Workspace of the device-controlled path: ctl[2] | time rows (6 x 768 fp32) | error partials.
+static size_t auto_tproj_off() { return 2 * sizeof(OdeCtl); }
+static size_t auto_part_off() { return auto_tproj_off() + 6 * 768 * sizeof(float); }
+
+extern "C" size_t gp_ode_ctl_size(void) { return sizeof(OdeCtl); }
+
+extern "C" size_t gp_ode_auto_workspace_size(int rows) {
+    return auto_part_off() + sizeof(double) * (((size_t)rows + 15) / 16) + 256;
+}
+
+extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, int n, int what,
+                                   double t_bound, double direction, double rtol, double atol, double sig_min,
+                                   double base, double diff_scale, double* y0, double* y1,
+                                   double* const* kslots, const double* tableau_a, const double* b,
+                                   const double* e, int rows, int k, void* workspace, size_t workspace_bytes,
+                                   hipStream_t stream) {
+    GP_REQUIRE(w && pobj && y0 && y1 && kslots && tableau_a && b && e && workspace && rows >= 1 && k >= 1 && n >= 0,
+               "ode_auto_attempt: bad arguments");
+    GP_REQUIRE(workspace_bytes >= gp_ode_auto_workspace_size(rows), "ode_auto_attempt: workspace too small");
+    for (int j = 0; j < ODE_NK; ++j) GP_REQUIRE(kslots[j] != nullptr, "ode_auto_attempt: null K slot");
+    char* ws = static_cast<char*>(workspace);
+    OdeCtl* ctl = reinterpret_cast<OdeCtl*>(ws);
+    float* tproj6 = reinterpret_cast<float*>(ws + auto_tproj_off());
+    double* part = reinterpret_cast<double*>(ws + auto_part_off());
+    const int nwg = (rows + 15) / 16;
+    OdeConsts kc = {t_bound, direction, rtol, atol, sig_min, base, diff_scale, (double)rows * 9.0, nwg};
+    OdeCtl* cin = ctl + (n & 1);
+    OdeCtl* cout = ctl + ((n + 1) & 1);
+    GP_REQUIRE(what >= 1 && what <= 3, "ode_auto_attempt: what must be 1 (control), 2 (stages) or 3 (both)");
+    if (what & 1) {
+        hipLaunchKernelGGL(ode_control_kernel, dim3(6, ODE_CTL_CHUNKS), dim3(HT), 0, stream, *w, (const OdeCtl*)cin,
+                           cout, (const double*)part, n > 0 ? 1 : 0, kc, tproj6);
+        const int rc = gp_check_launch("ode_control_kernel");
+        if (rc || !(what & 2)) return rc;
+    }
+    OdeStageArgs a = {};
+    a.w = *w;
+    a.pobj = pobj;
+    a.rows = rows;
+    a.kper = k;
+    a.rtol = rtol;
+    a.atol = atol;
+    a.ctl = cout;
+    a.tproj6 = tproj6;
+    a.ybuf[0] = y0;
+    a.ybuf[1] = y1;
+    for (int j = 0; j < ODE_NK; ++j) a.kbuf[j] = kslots[j];
+    for (int s = 1; s < 6; ++s) {
+        a.stage = s;
+        a.nk = s;
+        for (int j = 0; j < s; ++j) a.a[j] = tableau_a[s * 6 + j];
+        hipLaunchKernelGGL(ode_stage_kernel<0>, dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    }
+    a.stage = 6;
+    a.nk = 6;
+    for (int j = 0; j < 6; ++j) a.a[j] = b[j];
+    for (int j = 0; j < ODE_NK; ++j) a.e[j] = e[j];
+    a.part = part;
+    hipLaunchKernelGGL(ode_stage_kernel<1>, dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    return gp_check_launch("ode_stage_kernel<auto>");
 }

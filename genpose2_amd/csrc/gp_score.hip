@@ -20,6 +20,8 @@
 // order so every workgroup derives the identical grad_norm -- and (b) evaluates the score at step i
 // and publishes its tile's partial. The kernel boundary is the only grid-wide synchronisation.
 
+#include "gp_common.h"
+
 // Phase timestamps for tuning builds only (make EXTRA=-DPC_TRACE; read by scripts/pc_trace.py).
 #ifdef PC_TRACE
 __device__ unsigned long long g_pc_trace[2 * 256 * 8 * 16];

@@ -54,6 +54,30 @@ ERROR_EXPONENT = -1 / (ERROR_ESTIMATOR_ORDER + 1)
 
 
 # ============================================================================ controller
+def initial_step(be, t0: float, tf: float, direction):
+    """RK45.__init__: f = fun(t0, y0) and h_abs = select_initial_step(...) (common.py), over backend
+    `be` (rhs0, init_norms, rhs_euler, diff_norm). Returns (h_abs, nfev)."""
+    interval_length = abs(tf - t0)
+    if interval_length == 0.0:
+        raise ValueError("RK45: empty integration interval (T0 == eps)")
+    nfev = 1
+    be.rhs0(t0)
+    d0, d1 = be.init_norms()
+    if d0 < 1e-5 or d1 < 1e-5:
+        h0 = 1e-6
+    else:
+        h0 = 0.01 * d0 / d1
+    h0 = min(h0, interval_length)
+    be.rhs_euler(t0 + h0 * direction, h0 * direction)
+    nfev += 1
+    d2 = be.diff_norm() / h0
+    if d1 <= 1e-15 and d2 <= 1e-15:
+        h1 = max(1e-6, h0 * 1e-3)
+    else:
+        h1 = (0.01 / max(d1, d2)) ** (1 / (ERROR_ESTIMATOR_ORDER + 1))
+    return min(100 * h0, h1, interval_length, np.inf), nfev
+
+
 def rk45_drive(be, t0: float, t_bound: float, rtol: float = 1e-5, atol: float = 1e-5,
                t_eval: Optional[np.ndarray] = None, keep_all: bool = True):
     """solve_ivp(fun, (t0, t_bound), y0, method="RK45", rtol, atol, t_eval) over backend `be`.
@@ -76,26 +100,7 @@ def rk45_drive(be, t0: float, t_bound: float, rtol: float = 1e-5, atol: float = 
             t_eval = t_eval[::-1]
             t_eval_i = t_eval.shape[0]
         be.set_t_eval(np.ascontiguousarray(t_eval), direction, keep_all)
-    interval_length = abs(tf - t0)
-    if interval_length == 0.0:
-        raise ValueError("RK45: empty integration interval (T0 == eps)")
-    # ---- RK45.__init__: f = fun(t0, y0); h_abs = select_initial_step(...)
-    nfev = 1
-    be.rhs0(t0)
-    d0, d1 = be.init_norms()
-    if d0 < 1e-5 or d1 < 1e-5:
-        h0 = 1e-6
-    else:
-        h0 = 0.01 * d0 / d1
-    h0 = min(h0, interval_length)
-    be.rhs_euler(t0 + h0 * direction, h0 * direction)
-    nfev += 1
-    d2 = be.diff_norm() / h0
-    if d1 <= 1e-15 and d2 <= 1e-15:
-        h1 = max(1e-6, h0 * 1e-3)
-    else:
-        h1 = (0.01 / max(d1, d2)) ** (1 / (ERROR_ESTIMATOR_ORDER + 1))
-    h_abs = min(100 * h0, h1, interval_length, np.inf)
+    h_abs, nfev = initial_step(be, t0, tf, direction)
     ts: List[float] = [t0] if t_eval is None else []
     if t_eval is None:
         be.keep_y(keep_all, first=True)
@@ -378,3 +383,103 @@ class DeviceRk45:
         if self.dense_out is not None:
             return self.dense_out
         return torch.stack(self.ys, 0)
+
+
+# ============================================================================ device-controlled driver
+class OdeCtl(ctypes.Structure):
+    """Host mirror of the device controller record (gp_ode.hip OdeCtl)."""
+    _fields_ = [("t", ctypes.c_double), ("h_abs", ctypes.c_double), ("t_old", ctypes.c_double),
+                ("h_last", ctypes.c_double), ("h", ctypes.c_double), ("t_new", ctypes.c_double),
+                ("h_abs_loc", ctypes.c_double), ("coef", ctypes.c_double * 6), ("t32", ctypes.c_float * 6),
+                ("sig", ctypes.c_float * 6), ("status", ctypes.c_int), ("active", ctypes.c_int),
+                ("rejected", ctypes.c_int), ("nfev", ctypes.c_int), ("n_acc", ctypes.c_int), ("yi", ctypes.c_int),
+                ("kidx", ctypes.c_int * 7)]
+
+
+_STATUS_OFF = OdeCtl.status.offset
+_SIDE = {}   # device -> (side stream, pinned status word), created once
+
+
+def _side_resources(dev):
+    r = _SIDE.get(dev)
+    if r is None:
+        r = (torch.cuda.Stream(device=dev), torch.empty(1, dtype=torch.int32).pin_memory())
+        _SIDE[dev] = r
+    return r
+
+
+def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.ndarray] = None,
+                max_attempts: int = 100000):
+    """solve_ivp(..., method="RK45", t_eval) with the step controller on the device.
+
+    select_initial_step runs host-side exactly as in rk45_drive; every attempted step is then
+    gp_ode_auto_attempt: the control kernel of attempt n decides attempt n-1 and prepares attempt
+    n, the stage kernels follow. The host keeps one attempt enqueued ahead and reads only the
+    status word of the newest controller record, so the device never waits for the host.
+    Returns (x (R*9) fp64 -- the value ``res.y[:, -1]`` that cond_ode_sampler continues from --,
+    nfev, status)."""
+    lib = be.lib
+    if ctypes.sizeof(OdeCtl) != int(lib.gp_ode_ctl_size()):
+        raise RuntimeError("OdeCtl layout does not match libgenpose_hip.so")
+    t0, tf = map(float, (t0, t_bound))
+    direction = np.sign(tf - t0) if tf != t0 else 1
+    if t_eval is not None:
+        t_eval = np.asarray(t_eval, dtype=np.float64)
+        if np.any(t_eval < min(t0, tf)) or np.any(t_eval > max(t0, tf)):
+            raise ValueError("Values in `t_eval` are not within `t_span`.")
+    h_abs, nfev = initial_step(be, t0, tf, direction)
+    dev = be.dev
+    ws = torch.empty(int(lib.gp_ode_auto_workspace_size(be.R)), dtype=torch.uint8, device=dev)
+    rec = ctypes.sizeof(OdeCtl)
+    c0 = OdeCtl(t=t0, h_abs=float(h_abs), nfev=nfev)
+    c0.kidx[:] = list(range(N_STAGES + 1))
+    ws[:rec].copy_(torch.frombuffer(bytearray(c0), dtype=torch.uint8))
+    ybuf = [be.y, torch.empty_like(be.y)]
+    kbuf = list(be.K)
+    karr = _ptr_array(kbuf)
+    stream = torch.cuda.current_stream(dev)
+    side, stat = _side_resources(dev)
+    args = (float(tf), float(direction), be.rtol, be.atol, arch.SIGMA_MIN, arch.SIGMA_MAX / arch.SIGMA_MIN,
+            float(sde._DIFF_SCALE_T), ctypes.c_void_p(ybuf[0].data_ptr()), ctypes.c_void_p(ybuf[1].data_ptr()), karr,
+            _A6.ctypes.data_as(ctypes.c_void_p), _B6.ctypes.data_as(ctypes.c_void_p),
+            _E7.ctypes.data_as(ctypes.c_void_p), be.R, be.k, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+            ctypes.c_void_p(stream.cuda_stream))
+
+    def launch(n, what):
+        check(lib.gp_ode_auto_attempt(ctypes.byref(be.h.w), ctypes.c_void_p(be.pobj.data_ptr()), n, what, *args),
+              "ode_auto_attempt")
+
+    launch(0, 3)
+    n = 0
+    while True:
+        launch(n + 1, 1)                       # decides attempt n, prepares attempt n+1
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        launch(n + 1, 2)                       # attempt n+1 (no-op if attempt n ended the solve)
+        off = ((n + 2) & 1) * rec + _STATUS_OFF
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            stat.copy_(ws[off:off + 4].view(torch.int32), non_blocking=True)
+        side.synchronize()
+        if int(stat[0]) != 0:
+            break
+        n += 1
+        if n > max_attempts:
+            raise RuntimeError("RK45: attempt limit reached")
+    last = ((n + 2) & 1) * rec
+    ctl = OdeCtl.from_buffer_copy(bytes(ws[last:last + rec].cpu().numpy()))
+    if ctl.status < 0:
+        warnings.warn("RK45: required step size is less than spacing between numbers.")
+    x = ybuf[ctl.yi]
+    if t_eval is not None and ctl.status > 0:
+        # res.y[:, -1] is the dense output of the final step at t_eval's last point (= t_bound)
+        step_k = [kbuf[ctl.kidx[j]] for j in range(N_STAGES + 1)]
+        step_k[0], step_k[N_STAGES] = step_k[N_STAGES], step_k[0]     # undo the FSAL swap
+        tev = torch.tensor([t_eval[-1]], dtype=torch.float64, device=dev)
+        out = torch.empty((1, be.n), dtype=torch.float64, device=dev)
+        check(lib.gp_ode_dense(_ptr_array(step_k), _P74.ctypes.data_as(ctypes.c_void_p),
+                               ctypes.c_void_p(ybuf[ctl.yi ^ 1].data_ptr()), ctypes.c_void_p(tev.data_ptr()), 0, 1, 0,
+                               0, float(ctl.t_old), float(ctl.t - ctl.t_old), be.n, ctypes.c_void_p(out.data_ptr()),
+                               ctypes.c_void_p(stream.cuda_stream)), "ode_dense")
+        x = out[0]
+    return x, int(ctl.nfev), int(ctl.status)

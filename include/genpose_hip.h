@@ -171,6 +171,24 @@ int gp_ode_init_norms(const double *y0, const double *f0, const double *f1, long
 int gp_ode_dense(const double *const *kslots, const double *P7x4, const double *y_old,
                  const double *t_eval, int i0, int i1, int i_base, int reverse, double t_old,
                  double h, long long n, double *out, hipStream_t stream);
+/* Device-controlled RK45 (the default pred_func path): the step controller itself runs on the
+ * device. gp_ode_auto_attempt(n, what): what & 1 launches the control kernel of attempt n -- it
+ * decides attempt n-1 from its error norm (scipy _step_impl accept/reject and step-size update)
+ * and prepares attempt n (min_step check, h, t_new, the 6 stage times with their scalars and time
+ * rows); what & 2 launches attempt n's 6 stage kernels, which return at once if no attempt was
+ * prepared. State: two OdeCtl records (gp_ode_ctl_size() bytes each, layout mirrored in
+ * genpose2_amd/ode.py) at the start of the workspace; attempt n reads record n & 1 and writes
+ * record (n + 1) & 1 (the host writes record 0 after select_initial_step). The status field of a
+ * record reads 0 running, 1 finished, -1 step size below the spacing of t. y0/y1: the two fp64
+ * state buffers; kslots (HOST, 7 device pointers), tableau_a (HOST 6x6), b (HOST 6), e (HOST 7). */
+size_t gp_ode_ctl_size(void);
+size_t gp_ode_auto_workspace_size(int rows);
+int gp_ode_auto_attempt(const gp_head_weights *w, const float *pobj, int n, int what,
+                        double t_bound, double direction, double rtol, double atol,
+                        double sig_min, double base, double diff_scale, double *y0, double *y1,
+                        double *const *kslots, const double *tableau_a, const double *b,
+                        const double *e, int rows, int k, void *workspace, size_t workspace_bytes,
+                        hipStream_t stream);
 /* Final denoise (samplers.py:240-249) + epilogue: grad = score(float(x), t32) fp32,
  * x + (0 - g2 * grad) * step (fp32 product, fp64 sum), GS of [:6], + pts_center, quaternion
  * (posenet_agent.py:554-556) -> pose (R,9) fp64, q (R,7) fp64. */

@@ -63,6 +63,12 @@ def main():
     w0 = buf.reshape(2, 256, 8, 16)[(T - 1) & 1, :nwg, 0, :].astype(np.int64)
     seq = [0, 9, 10, 11, 12, 1]
     out["wave0_update_cycles_mean"] = {f"{a}->{b}": float((w0[:, b] - w0[:, a]).mean()) for a, b in zip(seq, seq[1:])}
+    # launch-to-launch: launch T-2's last wave end -> launch T-1's first wave start (same clock domain
+    # only if s_memtime agrees across XCDs; reported per XCD = blockIdx % 8 as well)
+    prev = buf.reshape(2, 256, 8, 16)[(T - 2) & 1, :nwg, :, :9].astype(np.int64)
+    out["gap_prev_end_to_start_cycles"] = float(tr[:, :, 0].min() - prev[:, :, 8].max())
+    out["gap_per_xcd"] = [float(tr[x::8, :, 0].min() - prev[x::8, :, 8].max()) for x in range(8)]
+    out["launch_span_cycles"] = float(tr[:, :, 8].max() - tr[:, :, 0].min())
     print(json.dumps(out, indent=1))
 
 
