@@ -74,6 +74,8 @@ _SIGS: Dict[str, tuple] = {
                                     c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "gp_scale_forward": (c_int, [ctypes.POINTER(ScaleWeights), c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "gp_randn": (c_int, [c_uint64, ctypes.c_uint32, c_int, c_int, c_void_p, c_void_p]),
+    "gp_points_mean": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "gp_bbox_length": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "gp_rank_aggregate": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p,
                                   c_void_p, c_void_p]),
 }

@@ -297,3 +297,83 @@ extern "C" int gp_rank_aggregate(const float* poses, const float* energy, int b,
                        clustering, eps, min_samples, aggregated, sorted_pose, sorted_energy);
     return gp_check_launch("rank_aggregate_kernel");
 }
+
+// ============================================================================ stage glue
+// process_batch's pts_center (datasets_omni6dpose.py:746-752: zero_mean = mean(pts[:, :, :3], 1)).
+// One workgroup per object; per-thread strided sums over points, then a fixed-order tree.
+__global__ __launch_bounds__(256) void points_mean_kernel(const float* __restrict__ pts, int n, int c,
+                                                          float* __restrict__ out) {
+    __shared__ float red[3][256];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    const float* p = pts + (size_t)b * n * c;
+    for (int i = tid; i < n; i += 256) {
+        s0 += p[(size_t)i * c + 0];
+        s1 += p[(size_t)i * c + 1];
+        s2 += p[(size_t)i * c + 2];
+    }
+    red[0][tid] = s0;
+    red[1][tid] = s1;
+    red[2][tid] = s2;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (tid < st) {
+            red[0][tid] += red[0][tid + st];
+            red[1][tid] += red[1][tid + st];
+            red[2][tid] += red[2][tid + st];
+        }
+        __syncthreads();
+    }
+    if (tid < 3) out[(size_t)b * 3 + tid] = fdiv(red[tid][0], (float)n);
+}
+
+extern "C" int gp_points_mean(const float* pts, int b, int n, int c, float* out, hipStream_t stream) {
+    GP_REQUIRE(b >= 0 && n >= 1 && c >= 3 && (b == 0 || (pts && out)), "points_mean: bad arguments");
+    if (!b) return GP_OK;
+    hipLaunchKernelGGL(points_mean_kernel, dim3(b), dim3(256), 0, stream, pts, n, c, out);
+    return gp_check_launch("points_mean_kernel");
+}
+
+// inference_scale without a ScaleNet checkpoint (evaluation_single.py:233-252): the points in the
+// aggregated object frame, q = R^T (p - t), and length = 2 max_n |q| per axis. Max is
+// order-independent, so the result depends only on the per-point arithmetic.
+__global__ __launch_bounds__(256) void bbox_length_kernel(const float* __restrict__ pcl, int n, int c,
+                                                          const float* __restrict__ pose, float* __restrict__ out) {
+#pragma clang fp contract(off)
+    __shared__ float red[3][256];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const float* P = pose + (size_t)b * 16;
+    const float r00 = P[0], r01 = P[1], r02 = P[2], t0 = P[3];
+    const float r10 = P[4], r11 = P[5], r12 = P[6], t1 = P[7];
+    const float r20 = P[8], r21 = P[9], r22 = P[10], t2 = P[11];
+    float m0 = 0.f, m1 = 0.f, m2 = 0.f;
+    const float* p = pcl + (size_t)b * n * c;
+    for (int i = tid; i < n; i += 256) {
+        const float d0 = p[(size_t)i * c] - t0, d1 = p[(size_t)i * c + 1] - t1, d2 = p[(size_t)i * c + 2] - t2;
+        // bmm(R^T, d): row j of R^T is column j of R
+        m0 = fmaxf(m0, fabsf((r00 * d0 + r10 * d1) + r20 * d2));
+        m1 = fmaxf(m1, fabsf((r01 * d0 + r11 * d1) + r21 * d2));
+        m2 = fmaxf(m2, fabsf((r02 * d0 + r12 * d1) + r22 * d2));
+    }
+    red[0][tid] = m0;
+    red[1][tid] = m1;
+    red[2][tid] = m2;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (tid < st) {
+            red[0][tid] = fmaxf(red[0][tid], red[0][tid + st]);
+            red[1][tid] = fmaxf(red[1][tid], red[1][tid + st]);
+            red[2][tid] = fmaxf(red[2][tid], red[2][tid + st]);
+        }
+        __syncthreads();
+    }
+    if (tid < 3) out[(size_t)b * 3 + tid] = red[tid][0] * 2.0f;
+}
+
+extern "C" int gp_bbox_length(const float* pcl, int b, int n, int c, const float* pose, float* length,
+                              hipStream_t stream) {
+    GP_REQUIRE(b >= 0 && n >= 1 && c >= 3 && (b == 0 || (pcl && pose && length)), "bbox_length: bad arguments");
+    if (!b) return GP_OK;
+    hipLaunchKernelGGL(bbox_length_kernel, dim3(b), dim3(256), 0, stream, pcl, n, c, pose, length);
+    return gp_check_launch("bbox_length_kernel");
+}

@@ -203,6 +203,30 @@ def pose_epilogue_f64(pose: torch.Tensor, k: int, pts_center: torch.Tensor):
     return pose, q
 
 
+def points_mean(pts: torch.Tensor) -> torch.Tensor:
+    """gp_points_mean: (B,N,C>=3) -> (B,3) mean of the first three channels over the points."""
+    pts = require_device_tensor(pts, "pts")
+    B, N, C = pts.shape
+    out = torch.empty((B, 3), dtype=torch.float32, device=pts.device)
+    check(_lib.load().gp_points_mean(ctypes.c_void_p(pts.data_ptr()), B, N, C, ctypes.c_void_p(out.data_ptr()),
+                                     ctypes.c_void_p(stream_handle(pts.device))), "points_mean")
+    return out
+
+
+def bbox_length(pcl: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
+    """gp_bbox_length: raw points (B,N,C>=3) and aggregated poses (B,4,4) -> (B,3) box lengths."""
+    pcl = require_device_tensor(pcl, "pcl")
+    pose = require_device_tensor(pose, "pose")
+    B, N, C = pcl.shape
+    if pose.shape != (B, 4, 4):
+        raise ValueError(f"pose must be ({B},4,4), got {tuple(pose.shape)}")
+    out = torch.empty((B, 3), dtype=torch.float32, device=pcl.device)
+    check(_lib.load().gp_bbox_length(ctypes.c_void_p(pcl.data_ptr()), B, N, C, ctypes.c_void_p(pose.data_ptr()),
+                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream_handle(pcl.device))),
+          "bbox_length")
+    return out
+
+
 def randn(seed: int, stream: int, rows: int, cols: int, device) -> torch.Tensor:
     """gp_randn: the device draws gp_pc_sample uses (streams 2j / 2j+1 for step j, cols = 9)."""
     lib = _lib.load()

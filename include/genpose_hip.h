@@ -225,6 +225,16 @@ int gp_rank_aggregate(const float *poses, const float *energy, int b, int k, int
                       int clustering, float eps, int min_samples, float *aggregated,
                       float *sorted_pose, float *sorted_energy, hipStream_t stream);
 
+/* ===================================================================== stage glue
+ * process_batch's pts_center (datasets_omni6dpose.py:746-752): out (b,3) = mean over n of
+ * pts (b,n,c)[:, :, :3], c >= 3. */
+int gp_points_mean(const float *pts, int b, int n, int c, float *out, hipStream_t stream);
+/* inference_scale without a ScaleNet checkpoint (runners/evaluation_single.py:233-252):
+ * pcl (b,n,c) raw points, pose (b,4,4) aggregated [R t; 0 1] -> length (b,3) =
+ * 2 * max_n |R^T (p_n - t)| per axis. */
+int gp_bbox_length(const float *pcl, int b, int n, int c, const float *pose, float *length,
+                   hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

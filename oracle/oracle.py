@@ -439,6 +439,22 @@ def aggregate_pose(pred_pose: np.ndarray, pred_energy: np.ndarray, retain_ratio=
     return out
 
 
+# ============================================================ stage glue
+def points_mean(pts: np.ndarray) -> np.ndarray:
+    """process_batch's pts_center (datasets_omni6dpose.py:746-752): mean of pts[:, :, :3] over points."""
+    return pts[..., :3].astype(np.float64).mean(1).astype(F32)
+
+
+def bbox_length(pcl: np.ndarray, pose: np.ndarray) -> np.ndarray:
+    """inference_scale without a ScaleNet checkpoint (evaluation_single.py:233-252):
+    2 * max_n |R^T (p_n - t)| per axis, fp32 as the reference's CPU tensors."""
+    R = pose[:, :3, :3].astype(F32)
+    t = pose[:, :3, 3].astype(F32)
+    d = (pcl[..., :3].astype(F32) - t[:, None, :]).astype(F32)              # (B, N, 3)
+    q = np.einsum("bji,bnj->bni", R, d).astype(F32)                          # bmm(R^T, d)
+    return (np.abs(q).max(1) * 2).astype(F32)
+
+
 # ============================================================ ScaleNet
 def encode_axes(axes: np.ndarray, dim: int) -> np.ndarray:
     """genpose_utils.py:8-18."""

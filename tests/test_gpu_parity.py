@@ -10,6 +10,7 @@ import pytest
 import torch
 
 from conftest import golden
+from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -417,3 +418,97 @@ def test_pc_philox_equals_injected_draws(score_agent):
     z2 = torch.stack([device.randn(seed, 2 * j + 1, R, 9, DEV) for j in range(T)])
     res_i, q_i, xs_i = heads.pc_sample(pobj, tproj, tab, x0.clone(), K, center, z1=z1, z2=z2, want_xs=True)
     assert torch.equal(res_p, res_i) and torch.equal(q_p, q_i) and torch.equal(xs_p, xs_i)
+
+
+# ---------------------------------------------------------------- stage hand-off
+@pytest.mark.parametrize("n,c", [(1024, 3), (1000, 6), (2048, 3)])
+def test_points_mean_and_bbox_length_vs_oracle(n, c):
+    from genpose2_amd import device as dev
+    rng = np.random.default_rng(n + c)
+    B = 5
+    pcl = (rng.normal(size=(B, n, c)) * 0.05 + 0.3).astype(np.float32)
+    center = dev.points_mean(torch.from_numpy(pcl).to(DEV)).cpu().numpy()
+    assert rel(center, oracle.points_mean(pcl)) < 1e-6
+    q = rng.normal(size=(B, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    pose = np.zeros((B, 4, 4), np.float32)
+    pose[:, :3, :3] = oracle.quaternion_to_matrix(q.astype(np.float32))
+    pose[:, :3, 3] = center
+    pose[:, 3, 3] = 1
+    length = dev.bbox_length(torch.from_numpy(pcl).to(DEV), torch.from_numpy(pose).to(DEV)).cpu().numpy()
+    assert rel(length, oracle.bbox_length(pcl, pose)) < 1e-6
+
+
+def _loader(seed, nb, B, N):
+    from genpose2_amd import synthetic
+    out = []
+    for i in range(nb):
+        pts, _ = synthetic.make_batch(seed + i, B, N)
+        out.append({"pcl_in": torch.from_numpy(pts), "sym_info": torch.zeros(B, 4),
+                    "rotation": torch.eye(3).expand(B, 3, 3).clone(), "translation": torch.zeros(B, 3)})
+    return out
+
+
+def test_stage_files_match_reference_format(tmp_path):
+    """inference_score -> inference_energy -> aggregate_pose -> inference_scale through pickle files
+    in the reference's formats (evaluation_single.py:120,157,219,254,288), against the in-memory
+    calls on the same batches."""
+    import pickle
+    from genpose2_amd import aggregate, runner
+    from genpose2_amd.config import GenPoseConfig
+    cfg = GenPoseConfig(device=DEV, sampling_steps=20, eval_repeat_num=20, T0=1.0)
+    loader = _loader(300, 2, 3, 1024)
+    sp, ep, ap, fp = (str(tmp_path / f) for f in ("score.pkl", "energy.pkl", "agg.pkl", "final.pkl"))
+    runner.inference_score(cfg, loader, sp)
+    runner.inference_energy(cfg, loader, sp, ep)
+    runner.aggregate_pose(cfg, sp, ep, ap)
+    runner.inference_scale(cfg, loader, sp, ap, fp)
+    with open(sp, "rb") as f:
+        poses, feats = pickle.load(f)
+    with open(ep, "rb") as f:
+        energies = pickle.load(f)
+    with open(ap, "rb") as f:
+        aggs = pickle.load(f)
+    with open(fp, "rb") as f:
+        finals, lengths = pickle.load(f)
+    assert len(poses) == len(feats) == len(energies) == len(aggs) == len(finals) == len(lengths) == 2
+    for i, batch in enumerate(loader):
+        assert poses[i].shape == (3, 20, 9) and poses[i].is_cuda and poses[i].dtype == torch.float32
+        assert set(feats[i]) == {"pts_feat", "rgb_feat"} and feats[i]["rgb_feat"] is None
+        assert feats[i]["pts_feat"].shape == (3, 1024) and not feats[i]["pts_feat"].is_cuda
+        assert energies[i].shape == (3, 20, 2) and not energies[i].is_cuda
+        agg = aggregate.aggregate_pose(poses[i], energies[i].to(DEV), cfg.retain_ratio, cfg.clustering,
+                                       cfg.clustering_eps, cfg.clustering_minpts).cpu()
+        assert aggs[i].shape == (3, 4, 4) and torch.equal(aggs[i], agg)
+        assert torch.equal(finals[i], aggs[i])                       # no ScaleNet: aggregated poses
+        ref_len = oracle.bbox_length(batch["pcl_in"].numpy(), aggs[i].numpy())
+        assert rel(lengths[i].numpy(), ref_len) < 1e-6
+        # pts_center of process_batch == mean of the points
+        pb = runner.process_batch(batch, DEV)
+        assert rel(pb["pts_center"].cpu().numpy(), oracle.points_mean(batch["pcl_in"].numpy())) < 1e-6
+        assert pb["gt_pose"].shape == (3, 9)
+
+
+def test_stage_scale_with_scalenet(tmp_path):
+    """inference_scale with a ScaleNet agent: final rotation = pred_scale_func's axes, lengths (B,3)."""
+    import pickle
+    from genpose2_amd import runner
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    cfg = GenPoseConfig(device=DEV, sampling_steps=20, eval_repeat_num=20, T0=1.0)
+    loader = _loader(310, 1, 2, 1024)
+    sp, ap, fp = (str(tmp_path / f) for f in ("score.pkl", "agg.pkl", "final.pkl"))
+    runner.inference_score(cfg, loader, sp)
+    runner.aggregate_pose(cfg, sp, None, ap)
+    scale = PoseNet(cfg.copy(agent_type="scale")).eval()
+    runner.inference_scale(cfg, loader, sp, ap, fp, agent=scale)
+    with open(ap, "rb") as f:
+        aggs = pickle.load(f)
+    with open(sp, "rb") as f:
+        _, feats = pickle.load(f)
+    with open(fp, "rb") as f:
+        finals, lengths = pickle.load(f)
+    _, ref = scale.pred_scale_func({"pts_feat": feats[0]["pts_feat"].to(DEV),
+                                    "axes": aggs[0][:, :3, :3].to(DEV).contiguous()})
+    assert torch.equal(lengths[0], ref.cpu()) and lengths[0].shape == (2, 3)
+    assert torch.equal(finals[0][:, :3, 3], aggs[0][:, :3, 3])

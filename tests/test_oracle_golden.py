@@ -105,3 +105,31 @@ def test_energy_sort_aggregate_scale(energy_sd, scale_sd):
     assert np.abs(a - g["cl_aggregated"]).max() < 1e-4
     L = oracle.scale_forward(scale_sd, g["pts_feat"], g["scale_axes"])
     assert rel(L, g["scale_length"]) < 1e-5
+
+
+def test_stage_glue_oracle_restatements():
+    """oracle.points_mean / bbox_length against the reference's own torch expressions
+    (datasets_omni6dpose.py:746-752; evaluation_single.py:233-252), typed out op for op."""
+    import torch
+    rng = np.random.default_rng(4)
+    B, N = 3, 1000
+    pcl = rng.normal(size=(B, N, 3)).astype(np.float32) * 0.05 + np.array([0.0, 0.1, 0.7], np.float32)
+    ref_center = torch.mean(torch.from_numpy(pcl)[:, :, :3], dim=1).numpy()
+    np.testing.assert_allclose(oracle.points_mean(pcl), ref_center, rtol=1e-6, atol=1e-7)
+    q = rng.normal(size=(B, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    pose = np.zeros((B, 4, 4), np.float32)
+    pose[:, :3, :3] = oracle.quaternion_to_matrix(q.astype(np.float32))
+    pose[:, :3, 3] = ref_center
+    pose[:, 3, 3] = 1
+    p = torch.from_numpy(pcl)
+    rotation = torch.from_numpy(pose)[:, :3, :3]
+    rotation_t = torch.transpose(rotation, 1, 2)
+    translation = torch.from_numpy(pose)[:, :3, 3]
+    p = p - translation.unsqueeze(1)
+    p = p.reshape(-1, 3, 1)
+    rotation_t = torch.repeat_interleave(rotation_t, N, dim=0)
+    p = torch.bmm(rotation_t, p).reshape(-1, N, 3)
+    ref_len, _ = torch.max(torch.abs(p), dim=1)
+    ref_len *= 2
+    np.testing.assert_allclose(oracle.bbox_length(pcl, pose), ref_len.numpy(), rtol=2e-6, atol=1e-7)
