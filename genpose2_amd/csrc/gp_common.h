@@ -107,13 +107,14 @@ __device__ __forceinline__ float rows_sum(float v) {
     const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
-__device__ __forceinline__ float wave_sum(float v) {
+// sum over the 16 lanes of each row (every lane of the row ends with the row's sum)
+__device__ __forceinline__ float row16_sum(float v) {
     v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
     v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
     v = dpp_add<0x141>(v);   // row_half_mirror
-    v = dpp_add<0x140>(v);   // row_mirror
-    return rows_sum(v);
+    return dpp_add<0x140>(v);   // row_mirror
 }
+__device__ __forceinline__ float wave_sum(float v) { return rows_sum(row16_sum(v)); }
 // value of lane 4*(l/4) (first lane of the quad)
 __device__ __forceinline__ float quad_bcast0(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x00, 0xF, 0xF, false));

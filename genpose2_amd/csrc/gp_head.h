@@ -38,9 +38,7 @@ struct HeadSmem {
     f32x4 act1[KG_HID * NT * 64];      // pose_encoder.0 output, accumulator-native [g][ct][lane]
     f32x4 act2[KG_HID * NT * 64];      // pose_encoder.2 output
     float red[NT * 16][9][WV];         // per-wave head-layer-2 partials, wave-minor (head_out reads a row)
-    float xu[NT * 16 * 9];             // PC update inputs: state x and score s of this tile's rows
-    float su[NT * 16 * 9];
-    float noise[NT * 16][2][12];       // PC corrector / predictor draws of this step
+    float xu[NT * 16 * 9];             // PC: last-step mean rows, gathered for the quaternion
     float scratch[WV * 64];
     // small per-launch weights staged once per workgroup (their loads overlap the PC update)
     f32x4 pe0w[16 * 64];               // pose_encoder.0 packed A fragments

@@ -165,111 +165,95 @@ struct PCArgs {
 template <int NT, int WV>
 __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
     constexpr int ROWS = NT * 16;
-    constexpr int NLD = (ROWS * 9 + 63) / 64;   // per-lane loads covering the tile's rows
-    static_assert(ROWS <= 64, "one wave updates the tile");
     __shared__ HeadSmem<NT, WV> sm;
     __shared__ int obj[ROWS];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r0 = blockIdx.x * ROWS;
-    const int nval = min(ROWS, a.rows - r0) * 9;   // valid floats of this tile's (R,9) block
     const int trace_slot = i & 1;
     PC_MARK(0);
     if (wid == 0) {
-        // ---- loads first: x, s (and injected draws) of the tile, grad-norm partials of step i-1
-        float xr[NLD], sr[NLD], z1r[NLD], z2r[NLD];
-        const size_t base = (size_t)r0 * 9;
+        // ---- every load first and unconditional (rows clamped: a guarded load becomes a branch,
+        //      and the compiler then drains the first batch before issuing the next): the
+        //      grad-norm partials of step i-1, then this lane's elements of x, s and the two draws.
+        //      Four lanes per row: part p < 3 owns elements [3p, 3p+3) (rot6 columns a1, a2,
+        //      translation); lane 4c+3 only pads the row.
         const bool inj = a.z1 != nullptr;
         const float* zslot = a.zbuf + (size_t)((i - 1) & 1) * 2 * a.rows * 9;
         const float* z1p = inj ? a.z1 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : zslot;
         const float* z2p = inj ? a.z2 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : zslot + (size_t)a.rows * 9;
+        const float* part = a.part + (size_t)((i - 1) & 1) * a.nwg;
+        float pv[8];
 #pragma unroll
-        for (int j = 0; j < NLD; ++j) {
-            const int e = lane + 64 * j;
-            const bool v = e < nval && i > 0;
-            xr[j] = e < nval ? a.x[base + e] : 0.f;
-            sr[j] = v ? a.s[base + e] : 0.f;
-            z1r[j] = v ? z1p[base + e] : 0.f;
-            z2r[j] = v ? z2p[base + e] : 0.f;
-        }
-        float gacc = 0.f;
-        if (i > 0) {   // 8 independent loads per lane in flight, summed in a fixed order
-            const float* part = a.part + (size_t)((i - 1) & 1) * a.nwg;
-            for (int t0 = 0; t0 < a.nwg; t0 += 512) {
-                float pv[8];
+        for (int u = 0; u < 8; ++u) pv[u] = part[min(lane + 64 * u, a.nwg - 1)];
+        const int p = lane & 3;
+        const int e0 = 3 * (p < 3 ? p : 0);
+        float xv[NT][3], sv[NT][3], z1v[NT][3], z2v[NT][3];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int t = t0 + lane + 64 * u;
-                    pv[u] = t < a.nwg ? part[t] : 0.f;
-                }
+        for (int g = 0; g < NT; ++g) {
+            const size_t e = (size_t)min(r0 + 16 * g + (lane >> 2), a.rows - 1) * 9 + e0;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) gacc += pv[u];
+            for (int k = 0; k < 3; ++k) {
+                xv[g][k] = a.x[e + k];
+                sv[g][k] = a.s[e + k];
+                z1v[g][k] = z1p[e + k];
+                z2v[g][k] = z2p[e + k];
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
+        // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); the same lane
+        // order and xor tree in every workgroup, so all derive the identical value (unused at i=0)
+        float gacc = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) gacc += lane + 64 * u < a.nwg ? pv[u] : 0.f;
+        for (int t0 = 512; t0 < a.nwg; t0 += 512) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) pv[u] = part[min(t0 + lane + 64 * u, a.nwg - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) gacc += t0 + lane + 64 * u < a.nwg ? pv[u] : 0.f;
+        }
         PC_MARK(9);
         if (lane < ROWS) {
             const int r = r0 + lane;
             obj[lane] = (r < a.rows ? r : a.rows - 1) / a.kper;
         }
         PC_MARK(10);
-#pragma unroll
-        for (int j = 0; j < NLD; ++j) {
-            const int e = lane + 64 * j;
-            if (e < ROWS * 9) {
-                sm.xu[e] = xr[j];
-                sm.su[e] = sr[j];
-                const int c = e / 9, k = e - c * 9;
-                sm.noise[c][0][k] = z1r[j];
-                sm.noise[c][1][k] = z2r[j];
-            }
-        }
-        // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); the same lane
-        // order and xor tree in every workgroup, so all derive the identical value
         gacc = wave_sum(gacc);
-        wave_sync();
         PC_MARK(11);
-        // four lanes per row: part p < 3 owns elements [3p, 3p+3) (rot6 columns a1, a2, translation)
-        {
-#pragma clang fp contract(off)
-            const int c = lane >> 2, p = lane & 3;
-            const int r = r0 + c;
-            const int e0 = 3 * (p < 3 ? p : 0);
-            float xv[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) xv[k] = sm.xu[c * 9 + e0 + k];
+        for (int g = 0; g < NT; ++g) {
+#pragma clang fp contract(off)
+            const int c = 16 * g + (lane >> 2);
+            const int r = r0 + c;
+            float* x3 = xv[g];
             const bool upd = i > 0 && r < a.rows && p < 3;
             if (upd) {
                 const float gn = gacc / (float)a.rows;
                 const float ratio = a.ls_coef / gn;
                 const float ls = 2.0f * (ratio * ratio);
                 const float sq2ls = sqrtf(2.0f * ls);
-                float sv[3], mean[3];
+                float mean[3];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    sv[k] = sm.su[c * 9 + e0 + k];
-                    xv[k] = (xv[k] + ls * sv[k]) + sq2ls * sm.noise[c][0][e0 + k];
-                }
+                for (int k = 0; k < 3; ++k) x3[k] = (x3[k] + ls * sv[g][k]) + sq2ls * z1v[g][k];
                 if (p < 2) {   // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
-                    const float nn = sqrtf((xv[0] * xv[0] + xv[1] * xv[1]) + xv[2] * xv[2]);
-                    xv[0] /= nn; xv[1] /= nn; xv[2] /= nn;
+                    const float nn = sqrtf((x3[0] * x3[0] + x3[1] * x3[1]) + x3[2] * x3[2]);
+                    x3[0] /= nn; x3[1] /= nn; x3[2] /= nn;
                 }
                 // reverse-SDE Euler-Maruyama predictor (samplers.py:163-166; sign as in the reference)
                 const float g2 = prev.g * prev.g;
                 const float gs = prev.g * prev.sqrt_dt;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    const float drift = 0.0f - g2 * sv[k];
-                    mean[k] = xv[k] + drift * prev.dt;
-                    xv[k] = mean[k] + gs * sm.noise[c][1][e0 + k];
+                    const float drift = 0.0f - g2 * sv[g][k];
+                    mean[k] = x3[k] + drift * prev.dt;
+                    x3[k] = mean[k] + gs * z2v[g][k];
                 }
-                gram_schmidt6_quad(xv, p, lane);
-                const float* cen = a.center + (size_t)obj[c] * 3;
+                gram_schmidt6_quad(x3, p, lane);
+                const float* cen = a.center + (size_t)(r / a.kper) * 3;
                 if (a.xs) {
                     float* o = a.xs + ((size_t)r * a.steps + (i - 1)) * 9 + e0;
 #pragma unroll
-                    for (int k = 0; k < 3; ++k) o[k] = p == 2 ? xv[k] + cen[k] : xv[k];
+                    for (int k = 0; k < 3; ++k) o[k] = p == 2 ? x3[k] + cen[k] : x3[k];
                 }
                 if (i == a.steps) {  // res = mean_x of the last step (+centre, GS), samplers.py:174-177
                     if (p == 2) {
@@ -285,7 +269,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < 3; ++k) a.x[(size_t)r * 9 + e0 + k] = xv[k];
+                for (int k = 0; k < 3; ++k) a.x[(size_t)r * 9 + e0 + k] = x3[k];
             }
             if (i == a.steps) {
                 wave_sync();
@@ -303,7 +287,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             }
             if (p < 3) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) sm.xin[c * 16 + e0 + k] = (r < a.rows) ? xv[k] : 0.f;
+                for (int k = 0; k < 3; ++k) sm.xin[c * 16 + e0 + k] = (r < a.rows) ? x3[k] : 0.f;
             } else {
 #pragma unroll
                 for (int j = 9; j < 16; ++j) sm.xin[c * 16 + j] = 0.f;
@@ -331,23 +315,30 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     stage_small_weights<NT, WV, 64>(a.w, sm);
     head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
     PC_MARK(7);
-    // ---- s = f / (sigma + 1e-7); workgroup partial of sum_r ||s_r||
-    if (wid == 0) {
-        float nrm = 0.f;
-        const int r = r0 + lane;
-        if (lane < ROWS && r < a.rows) {
-            const float den = fadd(cur.sigma, 1e-7f);
-            float ss = 0.f;
-#pragma unroll
-            for (int j = 0; j < 9; ++j) {
-                const float v = fdiv(head_out(sm, lane, j), den);
-                a.s[(size_t)r * 9 + j] = v;
-                ss = fadd(ss, fmul(v, v));
+    // ---- s = f / (sigma + 1e-7); workgroup partial of sum_r ||s_r||. A lane per (row, output):
+    //      4 rows per wave as 16-lane rows (outputs 0..8 valid), row norms by a DPP row sum, the
+    //      waves' partials combined in wave order after one barrier
+    {
+        const float den = fadd(cur.sigma, 1e-7f);
+        float wsum = 0.f;
+        for (int cg = wid; cg < ROWS / 4; cg += WV) {
+            const int c = 4 * cg + (lane >> 4), o = lane & 15;
+            const int r = r0 + c;
+            float v = 0.f;
+            if (o < 9 && r < a.rows) {
+                v = fdiv(head_out(sm, c, o), den);
+                a.s[(size_t)r * 9 + o] = v;
             }
-            nrm = sqrtf(ss);
+            wsum += rows_sum(sqrtf(row16_sum(fmul(v, v))));
         }
-        nrm = wave_sum(nrm);
-        if (lane == 0) a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = nrm;
+        if (lane == 0) sm.scratch[wid] = wsum;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float t = 0.f;
+#pragma unroll
+        for (int v = 0; v < WV; ++v) t += sm.scratch[v];
+        a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = t;
     }
     PC_MARK(8);
 }
