@@ -149,20 +149,25 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
     }
 }
 
-// out[slot] = sqrt(sum(part[0..n))) / sqrt(count): scipy's RMS norm over the reduced partials in a
-// fixed order (one workgroup).
-__global__ __launch_bounds__(256) void ode_norm_kernel(const double* __restrict__ part, int n, double count,
-                                                       double* __restrict__ out) {
-    __shared__ double red[256];
+// Sum of part[0..n) by a 256-thread workgroup in a fixed order (strided per-thread sums, xor
+// shuffles within each wave, the four wave sums in wave order): every caller that reduces the same
+// partials gets the same bits. `red` is 4 doubles of LDS.
+__device__ __forceinline__ double block_sum_f64(const double* __restrict__ part, int n, double* red) {
     double t = 0.0;
     for (int i = threadIdx.x; i < n; i += 256) t += part[i];
-    red[threadIdx.x] = t;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) t += __shfl_xor(t, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
     __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out[0] = sqrt(red[0]) / sqrt(count);
+    return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// out[0] = sqrt(sum(part[0..n))) / sqrt(count): scipy's RMS norm over the error partials.
+__global__ __launch_bounds__(256) void ode_norm_kernel(const double* __restrict__ part, int n, double count,
+                                                       double* __restrict__ out) {
+    __shared__ double red[4];
+    const double t = block_sum_f64(part, n, red);
+    if (threadIdx.x == 0) out[0] = sqrt(t) / sqrt(count);
 }
 
 // select_initial_step norms (scipy _ivp/common.py): scale = atol + |y0| rtol;
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(1024) void ode_init_norms_kernel(const double* __re
                                                               const double* __restrict__ f1, long long n,
                                                               double atol, double rtol, double* __restrict__ out) {
 #pragma clang fp contract(off)
-    __shared__ double r0[1024], r1[1024];
+    __shared__ double r0[16], r1[16];
     double s0 = 0.0, s1 = 0.0;
     for (long long i = threadIdx.x; i < n; i += 1024) {
         const double sc = atol + fabs(y0[i]) * rtol;
@@ -185,15 +190,21 @@ __global__ __launch_bounds__(1024) void ode_init_norms_kernel(const double* __re
             s0 += v * v;
         }
     }
-    r0[threadIdx.x] = s0;
-    r1[threadIdx.x] = s1;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        s0 += __shfl_xor(s0, off, 64);
+        s1 += __shfl_xor(s1, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        r0[threadIdx.x >> 6] = s0;
+        r1[threadIdx.x >> 6] = s1;
+    }
     __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            r0[threadIdx.x] += r0[threadIdx.x + s];
-            r1[threadIdx.x] += r1[threadIdx.x + s];
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 16; ++i) {
+            r0[0] += r0[i];
+            r1[0] += r1[i];
         }
-        __syncthreads();
     }
     if (threadIdx.x == 0) {
         const double rn = sqrt((double)n);
@@ -307,14 +318,17 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_denoise_kernel(OdeDenoiseArg
     }
 }
 
-// Time rows of up to 6 stage times passed by value (no host->device copy per attempt).
+// Time rows of up to 6 stage times passed by value (no host->device copy per attempt); each row is
+// split over ODE_ROW_CHUNKS workgroups.
+#define ODE_ROW_CHUNKS 8
 struct OdeTimes {
     float t[6];
 };
 __global__ __launch_bounds__(HT) void ode_time_rows_kernel(gp_head_weights w, OdeTimes tv, float* __restrict__ out) {
     __shared__ float emb[128];
     __shared__ float tf[128];
-    time_row(w, tv.t[blockIdx.x], emb, tf, out + (size_t)blockIdx.x * 768);
+    constexpr int PER = 768 / ODE_ROW_CHUNKS;
+    time_row(w, tv.t[blockIdx.x], emb, tf, out + (size_t)blockIdx.x * 768, blockIdx.y * PER, blockIdx.y * PER + PER);
 }
 
 // ------------------------------------------------------------------------------ C ABI
@@ -328,7 +342,8 @@ extern "C" size_t gp_ode_workspace_size(int rows) {
 static int ode_launch_times(const gp_head_weights* w, const float* t32, int nt, void* ws, hipStream_t stream) {
     OdeTimes tv = {};
     for (int i = 0; i < nt; ++i) tv.t[i] = t32[i];
-    hipLaunchKernelGGL(ode_time_rows_kernel, dim3(nt), dim3(HT), 0, stream, *w, tv, static_cast<float*>(ws));
+    hipLaunchKernelGGL(ode_time_rows_kernel, dim3(nt, ODE_ROW_CHUNKS), dim3(HT), 0, stream, *w, tv,
+                       static_cast<float*>(ws));
     return gp_check_launch("ode_time_rows_kernel");
 }
 
@@ -485,31 +500,23 @@ struct OdeConsts {
     int nwg;                            // error partials
 };
 
-#define ODE_CTL_CHUNKS 4   // workgroups per stage time row (768 / 4 outputs each)
+#define ODE_CTL_CHUNKS 8   // workgroups per stage time row (768 / 8 outputs each)
 
 __global__ __launch_bounds__(HT) void ode_control_kernel(gp_head_weights w, const OdeCtl* __restrict__ cin,
                                                          OdeCtl* __restrict__ cout, const double* __restrict__ part,
                                                          int decide, OdeConsts k, float* __restrict__ tproj6) {
 #pragma clang fp contract(off)
-    __shared__ double red[HT];
+    __shared__ double red[4];
     __shared__ OdeCtl s;
     __shared__ float emb[128], tf[128];
     const int tid = threadIdx.x;
-    // error norm of attempt n-1 (same fixed order in every workgroup)
-    double v = 0.0;
-    if (decide)
-        for (int i = tid; i < k.nwg; i += HT) v += part[i];
-    red[tid] = v;
-    __syncthreads();
-    for (int st = HT / 2; st > 0; st >>= 1) {
-        if (tid < st) red[tid] += red[tid + st];
-        __syncthreads();
-    }
+    // error norm of attempt n-1 (the same fixed order in every workgroup)
+    const double esum = decide ? block_sum_f64(part, k.nwg, red) : 0.0;
     if (tid == 0) {
         OdeCtl c = *cin;
         const double dir = k.direction;
         if (decide && c.active) {   // scipy RK45._step_impl, after rk_step / _estimate_error_norm
-            const double err = sqrt(red[0]) / sqrt(k.count);
+            const double err = sqrt(esum) / sqrt(k.count);
             c.nfev += 6;
             if (err < 1.0) {
                 double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * pow(err, -0.2));
@@ -545,23 +552,28 @@ __global__ __launch_bounds__(HT) void ode_control_kernel(gp_head_weights w, cons
                 c.t_new = t_new;
                 c.h_abs_loc = fabs(h);
                 c.active = 1;
-                const double cs[6] = {1.0 / 5.0, 3.0 / 10.0, 4.0 / 5.0, 8.0 / 9.0, 1.0, 0.0};
-                for (int st = 0; st < 6; ++st) {
-                    const double ts = st < 5 ? c.t + cs[st] * h : c.t + h;
-                    const float t32 = (float)ts;
-                    c.t32[st] = t32;
-                    c.sig[st] = fmul((float)k.sig_min, (float)pow(k.base, (double)t32));
-                    const double g = (k.sig_min * pow(k.base, ts)) * k.diff_scale;
-                    c.coef[st] = -(0.5 * (g * g));
-                }
             }
         }
         s = c;
-        if (blockIdx.x == 0 && blockIdx.y == 0) *cout = c;
     }
     __syncthreads();
-    if (!s.active) return;
-    // time row slice of stage blockIdx.x: outputs [chunk * 192, chunk * 192 + 192)
+    if (!s.active) {
+        if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) *cout = s;
+        return;
+    }
+    // stage times t + c_s h (s = 1..5) and t + h, one thread each (rk.py rk_step)
+    if (tid < 6) {
+        const double cs[5] = {1.0 / 5.0, 3.0 / 10.0, 4.0 / 5.0, 8.0 / 9.0, 1.0};
+        const double ts = tid < 5 ? s.t + cs[tid] * s.h : s.t + s.h;
+        const float t32 = (float)ts;
+        s.t32[tid] = t32;
+        s.sig[tid] = fmul((float)k.sig_min, (float)pow(k.base, (double)t32));
+        const double g = (k.sig_min * pow(k.base, ts)) * k.diff_scale;
+        s.coef[tid] = -(0.5 * (g * g));
+    }
+    __syncthreads();
+    if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) *cout = s;
+    // time row slice of stage blockIdx.x: outputs [chunk * 96, chunk * 96 + 96)
     constexpr int PER = 768 / ODE_CTL_CHUNKS;
     time_row(w, s.t32[blockIdx.x], emb, tf, tproj6 + (size_t)blockIdx.x * 768, blockIdx.y * PER, blockIdx.y * PER + PER);
 }
