@@ -24,7 +24,8 @@ class GenPoseHipError(RuntimeError):
 
 class HeadWeights(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("pe0_w", "pe0_b", "pe2_w", "pe2_b", "h1p_w", "h2_w", "h2_b",
-                                       "h1pts_t", "h1_b", "gfp_w", "te_w_t", "te_b", "h1t_t")]
+                                       "h1pts_t", "h1_b", "gfp_w", "te_w_t", "te_b", "h1t_t", "pe2_h", "h1p_h",
+                                       "hsc")]
 
 
 class ScaleWeights(ctypes.Structure):

@@ -244,6 +244,233 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
     PC_MARK(6);
 }
 
+// ============================================================================ split-f16 trunk
+// The two per-candidate GEMMs (pose_encoder.2 and head layer 1's pose block) on
+// v_mfma_f32_16x16x32_f16. Both operands are scaled by exact powers of two and split x = hi + lo with
+// hi = f16(x), lo = f16(x - hi), so each keeps ~22 significant bits. Per 32-deep chunk, three MFMAs
+// (w_lo*a_hi, w_hi*a_lo, w_hi*a_hi) accumulate in fp32; the dropped w_lo*a_lo term is ~2^-22
+// relative. Weights: per-layer exponents and packed hi/lo planes from pack.py (4 B per weight, the
+// same bytes as fp32). Activations: a per-candidate exponent from a rigorous bound on the layer's
+// outputs (max|pose| times the layer's max row L1 norm plus max|bias|, chained), so no extra
+// barrier is needed and f16 cannot overflow. scripts/precision_study2.py (STUDY_F16=1): through
+// the sampler this is as close to the golden trajectories as fp32 (rotation 1.51e-5 vs 1.56e-5).
+#ifndef PC_D2H
+#define PC_D2H 2                 // 32-deep chunks of pose_encoder.2 weights kept in flight
+#endif
+#ifndef HEAD_PREFETCH_H
+#define HEAD_PREFETCH_H 2        // 32-deep chunks of head-layer-1 weights kept in flight
+#endif
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int KC_HID = HID / 32;   // 32-deep chunks over a 256-wide activation
+
+__device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// 2^e (e clamped to the normal range) and floor(log2(v)) of a normal v > 0, both exact
+__device__ __forceinline__ float exp2i(int e) {
+    e = e < -126 ? -126 : (e > 127 ? 127 : e);
+    return __uint_as_float((uint32_t)(e + 127) << 23);
+}
+__device__ __forceinline__ int ilog2f(float v) { return (int)((__float_as_uint(v) >> 23) & 0xff) - 127; }
+// max over lanes l, l^16, l^32, l^48
+__device__ __forceinline__ float rows_max(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// hi/lo planes of the 32-deep chunk made of two accumulator tiles (u: tile 2c, v: tile 2c+1), times
+// s. Lane (q, n) holds k = 4q + j (j < 4) from u and 16 + 4q + j - 4 from v: the k order pack.py's
+// pack_h16_fragments gives the weights.
+__device__ __forceinline__ void split_pair(f32x4 u, f32x4 v, float s, f16x8& hi, f16x8& lo) {
+#pragma clang fp contract(off)
+    const float x[8] = {u.x * s, u.y * s, u.z * s, u.w * s, v.x * s, v.y * s, v.z * s, v.w * s};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const _Float16 h = (_Float16)x[j];
+        hi[j] = h;
+        lo[j] = (_Float16)(x[j] - (float)h);
+    }
+}
+
+// stream_step on f16 planes: ring slot = [tile][hi, lo] of one 32-deep chunk (2 x 1 KiB per tile);
+// B = activation planes in LDS, [chunk][ct][hi, lo][lane].
+template <int G, int GEND, int TT, int NT, int D>
+__device__ __forceinline__ void stream_h_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
+                                              int lane, int voff, f16x8 (&ring)[D + 1][TT][2], f32x4 (&acc)[TT][NT]) {
+    if constexpr (G < GEND) {
+        if constexpr (G < KC_HID) {
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+                    ring[G % (D + 1)][t][p] =
+                        __builtin_bit_cast(f16x8, ldbuf4(W, voff, ((T[t] * KC_HID + G) * 2 + p) * 1024));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (G >= D) {
+            constexpr int GG = G - D, S = GG % (D + 1);
+            f16x8 bh[NT], bl[NT];
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) {
+                bh[ct] = B[((GG * NT + ct) * 2 + 0) * 64 + lane];
+                bl[ct] = B[((GG * NT + ct) * 2 + 1) * 64 + lane];
+            }
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int ct = 0; ct < NT; ++ct) acc[t][ct] = mfma_h(ring[S][t][1], bh[ct], acc[t][ct]);
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int ct = 0; ct < NT; ++ct) acc[t][ct] = mfma_h(ring[S][t][0], bl[ct], acc[t][ct]);
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int ct = 0; ct < NT; ++ct) acc[t][ct] = mfma_h(ring[S][t][0], bh[ct], acc[t][ct]);
+        }
+        stream_h_step<G + 1, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc);
+    }
+}
+
+// head_trunk with the split-f16 GEMMs (same contract and phases; pose_encoder.0 and layer 2 stay fp32).
+template <int NT, int WV>
+__device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const float* __restrict__ pobj,
+                                                 const float* __restrict__ tproj, const int* obj_of_col,
+                                                 HeadSmem<NT, WV>& sm, int trace_slot = 0) {
+    constexpr int TPW = 16 / WV;   // output tiles per wave; tiles (2c, 2c+1) form 32-deep chunk c
+    static_assert(TPW % 2 == 0, "split trunk pairs a wave's output tiles into 32-deep chunks");
+    constexpr int CPW = TPW / 2;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane >> 4, n = lane & 15;
+    const int voff = lane * 16;
+    const __amdgpu_buffer_rsrc_t W2 = make_rsrc(w.pe2_h, HID * HID * 4);
+    const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_h, 3 * HID * HID * 4);
+    f16x8* act1h = reinterpret_cast<f16x8*>(sm.act1);   // same 16 KiB per column tile as fp32
+    f16x8* act2h = reinterpret_cast<f16x8*>(sm.act2);
+    constexpr int D2 = PC_D2H, DH = HEAD_PREFETCH_H;
+    int T2[TPW], TH[3 * TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) T2[t] = wid * TPW + t;
+#pragma unroll
+    for (int h = 0; h < 3; ++h)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) TH[h * TPW + t] = h * 16 + wid * TPW + t;
+    f32x4 acc2[TPW][NT];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) acc2[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f16x8 ring2[D2 + 1][TPW][2];
+    stream_h_step<0, D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
+    __syncthreads();
+    PC_MARK(1);
+    // ---- per-candidate exponents: bound1 >= |pose_encoder.0 out|, bound2 >= |pose_encoder.2 out|
+    const float A0 = w.hsc[0], B0 = w.hsc[1], A2 = w.hsc[2], B2 = w.hsc[3];
+    const int ew2 = (int)w.hsc[4], ewh = (int)w.hsc[5];
+    f32x4 bf[NT];
+    float s1[NT], s2[NT], u2[NT], uh[NT], sh[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+        bf[ct] = ld4(&sm.xin[(ct * 16 + n) * 16 + 4 * q]);
+        const float m0 = rows_max(fmaxf(fmaxf(fabsf(bf[ct].x), fabsf(bf[ct].y)), fmaxf(fabsf(bf[ct].z), fabsf(bf[ct].w))));
+        const float b1 = fmaxf((A0 * m0 + B0) * 1.0009765625f, 1e-18f);
+        const float b2 = fmaxf((A2 * b1 + B2) * 1.0009765625f, 1e-18f);
+        const int e1 = ilog2f(b1), e2 = ilog2f(b2);
+        s1[ct] = exp2i(14 - e1);         // activations scaled into [2^14, 2^15) at their bound
+        s2[ct] = exp2i(14 - e2);
+        u2[ct] = exp2i(e1 - 14 - ew2);   // undo both scales of pose_encoder.2
+        uh[ct] = exp2i(e2 - 14 - ewh);   // undo both scales of head layer 1
+        sh[ct] = exp2i(14 - e2 + ewh);   // head layer 1's fp32 init (pts + t blocks) in the scaled domain
+    }
+    // ---- pose_encoder.0 (9 -> 256) in fp32, one k-group; ReLU, scale, split into the chunk planes
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        const int Ta = wid * TPW + 2 * c;
+        const f32x4 a0 = sm.pe0w[Ta * 64 + lane], a1 = sm.pe0w[(Ta + 1) * 64 + lane];
+        const f32x4 bias0 = ld4(&sm.pe0b[16 * Ta + 4 * q]), bias1 = ld4(&sm.pe0b[16 * (Ta + 1) + 4 * q]);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+            const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+            f16x8 hi, lo;
+            split_pair(relu4(mfma_kgroup(a0, bf[ct], z) + bias0), relu4(mfma_kgroup(a1, bf[ct], z) + bias1), s1[ct],
+                       hi, lo);
+            act1h[(((Ta >> 1) * NT + ct) * 2 + 0) * 64 + lane] = hi;
+            act1h[(((Ta >> 1) * NT + ct) * 2 + 1) * 64 + lane] = lo;
+        }
+    }
+    __syncthreads();
+    PC_MARK(2);
+    // ---- pose_encoder.2 (256 -> 256)
+    constexpr int PE2_TAIL = 2;
+    stream_h_step<D2, KC_HID + D2 - PE2_TAIL, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
+    f32x4 tpv[3 * TPW], pov[3 * TPW][NT];
+#pragma unroll
+    for (int i = 0; i < 3 * TPW; ++i) {
+        const int T = TH[i];
+        tpv[i] = ld4(tproj + 16 * T + 4 * q);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q);
+    }
+    stream_h_step<KC_HID + D2 - PE2_TAIL, KC_HID + D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
+    PC_MARK(3);
+    f32x4 acc[3 * TPW][NT];
+#pragma unroll
+    for (int i = 0; i < 3 * TPW; ++i)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) acc[i][ct] = (pov[i][ct] + tpv[i]) * sh[ct];
+    f16x8 ringh[DH + 1][3 * TPW][2];
+    stream_h_step<0, DH, 3 * TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc);
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        const int Ta = T2[2 * c];
+        const f32x4 bias0 = ld4(&sm.pe2b[16 * Ta + 4 * q]), bias1 = ld4(&sm.pe2b[16 * (Ta + 1) + 4 * q]);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+            f16x8 hi, lo;
+            split_pair(relu4(acc2[2 * c][ct] * u2[ct] + bias0), relu4(acc2[2 * c + 1][ct] * u2[ct] + bias1), s2[ct], hi,
+                       lo);
+            act2h[(((Ta >> 1) * NT + ct) * 2 + 0) * 64 + lane] = hi;
+            act2h[(((Ta >> 1) * NT + ct) * 2 + 1) * 64 + lane] = lo;
+        }
+    }
+    __syncthreads();
+    PC_MARK(4);
+    // ---- head layer 1 (pose block 256 -> 3x256)
+    stream_h_step<DH, KC_HID + DH, 3 * TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc);
+    PC_MARK(5);
+    // ---- ReLU -> head layer 2 partial dot products (fp32, as head_trunk)
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+            float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                const f32x4 u = relu4(acc[h * TPW + t][ct] * uh[ct]);
+                const int ch = 16 * (wid * TPW + t) + 4 * q;
+                const f32x4 w0 = ld4(&sm.h2w[(h * 3 + 0) * HID + ch]);
+                const f32x4 w1 = ld4(&sm.h2w[(h * 3 + 1) * HID + ch]);
+                const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
+                p0 += u.x * w0.x + u.y * w0.y + u.z * w0.z + u.w * w0.w;
+                p1 += u.x * w1.x + u.y * w1.y + u.z * w1.z + u.w * w1.w;
+                p2 += u.x * w2.x + u.y * w2.y + u.z * w2.z + u.w * w2.w;
+            }
+            p0 = rows_sum(p0);
+            p1 = rows_sum(p1);
+            p2 = rows_sum(p2);
+            if (q == 0) {
+                sm.red[ct * 16 + n][h * 3 + 0][wid] = p0;
+                sm.red[ct * 16 + n][h * 3 + 1][wid] = p1;
+                sm.red[ct * 16 + n][h * 3 + 2][wid] = p2;
+            }
+        }
+    }
+    __syncthreads();
+    PC_MARK(6);
+}
+
 // ============================================================================ pose helpers
 template <typename T>
 __device__ __forceinline__ T tsqrt(T v);

@@ -162,7 +162,7 @@ struct PCArgs {
 // Wave 0 runs the update (its global loads, the draws and the grad-norm reduction overlap) while
 // the other waves stage the small weights and issue their first weight-stream loads; one barrier
 // (inside head_trunk) joins them.
-template <int NT, int WV>
+template <int NT, int WV, bool SPLIT>
 __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
     constexpr int ROWS = NT * 16;
     __shared__ HeadSmem<NT, WV> sm;
@@ -313,7 +313,10 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
         }
     }
     stage_small_weights<NT, WV, 64>(a.w, sm);
-    head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
+    if constexpr (SPLIT)
+        head_trunk_split<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
+    else
+        head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
     PC_MARK(7);
     // ---- s = f / (sigma + 1e-7); workgroup partial of sum_r ||s_r||. A lane per (row, output):
     //      4 rows per wave as 16-lane rows (outputs 0..8 valid), row norms by a DPP row sum, the
@@ -390,6 +393,9 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     GP_REQUIRE((z1 == nullptr) == (z2 == nullptr), "pc_sample: z1/z2 must both be given or both null");
     GP_REQUIRE(workspace_bytes >= gp_pc_workspace_size(rows), "pc_sample: workspace too small");
     const int nt = pc_pick_nt(rows);
+    // split-f16 GEMMs when the packed planes are given (gp_head_weights), exact fp32 otherwise
+    const bool split = w->pe2_h != nullptr;
+    GP_REQUIRE(!split || (w->h1p_h && w->hsc), "pc_sample: pe2_h, h1p_h and hsc must be given together");
     PCArgs a;
     a.w = *w;
     a.pobj = pobj;
@@ -418,9 +424,11 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
         if (i > 0) prev = PCStep{step_tab[5 * (i - 1)], step_tab[5 * (i - 1) + 1], step_tab[5 * (i - 1) + 2],
                                  step_tab[5 * (i - 1) + 3], step_tab[5 * (i - 1) + 4]};
         if (nt == 2)
-            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV2>), grid, dim3(PC_WV2 * 64), 0, stream, a, i, cur, prev);
+            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV2, false>), grid, dim3(PC_WV2 * 64), 0, stream, a, i, cur, prev);
+        else if (split)
+            hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, true>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else
-            hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+            hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, false>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
     }
     return gp_check_launch("pc_step_kernel");
 }

@@ -6,6 +6,7 @@ computation on the path is a call into the HIP library.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -98,8 +99,20 @@ class HeadModel:
         self.lib = _lib.load()
         self.device = device
         self.up = _Uploaded(pack.pack_heads(sd), device)
-        self.w = _lib.HeadWeights(**{k: self.up.ptr(k) for k in pack.HEAD_FIELDS})
+        self.set_arith(os.environ.get("GENPOSE2_HEAD_ARITH", "split_f16"))
         self._pc_ws: Optional[torch.Tensor] = None
+
+    def set_arith(self, arith: str) -> None:
+        """PC sampler GEMM arithmetic: "split_f16" (pose_encoder.2 and head layer 1's pose block as
+        f16 hi/lo MFMA products, gp_head.h) or "f32" (exact fp32 MFMA). Evaluation and ODE kernels
+        are fp32 either way."""
+        if arith not in ("split_f16", "f32"):
+            raise ValueError(f"unknown head arithmetic {arith!r} (split_f16 | f32)")
+        ptrs = {k: self.up.ptr(k) for k in pack.HEAD_FIELDS}
+        if arith == "f32":
+            ptrs.update(pe2_h=None, h1p_h=None, hsc=None)
+        self.arith = arith
+        self.w = _lib.HeadWeights(**ptrs)
 
     def _s(self):
         return ctypes.c_void_p(stream_handle(self.device))

@@ -88,7 +88,45 @@ def pack_encoder(sd: weights.StateDict) -> Tuple[np.ndarray, np.ndarray]:
 
 # ---------------------------------------------------------------- score / energy heads
 HEAD_FIELDS = ("pe0_w", "pe0_b", "pe2_w", "pe2_b", "h1p_w", "h2_w", "h2_b", "h1pts_t", "h1_b",
-               "gfp_w", "te_w_t", "te_b", "h1t_t")
+               "gfp_w", "te_w_t", "te_b", "h1t_t", "pe2_h", "h1p_h", "hsc")
+
+
+def split_exponent(w: np.ndarray) -> int:
+    """e with max|w| * 2**e in [2**14, 2**15): the f16 planes of w * 2**e keep 11 bits and cannot overflow."""
+    m = float(np.abs(w).max())
+    return 14 - int(np.floor(np.log2(m))) if m > 0 else 0
+
+
+def pack_h16_fragments(w: np.ndarray, e: int) -> np.ndarray:
+    """(n_out, k_in) -> bits (int32 words) of the f16 hi/lo planes of w * 2**e (hi = f16(x), lo = f16(x - hi)) in
+    the A-operand order of v_mfma_f32_16x16x32_f16 used by gp_head.h's split trunk:
+
+        packed[T][c][plane][lane][j] = plane(W[16T + (lane & 15)][32c + 16*(j // 4) + 4*(lane >> 4) + j % 4])
+
+    i.e. chunk c pairs the fp32 accumulator tiles 2c and 2c+1 of the producing layer, so its output
+    feeds the B operand without moving data between lanes. One (T, c, plane) is 1 KiB."""
+    n_out, k_in = w.shape
+    assert n_out % 16 == 0 and k_in % 32 == 0, (n_out, k_in)
+    x = (np.asarray(w, np.float32) * np.float32(2.0 ** e)).astype(np.float32)
+    hi = x.astype(np.float16)
+    lo = (x - hi.astype(np.float32)).astype(np.float16)
+    NT, KC = n_out // 16, k_in // 32
+
+    def frag(p):   # [T][i][c][half][q][j4] -> [T][c][q][i][half][j4]: lane = 16q + i, j = 4*half + j4
+        return p.reshape(NT, 16, KC, 2, 4, 4).transpose(0, 2, 4, 1, 3, 5)
+    out = np.stack([frag(hi), frag(lo)], axis=2)
+    # int32 words (two f16 each): every torch.distributed backend broadcasts int32
+    return np.ascontiguousarray(out).reshape(-1).view(np.int32)
+
+
+def split_constants(p: Dict[str, np.ndarray], e2: int, eh: int) -> np.ndarray:
+    """hsc: bounds the split trunk derives its per-candidate activation exponents from
+    (|pose_encoder.0 out| <= A0*max|x| + B0, |pose_encoder.2 out| <= A2*bound0 + B2) + weight exponents."""
+    a0 = np.abs(p["pe0_w"].astype(np.float64)).sum(1).max()
+    a2 = np.abs(p["pe2_w"].astype(np.float64)).sum(1).max()
+    b0, b2 = np.abs(p["pe0_b"]).max(), np.abs(p["pe2_b"]).max()
+    # rounded up so that the fp32 values stay bounds
+    return np.nextafter(np.array([a0, b0, a2, b2], np.float32), np.float32(np.inf)).tolist() + [e2, eh, 0, 0]
 
 
 def pack_heads(sd: weights.StateDict) -> Dict[str, np.ndarray]:
@@ -109,7 +147,13 @@ def pack_heads(sd: weights.StateDict) -> Dict[str, np.ndarray]:
         "te_b": p["te_b"],
         "h1t_t": np.ascontiguousarray(p["h1_t"].reshape(3 * H, arch.T_EMB).T),
     }
-    return {k: np.ascontiguousarray(v, np.float32) for k, v in out.items()}
+    out = {k: np.ascontiguousarray(v, np.float32) for k, v in out.items()}
+    h1_pose = p["h1_pose"].reshape(3 * H, arch.POSE_HID)
+    e2, eh = split_exponent(p["pe2_w"]), split_exponent(h1_pose)
+    out["pe2_h"] = pack_h16_fragments(p["pe2_w"], e2)
+    out["h1p_h"] = pack_h16_fragments(h1_pose, eh)
+    out["hsc"] = np.asarray(split_constants(p, e2, eh), np.float32)
+    return out
 
 
 SCALE_FIELDS = ("ae0_w", "ae0_b", "ae2_w", "ae2_b", "ft0_w", "ft0_b", "ft2_w", "ft2_b")

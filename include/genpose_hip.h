@@ -30,7 +30,7 @@ enum { GP_OK = 0, GP_ERR_INVALID = -1, GP_ERR_LAUNCH = -2, GP_ERR_UNSUPPORTED = 
 const char *gp_last_error(void);
 /* ABI version of this header. */
 int gp_abi_version(void);
-#define GP_ABI_VERSION 2
+#define GP_ABI_VERSION 3
 
 /* ===================================================================== operator level
  * Drop-in forward ops of `pointnet2_cuda` (same argument meaning and layouts). */
@@ -89,6 +89,13 @@ typedef struct {
     const float *te_w_t;  /* t_encoder.1.weight transposed (128,128) */
     const float *te_b;    /* (128) */
     const float *h1t_t;   /* head layer 1, t columns, transposed (128, 768) */
+    /* Split-f16 form of pe2_w / h1p_w for the PC sampler (pack.py pack_h16_fragments): f16 hi/lo
+     * planes of W * 2^e. hsc = {A0, B0, A2, B2, e_pe2, e_h1p, 0, 0}: max row L1 norm and max |bias|
+     * of pose_encoder.0 / .2 (activation bounds) and the two weight exponents. All three NULL:
+     * gp_pc_sample computes those GEMMs in exact fp32 instead. */
+    const void *pe2_h;
+    const void *h1p_h;
+    const float *hsc;
 } gp_head_weights;
 
 /* Per-object projection P[b] = W1_pts . pts_feat[b] + b1 -> pobj (b,768). */

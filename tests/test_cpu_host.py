@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     from genpose2_amd import _lib
     assert set(_lib.EXPORTED) == declared   # the ctypes binding covers exactly the header
     lib = _lib.load()
-    assert lib.gp_abi_version() == 2
+    assert lib.gp_abi_version() == 3
     assert lib.gp_encoder_workspace_size(64, 1024) > 0 and lib.gp_pc_workspace_size(3200) >= 3200 * 36
 
 
@@ -48,6 +48,35 @@ def test_a_fragment_packing_layout():
     off = ((T * 3 + g) * 64 + lane) * 4
     assert np.array_equal(p[off:off + 4], np.pad(w, ((0, 8), (0, 13)))[16 * T + lane % 16, 16 * g + 4 * (lane // 16):][:4])
     np.testing.assert_array_equal(pack.unpack_a_fragments(p, 48, 48)[:40, :35], w)
+
+
+def test_split_f16_packing_layout_and_bounds(score_sd):
+    from genpose2_amd import pack, weights
+    rng = np.random.default_rng(1)
+    w = (rng.normal(size=(32, 64)) * 0.05).astype(np.float32)
+    e = pack.split_exponent(w)
+    assert 2.0 ** 14 <= np.abs(w).max() * 2.0 ** e < 2.0 ** 15
+    p = pack.pack_h16_fragments(w, e).view(np.float16).astype(np.float32)
+    assert p.size == 2 * w.size
+    # lane l of (tile T, chunk c, plane) holds W[16T + l%16][32c + 16(j//4) + 4(l//16) + j%4], j < 8
+    T, c, lane = 1, 1, 37
+    x = w.astype(np.float32) * np.float32(2.0 ** e)
+    for j in range(8):
+        k = 32 * c + 16 * (j // 4) + 4 * (lane // 16) + j % 4
+        hi = p[(((T * 2 + c) * 2 + 0) * 64 + lane) * 8 + j]
+        lo = p[(((T * 2 + c) * 2 + 1) * 64 + lane) * 8 + j]
+        assert hi == np.float16(x[16 * T + lane % 16, k])
+        assert abs((hi + lo) - x[16 * T + lane % 16, k]) <= 2.0 ** -21 * abs(x[16 * T + lane % 16, k])
+    # hsc bounds the layer outputs for any pose input
+    heads = pack.pack_heads(score_sd)
+    p = weights.head_params(score_sd)
+    A0, B0, A2, B2, e2, eh = heads["hsc"][:6]
+    xs = rng.normal(size=(256, 9)).astype(np.float32) * 3
+    a1 = np.maximum(xs @ p["pe0_w"].T + p["pe0_b"], 0)
+    a2 = np.maximum(a1 @ p["pe2_w"].T + p["pe2_b"], 0)
+    b1 = A0 * np.abs(xs).max(1) + B0
+    assert (a1.max(1) <= b1).all() and (a2.max(1) <= A2 * b1 + B2).all()
+    assert e2 == pack.split_exponent(p["pe2_w"]) and heads["pe2_h"].dtype == np.int32
 
 
 def test_encoder_packing_covers_every_layer(score_sd):

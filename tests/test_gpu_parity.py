@@ -177,6 +177,25 @@ def test_pc_full_size_properties():
     assert not torch.equal(p1, p3)
 
 
+def test_pc_split_f16_matches_exact_f32():
+    """The split-f16 GEMMs (default) against the exact fp32 MFMA path on identical inputs and noise,
+    at the PC golden tests' tolerances (1e-4 rotation, 1e-5 relative translation)."""
+    from genpose2_amd import synthetic
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    pts, center = synthetic.make_batch(5, 16, 1024)
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
+    out = {}
+    for arith in ("split_f16", "f32"):
+        a = PoseNet(GenPoseConfig(device=DEV, sampling_steps=100, noise_seed=7)).eval()
+        a.heads.set_arith(arith)
+        out[arith] = a.pred_func(dict(data), repeat_num=50)[0].cpu().numpy()
+    p, ref = out["split_f16"], out["f32"]
+    assert np.abs(p[..., :6] - ref[..., :6]).max() < 1e-4
+    assert rel(p[..., 6:], ref[..., 6:]) < 1e-5
+    assert not np.array_equal(p, ref)   # the two paths really differ in arithmetic
+
+
 # ---------------------------------------------------------------- ODE sampler
 @pytest.mark.parametrize("tag,rot_tol,tr_rel", [("t055_s20", 1e-4, 1e-5), ("t1_none", 5e-4, 1e-4)])
 def test_ode_pred_func_vs_golden(tag, rot_tol, tr_rel):
