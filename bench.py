@@ -31,6 +31,7 @@ CONFIGS = {
     5: dict(B=256, N=2048, K=100, T=1000, energy=False, scale=True),
 }
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (and vector) peak
+F16_PEAK_TFLOPS = 2516.6   # dense BF16/F16 MFMA: 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz
 
 
 def dist_env():
@@ -242,6 +243,14 @@ def main():
     per_launch_s = samp_ms / 1e3 / (T + 1)
     flop_launch = B * K * arch.score_flops_per_candidate_step()
     achieved = flop_launch / per_launch_s / 1e12
+    split = score.heads.arith == "split_f16"
+    # split-f16: the two per-candidate GEMMs run 3 f16 MFMA products per fp32 MAC, so their MFMA
+    # ceiling in algorithmic (fp32) FLOP/s is the dense f16 peak / 3
+    peak = F16_PEAK_TFLOPS / 3 if split else FP32_PEAK_TFLOPS
+    up = score.heads.up.t
+    wg_bytes = sum(up[k].numel() * up[k].element_size() for k in
+                   (("pe2_h", "h1p_h") if split else ("pe2_w", "h1p_w")))   # streamed per workgroup per step
+    nwg = -(-B * K // 16)
     if rank == 0:
         out = {
             "metric": "pose candidates/sec (B objs x K cands x T denoise steps)",
@@ -254,16 +263,21 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32 (pose_encoder.2 / head-1 GEMMs: split-f16 MFMA, fp32 accumulate)" if split else "f32",
             "data": "synthetic (seeded point clouds, seeded synthetic weights; no checkpoint exists for dino=none)",
             "config": {"workload": f"config{args.config}: B={B} objects/GPU, N={N} pts, K={K} candidates, T={T} PC "
                                    f"steps, {'ScoreNet+EnergyNet+ranking/aggregation' if cfgd['energy'] else 'ScoreNet'}"
                                    f"{' + ScaleNet' if cfgd['scale'] else ''} (encoder + sampler per step)",
                        "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": load_traffic(B * K),
-                         "kernel": "pc_step_kernel", "flop_per_launch": flop_launch,
-                         "avg_launch_us": per_launch_s * 1e6, "sampler_ms_per_step": samp_ms},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": load_traffic(B * K),
+                         "kernel": "pc_step_kernel", "arith": score.heads.arith, "flop_per_launch": flop_launch,
+                         "avg_launch_us": per_launch_s * 1e6, "sampler_ms_per_step": samp_ms,
+                         "fp32_mfma_equiv_frac": achieved / FP32_PEAK_TFLOPS,
+                         # what binds the split kernel: every workgroup streams the GEMM weights from L2
+                         "l2_weight_stream": {"bytes_per_workgroup": wg_bytes, "workgroups": nwg,
+                                              "GBps_per_CU": wg_bytes / per_launch_s / 1e9,
+                                              "TBps_chip": wg_bytes * nwg / per_launch_s / 1e12}},
         }
         if not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
