@@ -58,7 +58,7 @@ struct OdeStageArgs {
 };
 
 // MODE 0: stage derivative. MODE 1: last stage of an attempt (y_new, K_6, error partials).
-template <int MODE>
+template <int MODE, bool SPLIT>
 __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a) {
     __shared__ HeadSmem<1, EVAL_WV> sm;
     __shared__ int obj[16];
@@ -115,7 +115,10 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         const int r = r0 + tid;
         obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
     }
-    head_trunk<1, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
+    if constexpr (SPLIT)
+        head_trunk_split<1, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
+    else
+        head_trunk<1, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
     if (tid < 144) {
 #pragma clang fp contract(off)
         const int c = tid / 9, o = tid - c * 9;
@@ -372,7 +375,10 @@ extern "C" int gp_ode_rhs(const gp_head_weights* w, const float* pobj, float t32
     a.kper = k;
     int rc = ode_launch_times(w, &t32, 1, workspace, stream);
     if (rc) return rc;
-    hipLaunchKernelGGL(ode_stage_kernel<0>, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
+    if (a.w.pe2_h)
+        hipLaunchKernelGGL((ode_stage_kernel<0, true>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
+    else
+        hipLaunchKernelGGL((ode_stage_kernel<0, false>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
     return gp_check_launch("ode_stage_kernel");
 }
 
@@ -409,7 +415,10 @@ extern "C" int gp_ode_attempt(const gp_head_weights* w, const float* pobj, const
         a.nk = s;
         for (int j = 0; j < s; ++j) a.a[j] = tableau_a[s * 6 + j];
         a.kout = kslots[s];
-        hipLaunchKernelGGL(ode_stage_kernel<0>, dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+        if (a.w.pe2_h)
+            hipLaunchKernelGGL((ode_stage_kernel<0, true>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+        else
+            hipLaunchKernelGGL((ode_stage_kernel<0, false>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
     }
     // y_new = y + (sum_{j<6} B_j K_j) h ; K_6 = f(t + h, y_new) ; error partials
     a.tproj = tproj + (size_t)5 * 768;
@@ -421,7 +430,10 @@ extern "C" int gp_ode_attempt(const gp_head_weights* w, const float* pobj, const
     a.kout = kslots[6];
     a.ynew = ynew;
     a.part = part;
-    hipLaunchKernelGGL(ode_stage_kernel<1>, dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    if (a.w.pe2_h)
+        hipLaunchKernelGGL((ode_stage_kernel<1, true>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    else
+        hipLaunchKernelGGL((ode_stage_kernel<1, false>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
     hipLaunchKernelGGL(ode_norm_kernel, dim3(1), dim3(256), 0, stream, (const double*)part, nwg,
                        (double)rows * 9.0, err_out);
     return gp_check_launch("ode_stage_kernel<final>");
@@ -629,13 +641,19 @@ extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, 
         a.stage = s;
         a.nk = s;
         for (int j = 0; j < s; ++j) a.a[j] = tableau_a[s * 6 + j];
-        hipLaunchKernelGGL(ode_stage_kernel<0>, dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+        if (a.w.pe2_h)
+            hipLaunchKernelGGL((ode_stage_kernel<0, true>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+        else
+            hipLaunchKernelGGL((ode_stage_kernel<0, false>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
     }
     a.stage = 6;
     a.nk = 6;
     for (int j = 0; j < 6; ++j) a.a[j] = b[j];
     for (int j = 0; j < ODE_NK; ++j) a.e[j] = e[j];
     a.part = part;
-    hipLaunchKernelGGL(ode_stage_kernel<1>, dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    if (a.w.pe2_h)
+        hipLaunchKernelGGL((ode_stage_kernel<1, true>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    else
+        hipLaunchKernelGGL((ode_stage_kernel<1, false>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
     return gp_check_launch("ode_stage_kernel<auto>");
 }

@@ -9,10 +9,11 @@
 // GEMM as the accumulator's initial value. Per candidate-step only pose 9->256->256 -> 3x256 and the
 // block-diagonal 3x(256->3) remain: 0.5335 MFLOP instead of the reference's 2.336 MFLOP.
 //
-// Tiling. A workgroup (4 waves) owns 16 candidates. Candidates are MFMA columns, output channels are
-// MFMA rows, so weights are the streamed A operand (packed per lane by pack.py: one coalesced 1 KiB
-// load per 4 MFMAs) and activations stay in the accumulator-native LDS layout between layers.
-// Exact f32 MFMA (v_mfma_f32_16x16x4_f32).
+// Tiling. A workgroup (8 waves) owns 16 candidates. Candidates are MFMA columns, output channels are
+// MFMA rows, so weights are the streamed A operand (packed per lane by pack.py: coalesced 1 KiB
+// loads) and activations stay in the accumulator-native LDS layout between layers. The two
+// per-candidate GEMMs run as split-f16 MFMA (gp_head.h head_trunk_split) when gp_head_weights
+// carries the packed f16 planes, exact f32 MFMA (v_mfma_f32_16x16x4_f32) otherwise.
 //
 // PC step fusion. The Langevin step size uses the mean score norm over ALL rows of the call
 // (samplers.py:143), a grid-wide dependency. Launch i therefore (a) finishes step i-1 for its own
@@ -77,7 +78,7 @@ extern "C" int gp_head_time_proj(const gp_head_weights* w, const float* t, int n
 }
 
 // ============================================================================ score / energy eval
-template <int MODE>  // 0: score f/(sigma+1e-7), 1: energy (IP, decoupled)
+template <int MODE, bool SPLIT>  // MODE 0: score f/(sigma+1e-7), 1: energy (IP, decoupled)
 __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights w, const float* __restrict__ pobj,
                                                        const float* __restrict__ tproj, float sigma,
                                                        const float* __restrict__ x, int rows, int kper,
@@ -95,7 +96,10 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
         const int r = r0 + threadIdx.x;
         obj[threadIdx.x] = (r < rows ? r : rows - 1) / kper;
     }
-    head_trunk<1, EVAL_WV>(w, pobj, tproj, obj, sm);
+    if constexpr (SPLIT)
+        head_trunk_split<1, EVAL_WV>(w, pobj, tproj, obj, sm);
+    else
+        head_trunk<1, EVAL_WV>(w, pobj, tproj, obj, sm);
     if (MODE == 0) {
         if (threadIdx.x < 144) {
             const int c = threadIdx.x / 9, o = threadIdx.x - c * 9;
@@ -118,7 +122,11 @@ extern "C" int gp_score_eval(const gp_head_weights* w, const float* pobj, const 
                              const float* x, int rows, int k, float* score, hipStream_t stream) {
     GP_REQUIRE(w && pobj && tproj_row && x && score && rows >= 0 && k >= 1, "score_eval: bad arguments");
     if (!rows) return GP_OK;
-    hipLaunchKernelGGL(head_eval_kernel<0>, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
+    if (w->pe2_h)
+        hipLaunchKernelGGL((head_eval_kernel<0, true>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
+                       sigma, x, rows, k, score);
+    else
+        hipLaunchKernelGGL((head_eval_kernel<0, false>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
                        sigma, x, rows, k, score);
     return gp_check_launch("head_eval_kernel<score>");
 }
@@ -127,7 +135,11 @@ extern "C" int gp_energy_eval(const gp_head_weights* w, const float* pobj, const
                               const float* pose, int rows, int k, float* energy, hipStream_t stream) {
     GP_REQUIRE(w && pobj && tproj_row && pose && energy && rows >= 0 && k >= 1, "energy_eval: bad arguments");
     if (!rows) return GP_OK;
-    hipLaunchKernelGGL(head_eval_kernel<1>, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
+    if (w->pe2_h)
+        hipLaunchKernelGGL((head_eval_kernel<1, true>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
+                       sigma, pose, rows, k, energy);
+    else
+        hipLaunchKernelGGL((head_eval_kernel<1, false>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
                        sigma, pose, rows, k, energy);
     return gp_check_launch("head_eval_kernel<energy>");
 }

@@ -103,9 +103,9 @@ class HeadModel:
         self._pc_ws: Optional[torch.Tensor] = None
 
     def set_arith(self, arith: str) -> None:
-        """PC sampler GEMM arithmetic: "split_f16" (pose_encoder.2 and head layer 1's pose block as
-        f16 hi/lo MFMA products, gp_head.h) or "f32" (exact fp32 MFMA). Evaluation and ODE kernels
-        are fp32 either way."""
+        """Per-candidate GEMM arithmetic of every head kernel (PC step, score/energy eval, ODE stages):
+        "split_f16" (pose_encoder.2 and head layer 1's pose block as f16 hi/lo MFMA products,
+        gp_head.h) or "f32" (exact fp32 MFMA)."""
         if arith not in ("split_f16", "f32"):
             raise ValueError(f"unknown head arithmetic {arith!r} (split_f16 | f32)")
         ptrs = {k: self.up.ptr(k) for k in pack.HEAD_FIELDS}

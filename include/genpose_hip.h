@@ -91,8 +91,9 @@ typedef struct {
     const float *h1t_t;   /* head layer 1, t columns, transposed (128, 768) */
     /* Split-f16 form of pe2_w / h1p_w for the PC sampler (pack.py pack_h16_fragments): f16 hi/lo
      * planes of W * 2^e. hsc = {A0, B0, A2, B2, e_pe2, e_h1p, 0, 0}: max row L1 norm and max |bias|
-     * of pose_encoder.0 / .2 (activation bounds) and the two weight exponents. All three NULL:
-     * gp_pc_sample computes those GEMMs in exact fp32 instead. */
+     * of pose_encoder.0 / .2 (activation bounds) and the two weight exponents. Used by every
+     * per-candidate head kernel (PC step, score/energy eval, ODE stages). All three NULL: those
+     * GEMMs run in exact fp32 instead. */
     const void *pe2_h;
     const void *h1p_h;
     const float *hsc;
