@@ -499,23 +499,33 @@ __device__ __forceinline__ void gram_schmidt6(T* v) {
     v[5] = c2 / n2;
 }
 
+// Division / square root of the PC update chain: IEEE by default; PC_FAST_UPDATE builds use the
+// hardware v_rcp_f32 / v_sqrt_f32 (<= 1 ulp) to shorten wave 0's dependent chain (tuning only).
+#ifdef PC_FAST_UPDATE
+__device__ __forceinline__ float udiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ float usqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+#else
+__device__ __forceinline__ float udiv(float a, float b) { return fdiv(a, b); }
+__device__ __forceinline__ float usqrt(float x) { return sqrtf(x); }
+#endif
+
 // gram_schmidt6 spread over the four lanes of a row (lane part p: 0 -> v[0:3], 1 -> v[3:6],
 // 2 -> translation, untouched; 3 idle). Same operations and order as gram_schmidt6<float>.
 __device__ __forceinline__ void gram_schmidt6_quad(float* v, int p, int lane) {
 #pragma clang fp contract(off)
-    float n1 = sqrtf((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+    float n1 = usqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
     n1 = n1 > 1e-12f ? n1 : 1e-12f;
-    const float b0 = v[0] / n1, b1 = v[1] / n1, b2 = v[2] / n1;   // meaningful on p == 0
+    const float b0 = udiv(v[0], n1), b1 = udiv(v[1], n1), b2 = udiv(v[2], n1);   // meaningful on p == 0
     (void)lane;
     const float B0 = quad_bcast0(b0), B1 = quad_bcast0(b1), B2 = quad_bcast0(b2);
     const float d = (B0 * v[0] + B1 * v[1]) + B2 * v[2];
     float c0 = v[0] - d * B0, c1 = v[1] - d * B1, c2 = v[2] - d * B2;
-    float n2 = sqrtf((c0 * c0 + c1 * c1) + c2 * c2);
+    float n2 = usqrt((c0 * c0 + c1 * c1) + c2 * c2);
     n2 = n2 > 1e-12f ? n2 : 1e-12f;
     if (p == 0) {
         v[0] = b0; v[1] = b1; v[2] = b2;
     } else if (p == 1) {
-        v[0] = c0 / n2; v[1] = c1 / n2; v[2] = c2 / n2;
+        v[0] = udiv(c0, n2); v[1] = udiv(c1, n2); v[2] = udiv(c2, n2);
     }
 }
 

@@ -240,16 +240,16 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             float* x3 = xv[g];
             const bool upd = i > 0 && r < a.rows && p < 3;
             if (upd) {
-                const float gn = gacc / (float)a.rows;
-                const float ratio = a.ls_coef / gn;
+                const float gn = udiv(gacc, (float)a.rows);
+                const float ratio = udiv(a.ls_coef, gn);
                 const float ls = 2.0f * (ratio * ratio);
-                const float sq2ls = sqrtf(2.0f * ls);
+                const float sq2ls = usqrt(2.0f * ls);
                 float mean[3];
 #pragma unroll
                 for (int k = 0; k < 3; ++k) x3[k] = (x3[k] + ls * sv[g][k]) + sq2ls * z1v[g][k];
                 if (p < 2) {   // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
-                    const float nn = sqrtf((x3[0] * x3[0] + x3[1] * x3[1]) + x3[2] * x3[2]);
-                    x3[0] /= nn; x3[1] /= nn; x3[2] /= nn;
+                    const float nn = usqrt((x3[0] * x3[0] + x3[1] * x3[1]) + x3[2] * x3[2]);
+                    x3[0] = udiv(x3[0], nn); x3[1] = udiv(x3[1], nn); x3[2] = udiv(x3[2], nn);
                 }
                 // reverse-SDE Euler-Maruyama predictor (samplers.py:163-166; sign as in the reference)
                 const float g2 = prev.g * prev.g;
