@@ -384,6 +384,16 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
         uh[ct] = exp2i(e2 - 14 - ewh);   // undo both scales of head layer 1
         sh[ct] = exp2i(14 - e2 + ewh);   // head layer 1's fp32 init (pts + t blocks) in the scaled domain
     }
+    // head layer 1's fp32 init (pts + t blocks): first touch of pobj / tproj after the kernel
+    // boundary, so issued here, a whole pose_encoder.0 + .2 ahead of its use
+    f32x4 tpv[3 * TPW], pov[3 * TPW][NT];
+#pragma unroll
+    for (int i = 0; i < 3 * TPW; ++i) {
+        const int T = TH[i];
+        tpv[i] = ld4(tproj + 16 * T + 4 * q);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q);
+    }
     // ---- pose_encoder.0 (9 -> 256) in fp32, one k-group; ReLU, scale, split into the chunk planes
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
@@ -403,17 +413,7 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     __syncthreads();
     PC_MARK(2);
     // ---- pose_encoder.2 (256 -> 256)
-    constexpr int PE2_TAIL = 2;
-    stream_h_step<D2, KC_HID + D2 - PE2_TAIL, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
-    f32x4 tpv[3 * TPW], pov[3 * TPW][NT];
-#pragma unroll
-    for (int i = 0; i < 3 * TPW; ++i) {
-        const int T = TH[i];
-        tpv[i] = ld4(tproj + 16 * T + 4 * q);
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q);
-    }
-    stream_h_step<KC_HID + D2 - PE2_TAIL, KC_HID + D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
+    stream_h_step<D2, KC_HID + D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
     PC_MARK(3);
     f32x4 acc[3 * TPW][NT];
 #pragma unroll
