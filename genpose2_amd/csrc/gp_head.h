@@ -349,7 +349,7 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_h, 3 * HID * HID * 4);
     f16x8* act1h = reinterpret_cast<f16x8*>(sm.act1);   // same 16 KiB per column tile as fp32
     f16x8* act2h = reinterpret_cast<f16x8*>(sm.act2);
-    constexpr int D2 = PC_D2H, DH = HEAD_PREFETCH_H;
+    constexpr int D2 = PC_D2H, DH = NT > 1 ? 1 : HEAD_PREFETCH_H;   // NT = 2: registers for 2 column tiles
     int T2[TPW], TH[3 * TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) T2[t] = wid * TPW + t;

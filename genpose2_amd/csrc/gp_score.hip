@@ -387,12 +387,16 @@ extern "C" size_t gp_pc_workspace_size(int rows) {
     return sizeof(float) * ((size_t)rows * 9 * 5 + 2 * ntiles) + 256;
 }
 
-static int pc_pick_nt(int rows) {
-    // Measured on MI355X (scripts/kbench.py): 16 candidates x 8 waves per workgroup beats 32 x 4
-    // at every size (R=25,600: 125 vs 153 us/step) because 112 VGPRs leave room for two
-    // workgroups per CU, while the 32-wide tile needs 373 registers (one wave per SIMD).
-    (void)rows;
-    return 1;
+#ifndef PC_SPLIT_NT2_MIN
+#define PC_SPLIT_NT2_MIN 4097   // rows from which the split kernel takes 32-candidate tiles (> 256 tiles of 16)
+#endif
+static int pc_pick_nt(int rows, bool split) {
+    // exact fp32 (scripts/kbench.py): 16 candidates x 8 waves per workgroup beats 32 x 4 at every
+    // size (R=25,600: 125 vs 153 us/step): 112 VGPRs leave room for two workgroups per CU, while
+    // the 32-wide tile needs 373 registers (one wave per SIMD).
+    // split-f16: each workgroup streams the 1 MB of GEMM weights once per step whatever its width,
+    // so 32-candidate tiles halve the weight stream per candidate once there are enough tiles.
+    return split && rows >= PC_SPLIT_NT2_MIN ? 2 : 1;
 }
 
 extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const float* tproj, const float* step_tab,
@@ -404,9 +408,9 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     GP_REQUIRE(steps >= 2 && rows >= 1 && k >= 1, "pc_sample: need steps>=2, rows>=1, k>=1");
     GP_REQUIRE((z1 == nullptr) == (z2 == nullptr), "pc_sample: z1/z2 must both be given or both null");
     GP_REQUIRE(workspace_bytes >= gp_pc_workspace_size(rows), "pc_sample: workspace too small");
-    const int nt = pc_pick_nt(rows);
     // split-f16 GEMMs when the packed planes are given (gp_head_weights), exact fp32 otherwise
     const bool split = w->pe2_h != nullptr;
+    const int nt = pc_pick_nt(rows, split);
     GP_REQUIRE(!split || (w->h1p_h && w->hsc), "pc_sample: pe2_h, h1p_h and hsc must be given together");
     PCArgs a;
     a.w = *w;
@@ -435,7 +439,9 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
                                     step_tab[5 * i + 4]};
         if (i > 0) prev = PCStep{step_tab[5 * (i - 1)], step_tab[5 * (i - 1) + 1], step_tab[5 * (i - 1) + 2],
                                  step_tab[5 * (i - 1) + 3], step_tab[5 * (i - 1) + 4]};
-        if (nt == 2)
+        if (nt == 2 && split)
+            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV1, true>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+        else if (nt == 2)
             hipLaunchKernelGGL((pc_step_kernel<2, PC_WV2, false>), grid, dim3(PC_WV2 * 64), 0, stream, a, i, cur, prev);
         else if (split)
             hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, true>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);

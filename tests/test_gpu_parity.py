@@ -177,23 +177,42 @@ def test_pc_full_size_properties():
     assert not torch.equal(p1, p3)
 
 
-def test_pc_split_f16_matches_exact_f32():
-    """The split-f16 GEMMs (default) against the exact fp32 MFMA path on identical inputs and noise,
-    at the PC golden tests' tolerances (1e-4 rotation, 1e-5 relative translation)."""
+def _split_vs_f32(B, T):
     from genpose2_amd import synthetic
     from genpose2_amd.agent import PoseNet
     from genpose2_amd.config import GenPoseConfig
-    pts, center = synthetic.make_batch(5, 16, 1024)
+    pts, center = synthetic.make_batch(5, B, 1024)
     data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
     out = {}
     for arith in ("split_f16", "f32"):
-        a = PoseNet(GenPoseConfig(device=DEV, sampling_steps=100, noise_seed=7)).eval()
+        a = PoseNet(GenPoseConfig(device=DEV, sampling_steps=T, noise_seed=7)).eval()
         a.heads.set_arith(arith)
         out[arith] = a.pred_func(dict(data), repeat_num=50)[0].cpu().numpy()
-    p, ref = out["split_f16"], out["f32"]
+    return out["split_f16"], out["f32"]
+
+
+@pytest.mark.parametrize("B,T", [(16, 100), (96, 20)])
+def test_pc_split_f16_matches_exact_f32(B, T):
+    """The split-f16 GEMMs (default) against the exact fp32 MFMA path on identical inputs and noise,
+    at the PC golden tests' tolerances (1e-4 rotation, 1e-5 relative translation). 800 rows run
+    16-candidate tiles; 4800 rows (> PC_SPLIT_NT2_MIN = 4096) run the split path's 32-candidate
+    tiles against the fp32 path's 16-candidate tiles."""
+    p, ref = _split_vs_f32(B, T)
     assert np.abs(p[..., :6] - ref[..., :6]).max() < 1e-4
     assert rel(p[..., 6:], ref[..., 6:]) < 1e-5
     assert not np.array_equal(p, ref)   # the two paths really differ in arithmetic
+
+
+def test_pc_split_f16_long_trajectory_tail():
+    """4800 rows x 100 steps: a few of 28,800 rotation entries drift by up to ~7e-4 between any two
+    roundings of the same SDE (measured on MI355X for 16- and 32-candidate split tiles alike: the
+    untrained score net amplifies 1e-7 differences along a 100-step trajectory), so the bound here is
+    on the distribution: 99.9th percentile within the 1e-4 bar, max within 2e-3, mean within 1e-5."""
+    p, ref = _split_vs_f32(96, 100)
+    d = np.abs(p[..., :6] - ref[..., :6])
+    assert np.percentile(d, 99.9) < 1e-4
+    assert d.max() < 2e-3
+    assert d.mean() < 1e-5
 
 
 # ---------------------------------------------------------------- ODE sampler
