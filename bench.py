@@ -138,6 +138,10 @@ def main():
                     help="ode: the shipped evaluation's sampler (scripts/eval_single.sh: --sampler_mode ode "
                          "--T0 0.55, sampling_steps unset); reports B*K*nfev/s")
     ap.add_argument("--t0", type=float, default=0.55)
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1: encode batch k+1 on a side stream while batch k samples (every timed step "
+                         "still encodes and samples one batch; the first encode is not overlapped). "
+                         "Off by default: no gain measured (profiles/r1/ab_encoder_pipeline.txt)")
     args = ap.parse_args()
     cfgd = CONFIGS[args.config]
     ws, rank, local = dist_env()
@@ -167,11 +171,28 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(device=dev)
+    enc_side = torch.cuda.Stream(device=dev)
     samp_ev = []
+    pending = []   # --pipeline: the next batch's data dict, its encoder already enqueued on enc_side
+
+    def start_encode():
+        d = dict(data0)
+        enc_side.wait_stream(stream)
+        with torch.cuda.stream(enc_side):
+            score.encode_func(d)
+        pending.append(d)
     nfevs = []
 
-    def one_step(record=False):
-        data = dict(data0)
+    def one_step(record=False, last=False):
+        pipe = args.pipeline and not ode
+        if pipe:
+            if not pending:          # first step of a run: nothing to overlap with yet
+                start_encode()
+            data = pending.pop(0)
+            stream.wait_stream(enc_side)
+            data["pts_feat"].record_stream(stream)
+        else:
+            data = dict(data0)
         edata = None
         if energy is not None:
             # the energy encoder needs only the points: overlap it with the score sampler
@@ -195,7 +216,18 @@ def main():
                 e1.record(stream)
                 return out
             score.heads.pc_sample = timed
-        pose, _ = score.pred_func(data, repeat_num=K, T0=args.t0 if ode else None)
+        if pipe:
+            # the next batch's encoder runs beside this batch's sampler; after_encode
+            # (energy encoder) still starts here, before the sampler
+            if not last:
+                start_encode()
+            if score.after_encode is not None:
+                score.after_encode()
+            hook, score.after_encode = score.after_encode, None
+            pose, _ = score.pred_func(data, repeat_num=K, extract_feature=False)
+            score.after_encode = hook
+        else:
+            pose, _ = score.pred_func(data, repeat_num=K, T0=args.t0 if ode else None)
         if ode:
             nfevs.append(score.last_nfev)
         if record and not ode:
@@ -213,16 +245,16 @@ def main():
             scale.pred_scale_func({"pts_feat": data["pts_feat"], "axes": axes})
         return pose
 
-    for _ in range(args.warmup):
-        one_step()
+    for i in range(args.warmup):
+        one_step(last=i == args.warmup - 1)
     torch.cuda.synchronize(dev)
     if ws > 1:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step(record=True)
+    for i in range(args.steps):
+        one_step(record=True, last=i == args.steps - 1)
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
@@ -268,7 +300,8 @@ def main():
             "config": {"workload": f"config{args.config}: B={B} objects/GPU, N={N} pts, K={K} candidates, T={T} PC "
                                    f"steps, {'ScoreNet+EnergyNet+ranking/aggregation' if cfgd['energy'] else 'ScoreNet'}"
                                    f"{' + ScaleNet' if cfgd['scale'] else ''} (encoder + sampler per step)",
-                       "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)"},
+                       "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)",
+                       "encoder_pipelined": bool(args.pipeline)},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": load_traffic(B * K),
                          "kernel": "pc_step_kernel", "arith": score.heads.arith, "flop_per_launch": flop_launch,

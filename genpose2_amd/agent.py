@@ -123,12 +123,14 @@ class PoseNet:
     # ------------------------------------------------------------------ pred_func
     @torch.no_grad()
     def pred_func(self, data, repeat_num, save_path="./visualization_results", return_average_res=False,
-                  init_x: torch.Tensor = None, T0=None, return_process=False):
-        """posenet_agent.py:490-584."""
+                  init_x: torch.Tensor = None, T0=None, return_process=False, extract_feature=True):
+        """posenet_agent.py:490-584. extract_feature=False takes data["pts_feat"] from an earlier
+        encode_func (as get_energy's flag does), so a serving loop can encode the next batch on a
+        side stream while this one samples."""
         if self.cfg.agent_type != "score":
             raise NotImplementedError("pred_func needs agent_type='score'")
         self.is_testing = True
-        feat = self._encode(data)
+        feat = self._encode(data) if extract_feature else dev.require_device_tensor(data["pts_feat"], "pts_feat")
         data["pts_feat"] = feat
         data["rgb_feat"] = None                    # dino none (posenet.py:316-318)
         if self.after_encode is not None:          # pipeline hook: start side-stream work here

@@ -550,3 +550,26 @@ def test_stage_scale_with_scalenet(tmp_path):
                                     "axes": aggs[0][:, :3, :3].to(DEV).contiguous()})
     assert torch.equal(lengths[0], ref.cpu()) and lengths[0].shape == (2, 3)
     assert torch.equal(finals[0][:, :3, 3], aggs[0][:, :3, 3])
+
+
+def test_pred_func_with_precomputed_features():
+    """pred_func(extract_feature=False) on data["pts_feat"] from encode_func (encoded on a side
+    stream, as bench.py --pipeline does) equals the encode-inside call bit for bit."""
+    from genpose2_amd import synthetic
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    pts, center = synthetic.make_batch(3, 4, 1024)
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
+    cfg = GenPoseConfig(device=DEV, sampling_steps=10, noise_seed=3)
+    ref, _ = PoseNet(cfg).eval().pred_func(dict(data), repeat_num=8)
+    agent = PoseNet(cfg).eval()
+    d2 = dict(data)
+    side = torch.cuda.Stream(device=DEV)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        agent.encode_func(d2)
+    torch.cuda.current_stream().wait_stream(side)
+    got, _ = agent.pred_func(d2, repeat_num=8, extract_feature=False)
+    assert torch.equal(got, ref)
+    with pytest.raises(Exception):
+        agent.pred_func(dict(data), repeat_num=8, extract_feature=False)   # no pts_feat given
