@@ -257,6 +257,12 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
 #ifndef PC_D2H
 #define PC_D2H 2                 // 32-deep chunks of pose_encoder.2 weights kept in flight
 #endif
+#ifndef PC_NT2_D2H
+#define PC_NT2_D2H 2             // the same for 32-candidate (NT = 2) tiles
+#endif
+#ifndef PC_NT2_DH
+#define PC_NT2_DH 1              // NT = 2: one head-layer-1 chunk in flight leaves registers for 2 column tiles
+#endif
 #ifndef HEAD_PREFETCH_H
 #define HEAD_PREFETCH_H 2        // 32-deep chunks of head-layer-1 weights kept in flight
 #endif
@@ -349,7 +355,7 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_h, 3 * HID * HID * 4);
     f16x8* act1h = reinterpret_cast<f16x8*>(sm.act1);   // same 16 KiB per column tile as fp32
     f16x8* act2h = reinterpret_cast<f16x8*>(sm.act2);
-    constexpr int D2 = PC_D2H, DH = NT > 1 ? 1 : HEAD_PREFETCH_H;   // NT = 2: registers for 2 column tiles
+    constexpr int D2 = NT > 1 ? PC_NT2_D2H : PC_D2H, DH = NT > 1 ? PC_NT2_DH : HEAD_PREFETCH_H;
     int T2[TPW], TH[3 * TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) T2[t] = wid * TPW + t;
