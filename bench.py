@@ -89,9 +89,10 @@ def cpu_baseline(cfg, threads):
     return out
 
 
-def load_traffic(rows):
+def load_traffic(rows, split):
     """HBM(+Infinity Cache) bytes per pc_step launch from the newest committed PMC pass for the
-    same row count (profiles/**/pmc_pc_step*.json, scripts/pmc_passes.sh), or None."""
+    same row count and arithmetic (profiles/**/pmc_pc_step*.json, scripts/pmc_passes.sh), or None.
+    Split-f16 instantiations carry a `true` template argument in the recorded kernel name."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "**", "pmc_pc_step*.json"), recursive=True))
     for fn in reversed(files):
         try:
@@ -99,7 +100,7 @@ def load_traffic(rows):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("rows") == rows:
+        if d.get("rows") == rows and (", true>" in d.get("kernel", "")) == bool(split):
             return d.get("hbm_bytes_per_launch")
     return None
 
@@ -303,7 +304,7 @@ def main():
                        "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)",
                        "encoder_pipelined": bool(args.pipeline)},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": load_traffic(B * K),
+                         "frac": achieved / peak, "traffic": load_traffic(B * K, split),
                          "kernel": "pc_step_kernel", "arith": score.heads.arith, "flop_per_launch": flop_launch,
                          "avg_launch_us": per_launch_s * 1e6, "sampler_ms_per_step": samp_ms,
                          "fp32_mfma_equiv_frac": achieved / FP32_PEAK_TFLOPS,
