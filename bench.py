@@ -1,10 +1,12 @@
 """Benchmark: pose candidates/s (B objects x K candidates x T denoise steps) on MI355X.
 
-One "step" = one PoseNet.pred_func call (PointNet++ encoder + T-step PC sampler) over one batch of
-synthetic objects resident in HBM, i.e. the reference's inference_score stage per batch
-(runners/evaluation_single.py:98-104). Config (BASELINE.json configs[1]): B=64 objects/GPU,
-N=1024 points, K=50 candidates, T=500 steps, ScoreNet only. --config 3 adds EnergyNet + ranking +
-aggregation, --config 5 is the B=256, N=2048, K=100, T=1000 + ScaleNet stress case.
+One "step" = one pass of the pose-candidate path over one batch of synthetic objects resident in
+HBM. Default (--config 4): the north-star shape, i.e. one GPU's shard of BASELINE config 4 --
+B=256 objects/GPU, N=1024 points, K=50 candidates, T=500 PC steps, ScoreNet encoder + sampler,
+EnergyNet encoder + energy, ranking + aggregation (runners/evaluation_single.py:78-219 per batch).
+--config 2 is ScoreNet only at B=64, --config 3 adds EnergyNet at B=64, --config 5 is the B=256,
+N=2048, K=100, T=1000 + ScaleNet stress case. PC runs also time the shipped ODE sampler
+(T0=0.55) on the same objects and report it under "ode".
 
 Multi-GPU: one process per GPU (torchrun), objects sharded (weak scaling: B objects per GPU),
 packed weights broadcast once from rank 0 over RCCL, no collective on the timed data path.
@@ -48,44 +50,99 @@ def broadcast_weights(agent, ws):
         shard.broadcast_tensors(shard.model_tensors(agent), src=0)
 
 
-def cpu_baseline(cfg, threads):
-    """Oracle ("port") timing on a bounded sample of the same workload: the encoder on 2 objects
-    and the PC sampler at the full R = B*K rows for a few steps, extrapolated to B objects and T
-    steps (per-object and per-step costs are independent of B and T)."""
+def cpu_info():
+    """CPU model, physical cores and the CPUs this process may run on."""
+    model, phys = "unknown", set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            pid = cid = None
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name":
+                    model = v
+                elif k == "physical id":
+                    pid = v
+                elif k == "core id":
+                    cid = v
+                elif not k and pid is not None:
+                    phys.add((pid, cid))
+                    pid = cid = None
+    except OSError:
+        pass
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return model, len(phys) or avail, avail
+
+
+def cpu_threads_default():
+    """All physical cores this process may use, capped by the OMP_NUM_THREADS allotment when set (the
+    GPU box exports OMP_NUM_THREADS=16: one GPU's share of the host)."""
+    _, phys, avail = cpu_info()
+    n = min(phys, avail)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline(cfg, config_id, threads, sample_objects, reps=3):
+    """Oracle ("port") timing per BASELINE.md §3: 1 warm-up run, then the median of `reps` runs of the
+    SAME workload (every stage the GPU step runs: score encoder, T-step PC sampler with K candidates,
+    and for full-pipeline configs the energy encoder + energy + ranking/aggregation, ScaleNet for
+    config 5) on a bounded sample of `sample_objects` objects, so the default bench stays within
+    minutes. Nothing is extrapolated in steps or candidates; per-object work is independent, so the
+    rate (candidate-steps/s) is the sample's own. profiles/r2/cpu_full_vs_sample.json checks it
+    against a full-batch run on the GPU host."""
     from genpose2_amd import synthetic, weights
     from oracle import oracle
     torch.set_num_threads(threads)
-    B, N, K, T = cfg["B"], cfg["N"], cfg["K"], cfg["T"]
+    Bs, N, K, T = min(sample_objects, cfg["B"]), cfg["N"], cfg["K"], cfg["T"]
     sd = weights.synthetic_state_dict("score")
-    pts, center = synthetic.make_batch(77, 2, N)
-    oracle.encoder_forward(sd, pts[:1])
+    sd_e = weights.synthetic_state_dict("energy") if cfg["energy"] else None
+    sd_s = weights.synthetic_state_dict("scale") if cfg["scale"] else None
+    pts, center = synthetic.make_batch(config_id, Bs, N)
+    rng = np.random.Generator(np.random.PCG64(0))
+    prior = rng.standard_normal((Bs * K, 9), dtype=np.float32)
+    z1 = rng.standard_normal((T, Bs * K, 9), dtype=np.float32)
+    z2 = rng.standard_normal((T, Bs * K, 9), dtype=np.float32)
+
+    def run():
+        pose, _, feat, _ = oracle.pred_func(sd, pts, center, K, T, "pc", prior, z1, z2)
+        axes = np.broadcast_to(np.eye(3, dtype=np.float32), (Bs, 3, 3))
+        if sd_e is not None:
+            e = oracle.get_energy(sd_e, pts, center, pose, 1e-5)
+            axes = oracle.aggregate_pose(pose, e)[:, :3, :3]
+        if sd_s is not None:
+            oracle.scale_forward(sd_s, feat, np.ascontiguousarray(axes))
+
     t0 = time.perf_counter()
-    feat = oracle.encoder_forward(sd, pts)
-    t_enc_obj = (time.perf_counter() - t0) / 2
-    R = B * K
-    feat_rows = np.repeat(np.resize(feat, (B, feat.shape[1])), K, axis=0)
-    rng = np.random.default_rng(0)
-    ts_sample = 6
-    z = rng.standard_normal((ts_sample, R, 9)).astype(np.float32)
-    x0 = (rng.standard_normal((R, 9)) * 50).astype(np.float32)
-    t0 = time.perf_counter()
-    oracle.pc_sample(lambda x, t: oracle.score_forward(sd, feat_rows, x, t), x0,
-                     np.zeros((R, 3), np.float32), ts_sample, z, z)
-    t_step = (time.perf_counter() - t0) / ts_sample
-    total = t_enc_obj * B + t_step * T
-    out = {"value": B * K * T / total, "unit": "pose-candidate-steps/s", "cores": threads, "kind": "port",
-           "sample": f"oracle (numpy fp32, reference unhoisted score form) encoder on 2 objects "
-                     f"({t_enc_obj*1e3:.0f} ms/object) + PC sampler at R={R} rows for {ts_sample} steps "
-                     f"({t_step*1e3:.0f} ms/step), extrapolated to B={B}, T={T}"}
+    run()
+    warm = time.perf_counter() - t0
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        run()
+        ts.append(time.perf_counter() - t0)
+    med = float(np.median(ts))
+    model, phys, avail = cpu_info()
+    stages = "score encoder + PC sampler" + (" + energy encoder/eval + ranking/aggregation" if cfg["energy"] else "") \
+        + (" + ScaleNet" if cfg["scale"] else "")
+    out = {"value": Bs * K * T / med, "unit": "pose-candidate-steps/s", "cores": threads, "kind": "port",
+           "sample": f"oracle (numpy fp32, the reference's unhoisted score form; sklearn DBSCAN) on {Bs} of the "
+                     f"{cfg['B']} objects of config {config_id}, full K={K}, T={T} ({stages}); 1 warm-up "
+                     f"({warm:.2f} s) + median of {reps}: {med:.2f} s (runs {', '.join(f'{t:.2f}' for t in ts)} s)",
+           "cpu_model": model, "physical_cores": phys, "cpus_available": avail,
+           "torch_threads": torch.get_num_threads(),
+           "float32_matmul_precision": torch.get_float32_matmul_precision()}
     # SURVEY §8d (i): the oracle/reference time ratio measured in the build container on identical
-    # inputs and threads (oracle/calibrate_cpu.py); converts the port figure to reference terms
-    cal = os.path.join(REPO, "profiles", "r1", "cpu_calibration.json")
-    if os.path.exists(cal):
+    # inputs (oracle/calibrate_cpu.py); converts the port figure to reference terms
+    for cal in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "cpu_calibration.json")), reverse=True):
         with open(cal) as f:
             c = json.load(f)
         out["calibration"] = {"oracle_over_reference": round(c["oracle_over_reference"], 3),
-                              "threads": c["threads"], "source": "profiles/r1/cpu_calibration.json"}
+                              "threads": c["threads"], "source": os.path.relpath(cal, REPO)}
         out["reference_equivalent_value"] = out["value"] * c["oracle_over_reference"]
+        break
     return out
 
 
@@ -127,14 +184,52 @@ def report_ode(args, B, N, K, ws, rank, elapsed, nfevs, cfgd):
         }), flush=True)
 
 
+def time_ode_calls(args, cfg, data0, B, K, ws, dev):
+    """The shipped evaluation sampler (scripts/eval_single.sh: --sampler_mode ode --T0 0.55, steps unset)
+    on the same objects: encoder + device RK45 per pred_func call, 1 warm-up + args.ode_calls timed,
+    max over ranks. SURVEY §8d: report nfev and B*K*nfev/s."""
+    from genpose2_amd.agent import PoseNet
+    agent = PoseNet(cfg.copy(sampler_mode=["ode"], sampling_steps=None)).eval()
+    broadcast_weights(agent, ws)
+    agent.pred_func(dict(data0), repeat_num=K, T0=0.55)
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    nf = []
+    t0 = time.perf_counter()
+    for _ in range(args.ode_calls):
+        agent.pred_func(dict(data0), repeat_num=K, T0=0.55)
+        nf.append(agent.last_nfev)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    per = el / args.ode_calls
+    nfev = float(np.mean(nf))
+    return {"metric": "pose candidate-RHS evaluations/sec (B objs x K cands x nfev, ODE sampler, T0=0.55)",
+            "value": B * K * ws * float(np.sum(nf)) / el, "unit": "pose-candidate-evals/s", "nfev": nfev,
+            "ms_per_call": per * 1e3, "poses_per_s": B * K * ws / per, "calls": args.ode_calls,
+            "workload": f"B={B} objects/GPU, K={K}: encoder + RK45 (rtol=atol=1e-5) + denoise per call"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS),
+                    help="4 (default): the north-star shape, one GPU's shard of BASELINE config 4 "
+                         "(B=256, K=50, T=500, ScoreNet + EnergyNet + ranking/aggregation)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle CPU baseline threads (0: all physical "
+                                                               "cores available, capped by OMP_NUM_THREADS)")
+    ap.add_argument("--cpu-sample-objects", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ode-calls", type=int, default=3,
+                    help="PC runs: also time this many ODE pred_func calls (shipped setting T0=0.55, RK45) on "
+                         "the same objects and report them under 'ode' (0: off)")
     ap.add_argument("--sampler", choices=["pc", "ode"], default="pc",
                     help="ode: the shipped evaluation's sampler (scripts/eval_single.sh: --sampler_mode ode "
                          "--T0 0.55, sampling_steps unset); reports B*K*nfev/s")
@@ -271,6 +366,7 @@ def main():
         if ws > 1:
             dist.destroy_process_group()
         return
+    ode_info = time_ode_calls(args, cfg, data0, B, K, ws, dev) if args.ode_calls > 0 else None
     units = B * K * T * ws * args.steps
     samp_ms = float(np.mean([a.elapsed_time(b) for a, b in samp_ev]))
     per_launch_s = samp_ms / 1e3 / (T + 1)
@@ -283,7 +379,9 @@ def main():
     up = score.heads.up.t
     wg_bytes = sum(up[k].numel() * up[k].element_size() for k in
                    (("pe2_h", "h1p_h") if split else ("pe2_w", "h1p_w")))   # streamed per workgroup per step
-    nwg = -(-B * K // 16)
+    from genpose2_amd import _lib
+    tile = int(_lib.load().gp_pc_tile_rows(B * K, int(split)))   # the kernel's real tile width
+    nwg = -(-B * K // tile)
     if rank == 0:
         out = {
             "metric": "pose candidates/sec (B objs x K cands x T denoise steps)",
@@ -310,12 +408,16 @@ def main():
                          "fp32_mfma_equiv_frac": achieved / FP32_PEAK_TFLOPS,
                          # what binds the split kernel: every workgroup streams the GEMM weights from L2
                          "l2_weight_stream": {"bytes_per_workgroup": wg_bytes, "workgroups": nwg,
+                                              "candidates_per_workgroup": tile,
                                               "GBps_per_CU": wg_bytes / per_launch_s / 1e9,
                                               "TBps_chip": wg_bytes * nwg / per_launch_s / 1e12}},
         }
+        if ode_info is not None:
+            out["ode"] = ode_info
         if not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(cfgd, threads) if ws == 1 else None
+            threads = args.cpu_threads or cpu_threads_default()
+            out["cpu_baseline"] = (cpu_baseline(cfgd, args.config, threads, args.cpu_sample_objects)
+                                   if ws == 1 else None)
         print(json.dumps(out), flush=True)
     if ws > 1:
         dist.destroy_process_group()

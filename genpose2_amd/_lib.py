@@ -52,6 +52,7 @@ _SIGS: Dict[str, tuple] = {
     "gp_energy_eval": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_float, c_void_p, c_int, c_int,
                                c_void_p, c_void_p]),
     "gp_pc_workspace_size": (c_size_t, [c_int]),
+    "gp_pc_tile_rows": (c_int, [c_int, c_int]),
     "gp_pc_sample": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_float, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_size_t, c_void_p]),

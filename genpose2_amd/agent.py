@@ -168,7 +168,7 @@ class PoseNet:
             raise NotImplementedError(mode)
         self.pts_feature = False
         if return_average_res:
-            avg = torch.zeros((bs, 7), dtype=pred_q.dtype, device=self.device)
+            avg = torch.zeros((bs, 7), dtype=torch.float32, device=self.device)   # torch.zeros((bs, 7)): fp32 (:560)
             avg[:, :4] = aggregate.average_quaternion_batch(pred_q[:, :, :4])
             avg[:, 4:] = torch.mean(pred_q[:, :, 4:], dim=1)
             if return_process:
@@ -193,12 +193,21 @@ class PoseNet:
         t_eval = None if steps is None else np.linspace(T0, eps, steps)
         if want_process or self.ode_host_control:
             # every solve_ivp output is kept: host-side controller, one error norm read per attempt
-            _, nfev, _ = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process)
-            ys = be.outputs()                  # (n_t or 1, R*9) fp64
-            x = ys[-1]
+            _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process)
         else:
             # default: the step controller runs on the device (no host round trip per attempt)
-            x, nfev, _ = rk45_device(be, T0, eps, t_eval=t_eval)
+            x, nfev, status = rk45_device(be, T0, eps, t_eval=t_eval)
+        if status < 0 and t_eval is not None and not want_process:
+            # failed solve (step below spacing): solve_ivp returns the t_eval points collected so far and
+            # cond_ode_sampler continues from res.y[:, -1]; only the host restatement keeps them all
+            be = DeviceRk45(self.heads, pobj, x0.to(self.device), K)
+            _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=True)
+            want_process = False
+        if want_process or self.ode_host_control or (status < 0 and t_eval is not None):
+            ys = be.outputs()                  # (n_t or 1, R*9) fp64
+            if ys.shape[0] == 0:               # res.y[:, -1] of an empty solve_ivp result
+                raise IndexError("RK45 failed before collecting any t_eval point (res.y is empty)")
+            x = ys[-1]
         self.last_nfev = nfev
         # denoise with the PC predictor step (samplers.py:240-249), GS, + pts_center, quaternion
         t32, sig, _ = time_scalars(eps)

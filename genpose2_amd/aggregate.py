@@ -13,7 +13,7 @@ which the reference also runs as torch ops on device.
 from __future__ import annotations
 
 import ctypes
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 
@@ -92,12 +92,18 @@ def quaternion_to_matrix(q: torch.Tensor) -> torch.Tensor:
 
 
 def aggregate_pose(pred_pose: torch.Tensor, pred_energy: torch.Tensor, retain_ratio: float = 0.4,
-                   clustering: int = 1, clustering_eps: float = 0.05, clustering_minpts: float = 0.1667):
-    """evaluation_single.py:160-219 for one batch -> (B, 4, 4) float32 on pred_pose's device."""
+                   clustering: int = 1, clustering_eps: float = 0.05, clustering_minpts: float = 0.1667,
+                   retain_num: Optional[int] = None):
+    """evaluation_single.py:160-219 for one batch -> (B, 4, 4) float32 on pred_pose's device.
+
+    retain_num: the runner's ``int(cfg.eval_repeat_num * cfg.retain_ratio)`` (:180); defaults to
+    int(K * retain_ratio) for a batch of K candidates per object."""
     K = pred_pose.shape[1]
-    keep = int(K * retain_ratio)
+    keep = int(K * retain_ratio) if retain_num is None else int(retain_num)
     if keep < 1:
         raise ValueError(f"retain_ratio {retain_ratio} keeps no candidate of K={K}")
+    if keep > K:   # the reference's reshape(bs * retain_num, -1) fails the same way
+        raise ValueError(f"retain_num {keep} exceeds the {K} candidates per object")
     agg, _, _ = _rank_aggregate(pred_pose.to(torch.float32), pred_energy.to(torch.float32), keep, clustering,
                                 clustering_eps, int(clustering_minpts * keep), False)
     return agg

@@ -106,6 +106,14 @@ __device__ void top_eigvec4(double A[4][4], float* out) {
     for (int i = 0; i < 4; ++i) out[i] = (float)(sgn * v[i] / nrm);
 }
 
+// Does candidate (b, j) come before (a, i) in torch.sort(descending=True) order? NaN sorts as the
+// largest value (torch's comparator), equal keys (NaN with NaN too) keep the lower index first.
+__device__ __forceinline__ bool precedes(float b, int j, float a, int i) {
+    const bool an = a != a, bn = b != b;
+    if (an || bn) return bn && (!an || j < i);
+    return b > a || (b == a && j < i);
+}
+
 struct AggSmem {
     int rank_rot[AGG_MAXK];
     int rank_tr[AGG_MAXK];
@@ -130,14 +138,14 @@ __global__ __launch_bounds__(AGG_THREADS) void rank_aggregate_kernel(
     const int b = blockIdx.x, tid = threadIdx.x;
     const float* P = poses + (size_t)b * K * 9;
     const float* E = energy + (size_t)b * K * 2;
-    // ---- 1. descending ranks, ties by lower index (stable)
+    // ---- 1. descending ranks, ties by lower index (stable); a total order, so the ranks are a
+    //         permutation whatever the energies hold (precedes(): NaN first, as torch.sort orders it)
     for (int i = tid; i < K; i += AGG_THREADS) {
         const float er = E[2 * i], et = E[2 * i + 1];
         int rr = 0, rt = 0;
         for (int j = 0; j < K; ++j) {
-            const float fr = E[2 * j], ft = E[2 * j + 1];
-            rr += (fr > er) || (fr == er && j < i);
-            rt += (ft > et) || (ft == et && j < i);
+            rr += precedes(E[2 * j], j, er, i);
+            rt += precedes(E[2 * j + 1], j, et, i);
         }
         sm.rank_rot[i] = rr;
         sm.rank_tr[i] = rt;

@@ -399,6 +399,10 @@ static int pc_pick_nt(int rows, bool split) {
     return split && rows >= PC_SPLIT_NT2_MIN ? 2 : 1;
 }
 
+// Candidates per PC-step workgroup that gp_pc_sample picks for `rows` (split: head weights with
+// the f16 planes) -- lets callers size their accounting from the kernel's real tiling.
+extern "C" int gp_pc_tile_rows(int rows, int split) { return 16 * pc_pick_nt(rows, split != 0); }
+
 extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const float* tproj, const float* step_tab,
                             int steps, float* x, int rows, int k, const float* pts_center, const float* z1,
                             const float* z2, uint64_t seed, float snr, float* res, float* q, float* xs,

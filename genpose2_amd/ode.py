@@ -320,6 +320,7 @@ class DeviceRk45:
         self.t_eval_dev = torch.from_numpy(np.ascontiguousarray(t_eval, dtype=np.float64)).to(self.dev)
         rows = t_eval.shape[0] if keep_all else 1
         self.dense_out = torch.empty((rows, self.n), dtype=torch.float64, device=self.dev)
+        self.n_dense = 0    # t_eval points collected so far (solve_ivp order: the first n_dense rows)
 
     def rhs0(self, t):
         self._rhs(t, [], [], 0.0, self.K[0])
@@ -368,6 +369,7 @@ class DeviceRk45:
         h = t - t_old
         if self.keep_all:
             i0, i1, base, rev = lo, hi, (self.t_eval.shape[0] - 1 if self.direction < 0 else 0), int(self.direction < 0)
+            self.n_dense += max(0, hi - lo)
         else:   # only the final t_eval point (t_bound side) is kept
             last = 0 if self.direction < 0 else self.t_eval.shape[0] - 1
             if not (lo <= last < hi):
@@ -379,9 +381,10 @@ class DeviceRk45:
                                     ctypes.c_void_p(self.dense_out.data_ptr()), self._s()), "ode_dense")
 
     def outputs(self) -> torch.Tensor:
-        """(n_t, R*9) fp64 outputs in solve_ivp order (all kept, or only the last)."""
+        """(n_t, R*9) fp64 outputs in solve_ivp order (all kept, or only the last). After a failed
+        solve (status -1) with keep_all, only the t_eval points collected before the failure."""
         if self.dense_out is not None:
-            return self.dense_out
+            return self.dense_out[: self.n_dense] if self.keep_all else self.dense_out
         return torch.stack(self.ys, 0)
 
 

@@ -80,7 +80,8 @@ class EvaluationPipeline:
         energy = out.energy if out.energy is not None else torch.ones(*pred_pose.shape[:2], 2,
                                                                       device=pred_pose.device)
         out.aggregated = aggregate.aggregate_pose(pred_pose, energy, cfg.retain_ratio, cfg.clustering,
-                                                  cfg.clustering_eps, cfg.clustering_minpts)
+                                                  cfg.clustering_eps, cfg.clustering_minpts,
+                                                  retain_num=int(cfg.eval_repeat_num * cfg.retain_ratio))
         if self.scale_agent is not None:
             sdata = {"pts_feat": out.pts_feat, "rgb_feat": None,
                      "axes": out.aggregated[:, :3, :3].contiguous()}
@@ -89,6 +90,43 @@ class EvaluationPipeline:
 
 
 # ============================================================================ process_batch
+
+class ShardedEvaluationPipeline:
+    """EvaluationPipeline over one process group (config 4: B=2048 objects over 8 GPUs).
+
+    Every rank holds the same agents; their packed weights are broadcast from ``src`` once (RCCL over
+    xGMI), so weights loaded on ``src`` alone (load_ckpt) reach every GPU. ``run`` takes the WHOLE
+    batch on every rank, processes the rank's contiguous object block (shard.shard_range) with no
+    collective on the sampling path -- each shard is a reference call on its sub-batch -- and gathers
+    pred_pose, pts_feat, energy, aggregated and length back in object order on every rank (dst=None)
+    or on ``dst`` only."""
+
+    def __init__(self, cfg: GenPoseConfig, with_energy: bool = True, with_scale: bool = False, src: int = 0):
+        from . import shard
+        self.local = EvaluationPipeline(cfg, with_energy, with_scale)
+        self.src = src
+        for a in (self.local.score_agent, self.local.energy_agent, self.local.scale_agent):
+            if a is not None:
+                shard.broadcast_tensors(shard.model_tensors(a), src=src)
+
+    def run(self, batch: Dict[str, torch.Tensor], dst: Optional[int] = None) -> Optional[StageOutputs]:
+        import torch.distributed as dist
+        from . import arch, shard
+        total = int(batch["pts"].shape[0])
+        lo, hi = shard.shard_range(total, dist.get_world_size(), dist.get_rank())
+        K = self.local.cfg.eval_repeat_num
+        if hi > lo:
+            out = self.local.run({k: v[lo:hi] for k, v in batch.items()})
+        else:   # more ranks than objects: an empty shard still joins the gathers
+            d = batch["pts"].device
+            z = lambda *s: torch.zeros(s, dtype=torch.float32, device=d)  # noqa: E731
+            out = StageOutputs(pred_pose=z(0, K, arch.POSE_DIM), pts_feat=z(0, arch.PTS_FEAT_DIM),
+                               energy=z(0, K, 2) if self.local.energy_agent is not None else None,
+                               aggregated=z(0, 4, 4), length=z(0, 3) if self.local.scale_agent is not None else None)
+        g = shard.gather_outputs({"pred_pose": out.pred_pose, "pts_feat": out.pts_feat, "energy": out.energy,
+                                  "aggregated": out.aggregated, "length": out.length}, total, dst)
+        return None if g is None else StageOutputs(**g)
+
 def process_batch(batch_sample: Dict, device, pose_mode: str = "rot_matrix", PTS_AUG_PARAMS=None) -> Dict:
     """process_batch (datasets_omni6dpose.py:674-754) for inference: the keys the pose-candidate
     path reads. ``pts`` = ``pcl_in`` on the device (un-normalised camera-frame points,
@@ -182,7 +220,8 @@ def aggregate_pose(cfg: GenPoseConfig, score_path: str, energy_path: Optional[st
     for pred_pose, pred_energy in zip(all_pred_pose, all_pred_energy):
         dev_ = pred_pose.device if pred_pose.is_cuda else torch.device(cfg.device)
         agg = aggregate.aggregate_pose(pred_pose.to(dev_), pred_energy.to(dev_), cfg.retain_ratio,
-                                       cfg.clustering, cfg.clustering_eps, cfg.clustering_minpts)
+                                       cfg.clustering, cfg.clustering_eps, cfg.clustering_minpts,
+                                       retain_num=int(cfg.eval_repeat_num * cfg.retain_ratio))   # :180
         all_aggregated_pose.append(agg.cpu())
     with open(save_path, "wb") as f:
         pickle.dump(all_aggregated_pose, f)

@@ -4,17 +4,23 @@ Objects are independent on the path except for two batch-wide scalars the refere
 per call (F3): the PC sampler's mean score norm and RK45's error norm. The default semantics
 are those of the reference called on each shard's sub-batch (the same batch-composition
 dependence the reference has with --batch_size), so the data path needs no collective. The
-one-time exchange is the packed-weight broadcast from rank 0 over RCCL (gloo on CPU tests).
+exchanges are:
+
+* once: the packed weights of every agent, broadcast from rank 0 (RCCL over xGMI; gloo on CPU);
+* per evaluated batch: the per-object outputs (pred_pose, energy, aggregated 4x4, lengths;
+  about 4.5 MB at config 4) gathered to rank 0 or to every rank -- one all_gather per output
+  tensor, off the timed sampling loop.
 """
 from __future__ import annotations
 
-from typing import Iterable, Tuple
+from typing import Dict, Iterable, List, Optional, Tuple
 
+import numpy as np
 import torch
 
 
 def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
-    """Contiguous block of ceil(total/world) objects for ``rank`` (last shard may be short)."""
+    """Contiguous block of ceil(total/world) objects for ``rank`` (last shards may be short or empty)."""
     per = -(-total // world)
     lo = min(total, rank * per)
     return lo, min(total, lo + per)
@@ -26,8 +32,9 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0) -> None:
         dist.broadcast(t, src=src)
 
 
-def model_tensors(agent) -> list:
-    """Device tensors holding an agent's packed weights, in a fixed order."""
+def model_tensors(agent) -> List[torch.Tensor]:
+    """Device tensors holding an agent's packed weights, in a fixed order: the encoder buffer, then
+    the head (or ScaleNet) buffers by name -- the same order as ``packed_host_tensors``."""
     out = []
     if getattr(agent, "encoder", None) is not None:
         out.append(agent.encoder.wbuf)
@@ -35,3 +42,44 @@ def model_tensors(agent) -> list:
     if getattr(agent, "scale", None) is not None:
         out += [agent.scale.up.t[k] for k in sorted(agent.scale.up.t)]
     return out
+
+
+def packed_host_tensors(kind: str, sd) -> List[torch.Tensor]:
+    """Host (CPU) tensors of exactly the buffers ``model_tensors`` holds on the device for an agent of
+    ``kind`` built from state dict ``sd`` (genpose2_amd.pack), in the same order."""
+    from . import pack
+    if kind == "scale":
+        p = pack.pack_scale(sd)
+        return [torch.from_numpy(np.ascontiguousarray(p[k])) for k in sorted(p)]
+    p = pack.pack_heads(sd)
+    return [torch.from_numpy(pack.pack_encoder(sd)[0])] + [torch.from_numpy(np.ascontiguousarray(p[k]))
+                                                           for k in sorted(p)]
+
+
+def gather_outputs(outputs: Dict[str, Optional[torch.Tensor]], total: int, dst: Optional[int] = None
+                   ) -> Optional[Dict[str, Optional[torch.Tensor]]]:
+    """Reassemble per-object outputs sharded by ``shard_range``: every tensor's dim 0 is this rank's
+    objects. Each tensor is padded to ceil(total/world) rows and all-gathered; the result (rows in
+    object order, the padding dropped) is returned on every rank (dst=None) or on rank ``dst`` only
+    (other ranks get None). None entries stay None. Works on RCCL (device tensors) and gloo (CPU)."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    per = -(-total // world)
+    lo, hi = shard_range(total, world, rank)
+    res: Dict[str, Optional[torch.Tensor]] = {}
+    for name in sorted(outputs):
+        t = outputs[name]
+        if t is None:
+            res[name] = None
+            continue
+        if t.shape[0] != hi - lo:
+            raise ValueError(f"{name}: {t.shape[0]} rows on rank {rank}, shard holds {hi - lo} objects")
+        buf = torch.zeros((per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        buf[: hi - lo] = t
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf.contiguous())
+        rows = [parts[r][: shard_range(total, world, r)[1] - shard_range(total, world, r)[0]] for r in range(world)]
+        res[name] = torch.cat(rows, 0)
+    if dst is not None and rank != dst:
+        return None
+    return res

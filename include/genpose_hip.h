@@ -127,6 +127,9 @@ int gp_energy_eval(const gp_head_weights *w, const float *pobj, const float *tpr
  * Outputs: res (R,9) = mean_x of the last step (+pts_center, GS), q (R,7) = [quat_wxyz, trans]
  * (posenet_agent.py:554-556), xs (R,T,9) trajectory or NULL. */
 size_t gp_pc_workspace_size(int rows);
+/* Candidates per PC-step workgroup gp_pc_sample uses for `rows` (split != 0: head weights carry the
+ * split-f16 planes). For accounting only (the per-workgroup weight stream). */
+int gp_pc_tile_rows(int rows, int split);
 int gp_pc_sample(const gp_head_weights *w, const float *pobj, const float *tproj,
                  const float *step_tab, int steps, float *x, int rows, int k,
                  const float *pts_center, const float *z1, const float *z2, uint64_t seed,

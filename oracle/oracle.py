@@ -86,15 +86,16 @@ def gather_operation(features: np.ndarray, idx: np.ndarray) -> np.ndarray:
 
 # ============================================================ encoder (Pointnet2ClsMSG)
 def _conv_bn_relu(x: np.ndarray, sd, prefix: str) -> np.ndarray:
-    """Conv2d 1x1 (no bias) -> BatchNorm2d(eval) -> ReLU (pytorch_utils.py:58-106)."""
-    w = sd[f"{prefix}.conv.weight"][:, :, 0, 0].astype(F32)
-    y = np.einsum("oc,bcms->boms", w, x, optimize=True).astype(F32)
-    g = sd[f"{prefix}.bn.bn.weight"].astype(F32)[:, None, None]
-    b = sd[f"{prefix}.bn.bn.bias"].astype(F32)[:, None, None]
-    mu = sd[f"{prefix}.bn.bn.running_mean"].astype(F32)[:, None, None]
-    var = sd[f"{prefix}.bn.bn.running_var"].astype(F32)[:, None, None]
-    y = (y - mu) / np.sqrt(var + F32(arch.BN_EPS)) * g + b
-    return np.maximum(y, F32(0)).astype(F32)
+    """Conv2d 1x1 (no bias) -> BatchNorm2d(eval) -> ReLU (pytorch_utils.py:58-106), through the same
+    torch CPU operators the reference's SharedMLP calls (one thread pool with the rest of the CPU
+    baseline: numpy's OpenBLAS beside torch's OpenMP pool oversubscribes the cores)."""
+    import torch
+    import torch.nn.functional as tf
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(sd[f"{prefix}.{k}"], dtype=F32))  # noqa: E731
+    y = tf.conv2d(torch.from_numpy(np.ascontiguousarray(x, dtype=F32)), t("conv.weight"))
+    y = tf.batch_norm(y, t("bn.bn.running_mean"), t("bn.bn.running_var"), t("bn.bn.weight"), t("bn.bn.bias"),
+                      training=False, eps=arch.BN_EPS)
+    return torch.relu(y).numpy()
 
 
 def encoder_forward(sd, pts: np.ndarray, return_levels: bool = False):
@@ -166,7 +167,11 @@ def gram_schmidt(rot6: np.ndarray) -> np.ndarray:
 
 # ============================================================ score / energy MLP
 def _lin(x, w, b):
-    return (x @ w.T.astype(F32) + b.astype(F32)).astype(F32)
+    """nn.Linear as the reference calls it (torch CPU F.linear)."""
+    import torch
+    import torch.nn.functional as tf
+    c = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=F32))  # noqa: E731
+    return tf.linear(c(x), c(w), c(b)).numpy()
 
 
 def head_features(sd, pts_feat, pose, t):
@@ -377,8 +382,11 @@ def average_quaternion_batch(Q: np.ndarray) -> np.ndarray:
 def sort_poses_by_energy(poses: np.ndarray, energy: np.ndarray):
     """reward.py:131-155: rotation part ordered by energy[...,0] desc, translation part by
     energy[...,1] desc."""
-    o_rot = np.argsort(-energy[..., 0], axis=1, kind="stable")
-    o_tr = np.argsort(-energy[..., 1], axis=1, kind="stable")
+    import torch   # torch.sort(descending=True) as reward.py:144 calls it: NaN first, ties keep index order
+    o_rot = torch.sort(torch.from_numpy(np.ascontiguousarray(energy[..., 0])), dim=1, descending=True,
+                       stable=True)[1].numpy()
+    o_tr = torch.sort(torch.from_numpy(np.ascontiguousarray(energy[..., 1])), dim=1, descending=True,
+                      stable=True)[1].numpy()
     sp = np.take_along_axis(poses, o_rot[..., None], 1).copy()
     sp[..., 6:] = np.take_along_axis(poses, o_tr[..., None], 1)[..., 6:]
     se = np.stack([np.take_along_axis(energy[..., 0], o_rot, 1),

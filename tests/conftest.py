@@ -8,6 +8,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(REPO, "tests", "golden")
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+if GOLDEN not in sys.path:     # large_noise: inputs of the large-row fixtures, regenerated from seeds
+    sys.path.insert(0, GOLDEN)
 
 
 def pytest_configure(config):
@@ -34,3 +36,19 @@ def energy_sd():
 def scale_sd():
     from genpose2_amd import weights
     return weights.synthetic_state_dict("scale", seed=0)
+
+
+def write_reference_checkpoint(path, kind, seed=0, prefix=""):
+    """A checkpoint in the file format of the reference's PoseNet.save_ckpt (posenet_agent.py:141-169,
+    pinned by golden_ckpt_layout.json): {clock, model_state_dict, optimizer_state_dict (Adam),
+    scheduler_state_dict (ExponentialLR)}, holding the seeded synthetic weights of `kind`.
+    prefix="module." mimics a DataParallel-wrapped net."""
+    import torch
+    from genpose2_amd import weights
+    sd = {prefix + k: torch.from_numpy(v) for k, v in weights.synthetic_state_dict(kind, seed=seed).items()}
+    params = [torch.nn.Parameter(torch.zeros(2))]
+    opt = torch.optim.Adam(params, betas=(0.9, 0.999), eps=1e-8, lr=1e-3)
+    sched = torch.optim.lr_scheduler.ExponentialLR(opt, 0.998)
+    torch.save({"clock": {"epoch": 1, "minibatch": 0, "step": 0}, "model_state_dict": sd,
+                "optimizer_state_dict": opt.state_dict(), "scheduler_state_dict": sched.state_dict()}, path)
+    return path

@@ -351,12 +351,48 @@ def gen_tracking(get_config, PoseNet):
     np.savez_compressed(os.path.join(HERE, "golden_tracking.npz"), **out)
 
 
+def gen_ckpt_layout(get_config, PoseNet):
+    """The structure of a checkpoint written by the reference's own PoseNet.save_ckpt
+    (posenet_agent.py:141-169) for each agent type: top-level keys, every model_state_dict key with
+    shape and dtype, the optimizer/scheduler state keys and the clock. Written to a scratch dir, loaded
+    back with torch.load(weights_only=True) (what the build's load_ckpt does), summarised as JSON."""
+    import json
+    import tempfile
+    from networks.gf_algorithms.score_utils import ExponentialMovingAverage
+    out = {}
+    for kind in ("score", "energy", "scale"):
+        agent = make_agent(get_config, PoseNet, kind, "pc", 20)
+        # save_ckpt writes the EMA shadow weights: restart the EMA from the loaded weights
+        agent.ema = ExponentialMovingAverage(agent.net.parameters(), decay=agent.cfg.ema_rate)
+        with tempfile.TemporaryDirectory() as tmp:
+            agent.model_dir = tmp
+            agent.save_ckpt("latest")
+            ck = torch.load(os.path.join(tmp, "latest.pth"), map_location="cpu", weights_only=True)
+        sd = ck["model_state_dict"]
+        mine = weights.synthetic_state_dict(kind, seed=0)
+        same = all(np.array_equal(sd[k].numpy(), mine[k]) for k in mine)
+        out[kind] = {
+            "top_level_keys": sorted(ck),
+            "model_state_dict": {k: [list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()},
+            "optimizer_state_dict_keys": sorted(ck["optimizer_state_dict"]),
+            "scheduler_state_dict_keys": sorted(ck["scheduler_state_dict"]),
+            "clock": ck["clock"],
+            "weights_equal_synthetic": bool(same),
+        }
+    with open(os.path.join(HERE, "golden_ckpt_layout.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
     only = sys.argv[1] if len(sys.argv) > 1 else None      # e.g. "tracking": that fixture only
     get_config, PoseNet = import_reference("pc", 20)
     if only == "tracking":
         gen_tracking(get_config, PoseNet)
         print("tracking done")
+        return
+    if only == "ckpt":
+        gen_ckpt_layout(get_config, PoseNet)
+        print("ckpt layout done")
         return
     gen_encoder(get_config, PoseNet)
     print("encoder done")

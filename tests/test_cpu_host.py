@@ -175,35 +175,133 @@ def test_shard_ranges_cover_every_object_once():
         assert seen == list(range(total))
 
 
-def _gloo_worker(rank, world, port, out_dir):
+def _shard_reference(lo, hi, K, T):
+    """The per-shard computation (oracle): encoder + PC sampler (noise rows of objects lo..hi-1)
+    + energy + aggregation, i.e. a reference call on the sub-batch."""
+    from genpose2_amd import synthetic, weights
+    from oracle import oracle
+    pts, center = synthetic.make_batch(4, hi - lo, 1024, first_object=lo)
+    rng = [np.random.Generator(np.random.PCG64(1000 + b)) for b in range(lo, hi)]
+    prior = np.concatenate([r.standard_normal((K, 9), dtype=np.float32) for r in rng])
+    z = np.stack([np.concatenate([r.standard_normal((2 * T, 9), dtype=np.float32) for _ in range(K)], 1)
+                  for r in rng], 0)                                  # (b, 2T, K*9) -> rows of this shard
+    z = z.reshape(hi - lo, 2 * T, K, 9).transpose(1, 0, 2, 3).reshape(2 * T, (hi - lo) * K, 9)
+    pose, _, feat, _ = oracle.pred_func(weights.synthetic_state_dict("score"), pts, center, K, T, "pc", prior,
+                                        z[0::2], z[1::2])
+    energy = oracle.get_energy(weights.synthetic_state_dict("energy"), pts, center, pose, 1e-5)
+    agg = oracle.aggregate_pose(pose, energy, clustering=0)
+    return {"pred_pose": pose, "pts_feat": feat, "energy": energy, "aggregated": agg}
+
+
+def _gloo_worker(rank, world, port, out_dir, total):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from genpose2_amd import pack, shard, synthetic, weights
-    from oracle import oracle
-    # rank 0 owns the packed weights; other ranks receive them by broadcast (the RCCL step)
-    sd = weights.synthetic_state_dict("score", seed=0 if rank == 0 else 99)
-    heads = {k: torch.from_numpy(v) for k, v in sorted(pack.pack_heads(sd).items())}
-    shard.broadcast_tensors(list(heads.values()), src=0)
-    ref = pack.pack_heads(weights.synthetic_state_dict("score", seed=0))
-    ok = all(np.array_equal(heads[k].numpy(), ref[k]) for k in ref)
-    lo, hi = shard.shard_range(6, world, rank)
-    pts, _ = synthetic.make_batch(4, hi - lo, 1024, first_object=lo)
-    feat = oracle.encoder_forward(weights.synthetic_state_dict("score"), pts)
-    np.save(os.path.join(out_dir, f"feat_{rank}.npy"), feat)
+    from genpose2_amd import shard, weights
+    # every agent's packed buffers (encoder + heads for score/energy, ScaleNet): rank 0 owns the
+    # weights, the others start from different ones and receive rank 0's by broadcast (the RCCL step)
+    ok = True
+    for kind in ("score", "energy", "scale"):
+        mine = shard.packed_host_tensors(kind, weights.synthetic_state_dict(kind, seed=0 if rank == 0 else 99))
+        shard.broadcast_tensors(mine, src=0)
+        ref = shard.packed_host_tensors(kind, weights.synthetic_state_dict(kind, seed=0))
+        ok &= len(mine) == len(ref) and all(torch.equal(a, b) for a, b in zip(mine, ref))
+    lo, hi = shard.shard_range(total, world, rank)
+    K, T = 4, 5
+    if hi > lo:
+        out = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in _shard_reference(lo, hi, K, T).items()}
+    else:
+        out = {"pred_pose": torch.zeros(0, K, 9), "pts_feat": torch.zeros(0, 1024), "energy": torch.zeros(0, K, 2),
+               "aggregated": torch.zeros(0, 4, 4)}
+    out["length"] = None
+    g = shard.gather_outputs(out, total)                 # on every rank
+    g0 = shard.gather_outputs(out, total, dst=0)         # on rank 0 only
+    ok &= (g0 is None) == (rank != 0) and g["length"] is None
+    if rank == 0:
+        for k in ("pred_pose", "pts_feat", "energy", "aggregated"):
+            np.save(os.path.join(out_dir, f"{k}.npy"), g[k].numpy())
+            ok &= torch.equal(g[k], g0[k])
     np.save(os.path.join(out_dir, f"ok_{rank}.npy"), np.array(ok))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_world2_shards_equal_single_process(tmp_path):
+@pytest.mark.parametrize("world,total", [(2, 5), (3, 2)])
+def test_gloo_sharded_broadcast_and_gather(tmp_path, world, total):
+    """world_size 2 and 3 (gloo): broadcast of every agent's packed buffers, per-rank shards (uneven,
+    and an empty shard when ranks outnumber objects), gather of the per-object outputs in object
+    order on every rank and on rank 0 -- equal to the per-shard computations concatenated."""
     import torch.multiprocessing as mp
-    from genpose2_amd import synthetic, weights
-    from oracle import oracle
-    port = 29500 + os.getpid() % 1000
-    mp.spawn(_gloo_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    assert all(np.load(tmp_path / f"ok_{r}.npy") for r in range(2))
-    sharded = np.concatenate([np.load(tmp_path / f"feat_{r}.npy") for r in range(2)])
-    pts, _ = synthetic.make_batch(4, 6, 1024)
-    full = oracle.encoder_forward(weights.synthetic_state_dict("score"), pts)
-    np.testing.assert_array_equal(sharded, full)
+    from genpose2_amd import shard
+    port = 29500 + (os.getpid() + world) % 1000
+    mp.spawn(_gloo_worker, args=(world, port, str(tmp_path), total), nprocs=world, join=True)
+    assert all(np.load(tmp_path / f"ok_{r}.npy") for r in range(world))
+    parts = [_shard_reference(*shard.shard_range(total, world, r), 4, 5) for r in range(world)
+             if shard.shard_range(total, world, r)[1] > shard.shard_range(total, world, r)[0]]
+    for k in ("pred_pose", "pts_feat", "energy", "aggregated"):
+        np.testing.assert_array_equal(np.load(tmp_path / f"{k}.npy"), np.concatenate([p[k] for p in parts]))
+
+
+@pytest.mark.parametrize("t_eval", [None, 40])
+def test_rk45_controller_failed_solve_matches_scipy(t_eval):
+    """A solve that fails ("required step size is less than spacing between numbers", status -1):
+    y' = -y^2 has the solution 1/(t - 0.3), singular inside (1e-5, 0.55). The controller stops where
+    solve_ivp stops, with the same nfev, times and collected outputs (the t_eval points before the
+    failure), which is what cond_ode_sampler's res.y[:, -1] then reads."""
+    import warnings
+    from scipy.integrate import solve_ivp
+    from genpose2_amd.ode import NumpyRk45, rk45_drive
+
+    def f_np(t, y):
+        return -y * y
+
+    y0 = np.array([1.0 / (0.55 - 0.3), 2.0 / (0.55 - 0.3)])
+    te = None if t_eval is None else np.linspace(0.55, 1e-5, t_eval)
+    ref = solve_ivp(f_np, (0.55, 1e-5), y0, method="RK45", rtol=1e-5, atol=1e-5, t_eval=te)
+    assert ref.status == -1
+    be = NumpyRk45(f_np, y0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        ts, nfev, status = rk45_drive(be, 0.55, 1e-5, t_eval=te)
+    assert status == -1 and nfev == ref.nfev
+    np.testing.assert_array_equal(ts, ref.t)
+    ys = np.stack(be.ys, 1) if te is None else np.stack([v for _, v in be.dense_rows], 1)
+    np.testing.assert_array_equal(ys, ref.y)
+
+
+@pytest.mark.parametrize("kind", ["score", "energy", "scale"])
+def test_manifest_matches_reference_checkpoint_layout(kind):
+    """The weight manifest (keys, shapes, dtypes) equals the model_state_dict the reference's own
+    save_ckpt writes (golden_ckpt_layout.json, generated by make_golden.py ckpt)."""
+    import json
+    from conftest import GOLDEN
+    from genpose2_amd import weights
+    with open(os.path.join(GOLDEN, "golden_ckpt_layout.json")) as f:
+        lay = json.load(f)[kind]
+    assert lay["top_level_keys"] == ["clock", "model_state_dict", "optimizer_state_dict", "scheduler_state_dict"]
+    sd = weights.synthetic_state_dict(kind)
+    assert sorted(sd) == sorted(lay["model_state_dict"])
+    for k, (shape, dt) in lay["model_state_dict"].items():
+        assert list(sd[k].shape) == shape and str(sd[k].dtype) == dt, k
+
+
+@pytest.mark.parametrize("prefix", ["", "module."])
+def test_load_checkpoint_reference_format(tmp_path, prefix):
+    """weights.load_checkpoint (PoseNet.load_ckpt's loader) reads a save_ckpt-format file with
+    torch.load(weights_only=True), strips DataParallel's "module." prefix, and packs to exactly the
+    buffers the synthetic weights pack to; a missing file raises ValueError like the reference."""
+    from conftest import write_reference_checkpoint
+    from genpose2_amd import pack, weights
+    for kind in ("score", "scale"):
+        path = write_reference_checkpoint(str(tmp_path / f"{kind}.pth"), kind, prefix=prefix)
+        sd = weights.load_checkpoint(path)
+        weights.check_keys(sd, kind)
+        ref = weights.synthetic_state_dict(kind)
+        for k in ref:
+            np.testing.assert_array_equal(sd[k], ref[k])
+        if kind == "score":
+            a, b = pack.pack_heads(sd), pack.pack_heads(ref)
+            assert all(np.array_equal(a[k], b[k]) for k in a)
+            np.testing.assert_array_equal(pack.pack_encoder(sd)[0], pack.pack_encoder(ref)[0])
+    with pytest.raises(ValueError):
+        weights.load_checkpoint(str(tmp_path / "missing.pth"))

@@ -133,3 +133,28 @@ def test_stage_glue_oracle_restatements():
     ref_len, _ = torch.max(torch.abs(p), dim=1)
     ref_len *= 2
     np.testing.assert_allclose(oracle.bbox_length(pcl, pose), ref_len.numpy(), rtol=2e-6, atol=1e-7)
+
+
+# ---------------------------------------------------------------- large-row fixtures (> 4096 rows)
+def test_pc_large_rows_calibrated(score_sd):
+    """R = 4800 (B=96, K=50), T=100: the oracle (another fp32 rounding of the same sampler) is held to
+    the reference's own fp32-vs-float64 error budget (tests/golden/large_noise.py)."""
+    import large_noise
+    g = golden("large_pc_r4800_t100")
+    _, _, B, K, T, _, _ = large_noise.CASES["pc_r4800_t100"]
+    pts, center, prior, z1, z2 = large_noise.inputs("pc_r4800_t100")
+    pose, q, _, _ = oracle.pred_func(score_sd, pts, center, K, T, "pc", prior, z1, z2)
+    large_noise.check_pc_calibrated(pose, g)
+    assert rel(pose[..., 6:], g["pred_pose"][..., 6:]) < 1e-5
+
+
+def test_ode_large_rows(score_sd):
+    """R = 4800, the shipped ODE setting (T0=0.55, RK45): identical nfev, 1e-4 / 1e-5."""
+    import large_noise
+    g = golden("large_ode_r4800")
+    _, _, B, K, _, T0, _ = large_noise.CASES["ode_r4800"]
+    pts, center, prior, _, _ = large_noise.inputs("ode_r4800")
+    pose, q, _, ex = oracle.pred_func(score_sd, pts, center, K, None, "ode", prior, T0=T0)
+    assert ex["nfev"] == int(g["nfev"])
+    assert np.abs(pose[..., :6] - g["pred_pose"][..., :6]).max() < 1e-4
+    assert rel(pose[..., 6:], g["pred_pose"][..., 6:]) < 1e-5
