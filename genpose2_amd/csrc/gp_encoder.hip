@@ -19,6 +19,7 @@
 
 #include "gp_common.h"
 #include "gp_fps.h"
+#include "gp_head.h"   // split-f16 helpers: mfma_h, split_pair, stream_hk_step, rows_max, exp2i, ilog2f
 
 int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const int* m, int* const* idx,
                         float* const* nxyz, hipStream_t st);
@@ -359,6 +360,262 @@ __global__ __launch_bounds__(SA_THREADS, 2) void sa_pair_kernel(SAArgs a0, SAArg
     }
 }
 
+// ============================================================================ split-f16 levels (2, 3)
+// Layers 1 and 2 of a level as split-f16 MFMA GEMMs (v_mfma_f32_16x16x32_f16, three products of
+// hi/lo planes with fp32 accumulation, as the head trunk): per 32-deep chunk w_lo*a_hi + w_hi*a_lo
+// + w_hi*a_hi, ~22 significant bits per operand. The activation planes take a per-COLUMN power-of-two
+// scale from the column's actual maximum (a column is one grouped neighbour: its scale multiplies
+// out of every output of that column), so the split keeps ~22 bits wherever the values lie:
+//   * layer 0 (relu(Q[nbr] - W0_xyz . x_c), the per-point projection) is gathered by waves 0..CT-1,
+//     one 16-column tile each; the lane's values and a 4-lane max give the column maximum directly;
+//   * layer 1's outputs are spread over the waves by output chunk: every wave publishes its partial
+//     column maxima in LDS before the barrier that retires the reads of layer 0's planes, then
+//     writes its chunks' planes over them (one activation buffer, no extra barrier).
+// Weights carry a per-layer exponent (pack.pack_encoder). Wave w owns output chunks w, w+8, ...: the
+// two waves sharing a SIMD (w, w+4) split a level-3 branch-1 layer 1's 12 chunks 2 + 1.
+// 64 columns per workgroup: every weight fragment streamed from L2 feeds 4 column tiles x 3 MFMAs.
+constexpr int SPLIT_WV = 8;
+
+struct SplitArgs {
+    int n_prev, m, ns, cols;          // cols = m * ns, a multiple of the workgroup's 16*CT columns
+    const float* qin;                 // layer-0 projection Q (B, n_prev, q_stride), pre-activation
+    int q_stride, q_off;
+    const float* w0;                  // packed fp32 layer 0 (its xyz k-group gives W0_xyz)
+    int kg0, gx;
+    const int* nbr;                   // (B, m, ns)
+    const float* cent;                // (B, m, 3)
+    const float* w[2];                // split planes of layers 1, 2 (pack_h16_fragments)
+    const float* bias[2];             // padded to 32
+    int ew[2];                        // weight exponents
+    float* out;                       // (B, m, c_out_total)
+    int c_out_total, out_off;
+};
+
+__device__ __forceinline__ float max4(f32x4 v) { return fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)); }
+
+// Column exponent: E with the column maximum in [2^E, 2^(E+1)); all-zero columns get E = -100.
+__device__ __forceinline__ int col_exponent(float m) { return m > 1e-30f ? ilog2f(m) : -100; }
+
+// Layer-0 planes of column tile ct: lane (q, n) gathers column n's channels 32c + 4q + j and
+// 32c + 16 + 4q + j (j < 4) of every chunk c -- exactly its B fragments.
+template <int CT, int KC0>
+__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, const f32x4* w0x, int b,
+                                              int col0, int ct, int lane) {
+#pragma clang fp contract(off)
+    const int q = lane >> 4, n = lane & 15;
+    const int col = ct * 16 + n, g = col0 + col;
+    const int m = g / a.ns, s = g - (g / a.ns) * a.ns;
+    const int p = a.nbr[((size_t)b * a.m + m) * a.ns + s];
+    const float* cc = a.cent + ((size_t)b * a.m + m) * 3;
+    const float cx = cc[0], cy = cc[1], cz = cc[2];
+    const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
+    f32x4 v[KC0][2];
+#pragma unroll
+    for (int c = 0; c < KC0; ++c) {
+        v[c][0] = ld4(qrow + 32 * c);
+        v[c][1] = ld4(qrow + 32 * c + 16);
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < KC0; ++c)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float r[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const f32x4 w = w0x[32 * c + 16 * h + 4 * q + j];
+                r[j] = fmaxf(v[c][h][j] - ((w.x * cx + w.y * cy) + w.z * cz), 0.f);
+                mx = fmaxf(mx, r[j]);
+            }
+            v[c][h] = f32x4{r[0], r[1], r[2], r[3]};
+        }
+    const int E = col_exponent(rows_max(mx));
+    const float sc = exp2i(14 - E);
+#pragma unroll
+    for (int c = 0; c < KC0; ++c) {
+        f16x8 hi, lo;
+        split_pair(v[c][0], v[c][1], sc, hi, lo);
+        X[((c * CT + ct) * 2 + 0) * 64 + lane] = hi;
+        X[((c * CT + ct) * 2 + 1) * 64 + lane] = lo;
+    }
+    if (q == 0) e0s[col] = E;
+}
+
+// Layer 1 for this wave's NC output chunks (wid, wid + 8, ...): primes its weight ring, gathers layer
+// 0 (waves < CT), streams, and leaves the planes of its outputs in X (over layer 0's) plus every
+// column's exponent in e1[ct] (for lane column n). Executes the same two barriers in every wave.
+template <int CT, int KC0, int NC, int D>
+__device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* w0x,
+                                             int b, int col0, int wid, int lane, int oc1, int (&e1)[CT]) {
+    constexpr int C = 16 * CT;
+    const int q = lane >> 4, n = lane & 15;
+    float pmax[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) pmax[ct] = 0.f;
+    if constexpr (NC == 0) {
+        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, col0, wid, lane);
+        __syncthreads();
+        if (q == 0)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) pm[wid * C + ct * 16 + n] = 0.f;
+        __syncthreads();
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            float M = 0.f;
+#pragma unroll
+            for (int w = 0; w < SPLIT_WV; ++w) M = fmaxf(M, pm[w * C + ct * 16 + n]);
+            e1[ct] = col_exponent(M);
+        }
+    } else {
+        int T[2 * NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            T[2 * i] = 2 * (wid + SPLIT_WV * i);
+            T[2 * i + 1] = T[2 * i] + 1;
+        }
+        const __amdgpu_buffer_rsrc_t W = make_rsrc(a.w[0], (uint32_t)(2 * oc1) * KC0 * 2048u);
+        const int voff = lane * 16;
+        f16x8 ring[D + 1][2 * NC][2];
+        f32x4 acc[2 * NC][CT];
+#pragma unroll
+        for (int t = 0; t < 2 * NC; ++t)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        stream_hk_step<KC0, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
+        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, col0, wid, lane);
+        __syncthreads();
+        stream_hk_step<KC0, D, KC0 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
+        // unscale (exact powers of two), bias, ReLU, partial column maxima
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const float u = exp2i(e0s[ct * 16 + n] - 14 - a.ew[0]);
+#pragma unroll
+            for (int t = 0; t < 2 * NC; ++t) {
+                acc[t][ct] = relu4(acc[t][ct] * u + ld4(a.bias[0] + 16 * T[t] + 4 * q));
+                pmax[ct] = fmaxf(pmax[ct], max4(acc[t][ct]));
+            }
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const float M = rows_max(pmax[ct]);
+            if (q == 0) pm[wid * C + ct * 16 + n] = M;
+        }
+        __syncthreads();   // every read of layer 0's planes is done; the partial maxima are visible
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            float M = 0.f;
+#pragma unroll
+            for (int w = 0; w < SPLIT_WV; ++w) M = fmaxf(M, pm[w * C + ct * 16 + n]);
+            e1[ct] = col_exponent(M);
+            const float sc = exp2i(14 - e1[ct]);
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                const int oc = wid + SPLIT_WV * i;
+                f16x8 hi, lo;
+                split_pair(acc[2 * i][ct], acc[2 * i + 1][ct], sc, hi, lo);
+                X[((oc * CT + ct) * 2 + 0) * 64 + lane] = hi;
+                X[((oc * CT + ct) * 2 + 1) * 64 + lane] = lo;
+            }
+        }
+    }
+}
+
+// Layer 2 for this wave's NC output chunks, ReLU, and the max over each centroid's ns columns
+// (ns = 16: one column tile, 32: two) written to the level's point-major output.
+template <int CT, int KC1, int NC, int D>
+__device__ __forceinline__ void split_layer2(const SplitArgs& a, const f16x8* X, const int (&e1)[CT], int b,
+                                             int col0, int wid, int lane, int oc2) {
+    static_assert(NC >= 1, "every wave owns a layer-2 chunk");
+    const int q = lane >> 4, n = lane & 15;
+    int T[2 * NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+        T[2 * i] = 2 * (wid + SPLIT_WV * i);
+        T[2 * i + 1] = T[2 * i] + 1;
+    }
+    const __amdgpu_buffer_rsrc_t W = make_rsrc(a.w[1], (uint32_t)(2 * oc2) * KC1 * 2048u);
+    const int voff = lane * 16;
+    f16x8 ring[D + 1][2 * NC][2];
+    f32x4 acc[2 * NC][CT];
+#pragma unroll
+    for (int t = 0; t < 2 * NC; ++t)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    stream_hk_step<KC1, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
+    __syncthreads();   // layer 1's planes are complete
+    stream_hk_step<KC1, D, KC1 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
+    const int span = a.ns >> 4;   // column tiles per centroid (1 or 2)
+#pragma unroll
+    for (int t = 0; t < 2 * NC; ++t) {
+        const f32x4 bias = ld4(a.bias[1] + 16 * T[t] + 4 * q);
+        f32x4 v[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) v[ct] = relu4(acc[t][ct] * exp2i(e1[ct] - 14 - a.ew[1]) + bias);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            if (span == 2) {
+                if (ct & 1) continue;
+                v[ct] = f32x4{fmaxf(v[ct].x, v[ct + 1].x), fmaxf(v[ct].y, v[ct + 1].y), fmaxf(v[ct].z, v[ct + 1].z),
+                              fmaxf(v[ct].w, v[ct + 1].w)};
+            }
+            f32x4 r = v[ct];
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) {
+                r.x = fmaxf(r.x, __shfl_xor(r.x, off, 64));
+                r.y = fmaxf(r.y, __shfl_xor(r.y, off, 64));
+                r.z = fmaxf(r.z, __shfl_xor(r.z, off, 64));
+                r.w = fmaxf(r.w, __shfl_xor(r.w, off, 64));
+            }
+            if (n == 0) {
+                const int mi = (col0 + ct * 16) / a.ns;
+                st4(a.out + ((size_t)b * a.m + mi) * a.c_out_total + a.out_off + 16 * T[t] + 4 * q, r);
+            }
+        }
+    }
+}
+
+template <int CT, int KC0, int OC1, int OC2>
+__device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
+    constexpr int C = 16 * CT, KX = KC0 > OC1 ? KC0 : OC1, D = 2;
+    f16x8* X = reinterpret_cast<f16x8*>(smem);                       // [chunk][ct][plane][lane]
+    f32x4* w0x = reinterpret_cast<f32x4*>(smem + (size_t)KX * CT * 2048);   // (wx, wy, wz, 0) per channel
+    float* pm = reinterpret_cast<float*>(w0x + KC0 * 32);           // [wave][column] partial maxima
+    int* e0s = reinterpret_cast<int*>(pm + SPLIT_WV * C);           // layer-0 column exponents
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = blockIdx.y, col0 = blockIdx.x * C;
+    for (int ch = tid; ch < KC0 * 32; ch += SPLIT_WV * 64)   // packed layer-0 fragment of channel ch, q = 0
+        w0x[ch] = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
+    __syncthreads();
+    int e1[CT];
+    // layer-1 output chunks of this wave: wid, wid + 8, ... below OC1
+    constexpr int NC1_HI = (OC1 + SPLIT_WV - 1) / SPLIT_WV;
+    const int nc1 = wid < OC1 % SPLIT_WV || OC1 % SPLIT_WV == 0 ? NC1_HI : NC1_HI - 1;
+    if (nc1 == NC1_HI)
+        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1);
+    else
+        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1);
+    static_assert(OC2 % SPLIT_WV == 0, "layer-2 chunks spread evenly over the waves");
+    split_layer2<CT, OC1, OC2 / SPLIT_WV, D>(a, X, e1, b, col0, wid, lane, OC2);
+}
+
+// Both branches of a level per launch (blockIdx.z = branch).
+template <int CT, int KC0, int OC1A, int OC2A, int OC1B, int OC2B>
+__global__ __launch_bounds__(SPLIT_WV * 64) void sa_split_kernel(SplitArgs a0, SplitArgs a1) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (blockIdx.z == 0) {
+        if ((int)blockIdx.x * 16 * CT < a0.cols) sa_split_body<CT, KC0, OC1A, OC2A>(a0, smem);
+    } else {
+        if ((int)blockIdx.x * 16 * CT < a1.cols) sa_split_body<CT, KC0, OC1B, OC2B>(a1, smem);
+    }
+}
+
+template <int CT, int KC0, int OC1>
+static size_t sa_split_lds() {
+    constexpr int KX = KC0 > OC1 ? KC0 : OC1;
+    return (size_t)KX * CT * 2048 + (size_t)KC0 * 32 * 16 + sizeof(float) * SPLIT_WV * 16 * CT + sizeof(int) * 16 * CT;
+}
+
 // ============================================================================ narrow levels
 // Levels 0 and 1 (layers <= 128 wide): every wave owns whole centroids and runs layer 1, layer 2
 // and the max-pool for them entirely in registers -- the accumulator of one layer is the next
@@ -641,6 +898,10 @@ static int launch_pair(SAArgs a0, SAArgs a1, int B, hipStream_t st) {
     return GP_ERR_UNSUPPORTED;
 }
 
+// Row of the packed-layer table (pack.pack_encoder, [5][2][3][4]): {fp32 fragments, bias, split
+// planes or -1, split exponent}.
+static inline const int64_t* enc_layer(const int64_t* tab, int l, int br, int i) { return tab + ((l * 2 + br) * 3 + i) * 4; }
+
 extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N,
                                   void* workspace, size_t workspace_bytes, float* feat, hipStream_t st) {
     GP_REQUIRE(wbuf && layer_off && pts && workspace && feat, "encoder_forward: null pointer");
@@ -689,7 +950,7 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                 pa.xyz_prev = xyz_prev;
                 pa.feat_prev = l == 0 ? nullptr : reinterpret_cast<const float*>(ws + L.feat[l - 1]);
                 pa.nlayers = 1;
-                const int64_t* o = layer_off + ((l * 2 + br) * 3 + 0) * 2;
+                const int64_t* o = enc_layer(layer_off, l, br, 0);
                 GP_REQUIRE(o[0] >= 0 && o[1] >= 0, "encoder_forward: missing layer %d/%d/0", l, br);
                 pa.w[0] = wbuf + o[0];
                 pa.bias[0] = wbuf + o[1];
@@ -720,9 +981,9 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
                 n.q_off = q_off;
                 q_off += pad16(kWidths[l][br][1]);
                 n.n_prev = n_prev;
-                const int64_t* o0 = layer_off + ((l * 2 + br) * 3 + 0) * 2;
-                const int64_t* o1 = layer_off + ((l * 2 + br) * 3 + 1) * 2;
-                const int64_t* o2 = layer_off + ((l * 2 + br) * 3 + 2) * 2;
+                const int64_t* o0 = enc_layer(layer_off, l, br, 0);
+                const int64_t* o1 = enc_layer(layer_off, l, br, 1);
+                const int64_t* o2 = enc_layer(layer_off, l, br, 2);
                 GP_REQUIRE(o1[0] >= 0 && o2[0] >= 0, "encoder_forward: missing layers of %d/%d", l, br);
                 n.w0 = wbuf + o0[0];
                 n.c_out_total = kCout[l];
@@ -770,6 +1031,54 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
             if (rc) return rc;
             continue;
         }
+        // levels 2-3: split-f16 kernel when the table carries the planes (pack.pack_encoder)
+        if ((l == 2 || l == 3) && enc_layer(layer_off, l, 0, 1)[2] >= 0 && enc_layer(layer_off, l, 0, 2)[2] >= 0 &&
+            enc_layer(layer_off, l, 1, 1)[2] >= 0 && enc_layer(layer_off, l, 1, 2)[2] >= 0) {
+            constexpr int CT = 4;
+            SplitArgs sp[2];
+            int off_out = 0;
+            for (int br = 0; br < 2; ++br) {
+                SplitArgs& a = sp[br];
+                a = {};
+                a.n_prev = n_prev;
+                a.m = kNpoint[l];
+                a.ns = kNs[br];
+                a.cols = a.m * a.ns;
+                a.qin = qbuf;
+                a.q_stride = proj_stride(l);
+                a.q_off = br == 0 ? 0 : pad16(kWidths[l][0][1]);
+                const int64_t* o0 = enc_layer(layer_off, l, br, 0);
+                const int c_prev = kCout[l - 1];
+                a.w0 = wbuf + o0[0];
+                a.kg0 = (c_prev + 16) / 16;
+                a.gx = c_prev / 16;
+                a.nbr = br == 0 ? b0 : b1;
+                a.cent = nxyz[l];
+                for (int i = 0; i < 2; ++i) {
+                    const int64_t* o = enc_layer(layer_off, l, br, i + 1);
+                    a.w[i] = wbuf + o[2];
+                    a.bias[i] = wbuf + o[1];
+                    a.ew[i] = (int)o[3];
+                }
+                a.out = out;
+                a.c_out_total = kCout[l];
+                a.out_off = off_out;
+                off_out += kWidths[l][br][3];
+                GP_REQUIRE(a.cols % (16 * CT) == 0 && (16 * CT) % a.ns == 0,
+                           "encoder_forward: level %d columns %d do not tile by %d", l, a.cols, 16 * CT);
+            }
+            const dim3 grid(std::max(sp[0].cols, sp[1].cols) / (16 * CT), B, 2), blk(SPLIT_WV * 64);
+            if (l == 2) {
+                const size_t lds = sa_split_lds<CT, 4, 7>();
+                hipLaunchKernelGGL((sa_split_kernel<CT, 4, 7, 8, 7, 8>), grid, blk, lds, st, sp[0], sp[1]);
+            } else {
+                const size_t lds = std::max(sa_split_lds<CT, 8, 8>(), sa_split_lds<CT, 8, 12>());
+                hipLaunchKernelGGL((sa_split_kernel<CT, 8, 8, 16, 12, 16>), grid, blk, lds, st, sp[0], sp[1]);
+            }
+            rc = gp_check_launch("sa_split_kernel");
+            if (rc) return rc;
+            continue;
+        }
         int out_off = 0;
         SAArgs sa[2];
         for (int br = 0; br < 2; ++br) {
@@ -786,7 +1095,7 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
             a.nbr = l < 4 ? (br == 0 ? b0 : b1) : nullptr;
             a.nlayers = l < 4 ? 3 : 2;
             for (int i = 0; i < a.nlayers; ++i) {
-                const int64_t* o = layer_off + ((l * 2 + br) * 3 + i) * 2;
+                const int64_t* o = enc_layer(layer_off, l, br, i);
                 GP_REQUIRE(o[0] >= 0 && o[1] >= 0, "encoder_forward: missing layer %d/%d/%d", l, br, i);
                 a.w[i] = wbuf + o[0];
                 a.bias[i] = wbuf + o[1];

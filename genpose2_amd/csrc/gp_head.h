@@ -34,9 +34,12 @@ constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
 // NT = column tiles (16 candidates each) per workgroup.
 template <int NT, int WV>
 struct HeadSmem {
+    // 64-candidate tiles (NT = 4) alias pose_encoder.2's output onto pose_encoder.0's (written after
+    // a barrier that retires every read of act1), so one workgroup still fits the 160 KiB of a CU
+    static constexpr bool kAliasAct = NT >= 4;
     float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
     f32x4 act1[KG_HID * NT * 64];      // pose_encoder.0 output, accumulator-native [g][ct][lane]
-    f32x4 act2[KG_HID * NT * 64];      // pose_encoder.2 output
+    f32x4 act2[kAliasAct ? 4 : KG_HID * NT * 64];   // pose_encoder.2 output (act1 when aliased)
     float red[NT * 16][9][WV];         // per-wave head-layer-2 partials, wave-minor (head_out reads a row)
     float xu[NT * 16 * 9];             // PC: last-step mean rows, gathered for the quaternion
     float scratch[WV * 64];
@@ -137,6 +140,7 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
                            const float* __restrict__ tproj, const int* obj_of_col, HeadSmem<NT, WV>& sm,
                            int trace_slot = 0) {
     constexpr int TPW = 16 / WV;   // output tiles per wave and per 256-wide layer
+    static_assert(!HeadSmem<NT, WV>::kAliasAct, "the exact-fp32 trunk keeps separate activation buffers");
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
     const int q = lane >> 4, n = lane & 15;
@@ -299,19 +303,20 @@ __device__ __forceinline__ void split_pair(f32x4 u, f32x4 v, float s, f16x8& hi,
     }
 }
 
-// stream_step on f16 planes: ring slot = [tile][hi, lo] of one 32-deep chunk (2 x 1 KiB per tile);
-// B = activation planes in LDS, [chunk][ct][hi, lo][lane].
-template <int G, int GEND, int TT, int NT, int D>
-__device__ __forceinline__ void stream_h_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
-                                              int lane, int voff, f16x8 (&ring)[D + 1][TT][2], f32x4 (&acc)[TT][NT]) {
+// stream_step on f16 planes over KC 32-deep chunks: ring slot = [tile][hi, lo] of one chunk (2 x 1 KiB
+// per tile, weights packed by pack.pack_h16_fragments as [T][chunk][plane][lane]); B = activation
+// planes in LDS, [chunk][ct][hi, lo][lane].
+template <int KC, int G, int GEND, int TT, int NT, int D>
+__device__ __forceinline__ void stream_hk_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
+                                               int lane, int voff, f16x8 (&ring)[D + 1][TT][2], f32x4 (&acc)[TT][NT]) {
     if constexpr (G < GEND) {
-        if constexpr (G < KC_HID) {
+        if constexpr (G < KC) {
 #pragma unroll
             for (int t = 0; t < TT; ++t)
 #pragma unroll
                 for (int p = 0; p < 2; ++p)
                     ring[G % (D + 1)][t][p] =
-                        __builtin_bit_cast(f16x8, ldbuf4(W, voff, ((T[t] * KC_HID + G) * 2 + p) * 1024));
+                        __builtin_bit_cast(f16x8, ldbuf4(W, voff, ((T[t] * KC + G) * 2 + p) * 1024));
         }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (G >= D) {
@@ -335,8 +340,15 @@ __device__ __forceinline__ void stream_h_step(__amdgpu_buffer_rsrc_t W, const in
 #pragma unroll
                 for (int ct = 0; ct < NT; ++ct) acc[t][ct] = mfma_h(ring[S][t][0], bh[ct], acc[t][ct]);
         }
-        stream_h_step<G + 1, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc);
+        stream_hk_step<KC, G + 1, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc);
     }
+}
+
+// The 256-deep layers of the head trunk.
+template <int G, int GEND, int TT, int NT, int D>
+__device__ __forceinline__ void stream_h_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
+                                              int lane, int voff, f16x8 (&ring)[D + 1][TT][2], f32x4 (&acc)[TT][NT]) {
+    stream_hk_step<KC_HID, G, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc);
 }
 
 // head_trunk with the split-f16 GEMMs (same contract and phases; pose_encoder.0 and layer 2 stay fp32).
@@ -354,7 +366,7 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     const __amdgpu_buffer_rsrc_t W2 = make_rsrc(w.pe2_h, HID * HID * 4);
     const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_h, 3 * HID * HID * 4);
     f16x8* act1h = reinterpret_cast<f16x8*>(sm.act1);   // same 16 KiB per column tile as fp32
-    f16x8* act2h = reinterpret_cast<f16x8*>(sm.act2);
+    f16x8* act2h = reinterpret_cast<f16x8*>(HeadSmem<NT, WV>::kAliasAct ? sm.act1 : sm.act2);
     constexpr int D2 = NT > 1 ? PC_NT2_D2H : PC_D2H, DH = NT > 1 ? PC_NT2_DH : HEAD_PREFETCH_H;
     int T2[TPW], TH[3 * TPW];
 #pragma unroll
@@ -428,6 +440,7 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
         for (int ct = 0; ct < NT; ++ct) acc[i][ct] = (pov[i][ct] + tpv[i]) * sh[ct];
     f16x8 ringh[DH + 1][3 * TPW][2];
     stream_h_step<0, DH, 3 * TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc);
+    if constexpr (HeadSmem<NT, WV>::kAliasAct) __syncthreads();   // act2 overwrites act1: all reads done
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
         const int Ta = T2[2 * c];

@@ -171,12 +171,13 @@ struct PCArgs {
 };
 
 // Launch i in [0, steps]: finish step i-1 (if i > 0), then score at step i (if i < steps).
-// Wave 0 runs the update (its global loads, the draws and the grad-norm reduction overlap) while
-// the other waves stage the small weights and issue their first weight-stream loads; one barrier
-// (inside head_trunk) joins them.
+// Waves 0..NT-1 run the update, one 16-row column tile each (their global loads, the draws and the
+// grad-norm reduction overlap), while the other waves make the next step's draws, stage the small
+// weights and issue their first weight-stream loads; one barrier (inside the trunk) joins them.
 template <int NT, int WV, bool SPLIT>
 __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
     constexpr int ROWS = NT * 16;
+    static_assert(NT < WV, "at least one wave besides the update waves");
     __shared__ HeadSmem<NT, WV> sm;
     __shared__ int obj[ROWS];
     const int tid = threadIdx.x;
@@ -185,12 +186,13 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     const int r0 = blockIdx.x * ROWS;
     const int trace_slot = i & 1;
     PC_MARK(0);
-    if (wid == 0) {
+    if (wid < NT) {
         // ---- every load first and unconditional (rows clamped: a guarded load becomes a branch,
         //      and the compiler then drains the first batch before issuing the next): the
         //      grad-norm partials of step i-1, then this lane's elements of x, s and the two draws.
         //      Four lanes per row: part p < 3 owns elements [3p, 3p+3) (rot6 columns a1, a2,
-        //      translation); lane 4c+3 only pads the row.
+        //      translation); lane 4c+3 only pads the row. Wave g owns rows 16g .. 16g+15.
+        const int g = wid;
         const bool inj = a.z1 != nullptr;
         const float* zslot = a.zbuf + (size_t)((i - 1) & 1) * 2 * a.rows * 9;
         const float* z1p = inj ? a.z1 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : zslot;
@@ -201,20 +203,20 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
         for (int u = 0; u < 8; ++u) pv[u] = part[min(lane + 64 * u, a.nwg - 1)];
         const int p = lane & 3;
         const int e0 = 3 * (p < 3 ? p : 0);
-        float xv[NT][3], sv[NT][3], z1v[NT][3], z2v[NT][3];
-#pragma unroll
-        for (int g = 0; g < NT; ++g) {
+        float x3[3], sv[3], z1v[3], z2v[3];
+        {
             const size_t e = (size_t)min(r0 + 16 * g + (lane >> 2), a.rows - 1) * 9 + e0;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                xv[g][k] = a.x[e + k];
-                sv[g][k] = a.s[e + k];
-                z1v[g][k] = z1p[e + k];
-                z2v[g][k] = z2p[e + k];
+                x3[k] = a.x[e + k];
+                sv[k] = a.s[e + k];
+                z1v[k] = z1p[e + k];
+                z2v[k] = z2p[e + k];
             }
         }
         // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); the same lane
-        // order and xor tree in every workgroup, so all derive the identical value (unused at i=0)
+        // order and xor tree in every wave of every workgroup, so all derive the identical value
+        // (unused at i=0)
         float gacc = 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u) gacc += lane + 64 * u < a.nwg ? pv[u] : 0.f;
@@ -225,19 +227,17 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             for (int u = 0; u < 8; ++u) gacc += t0 + lane + 64 * u < a.nwg ? pv[u] : 0.f;
         }
         PC_MARK(9);
-        if (lane < ROWS) {
-            const int r = r0 + lane;
-            obj[lane] = (r < a.rows ? r : a.rows - 1) / a.kper;
+        if (lane < 16) {
+            const int r = r0 + 16 * g + lane;
+            obj[16 * g + lane] = (r < a.rows ? r : a.rows - 1) / a.kper;
         }
         PC_MARK(10);
         gacc = wave_sum(gacc);
         PC_MARK(11);
-#pragma unroll
-        for (int g = 0; g < NT; ++g) {
+        {
 #pragma clang fp contract(off)
             const int c = 16 * g + (lane >> 2);
             const int r = r0 + c;
-            float* x3 = xv[g];
             const bool upd = i > 0 && r < a.rows && p < 3;
             if (upd) {
                 const float gn = udiv(gacc, (float)a.rows);
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
                 const float sq2ls = usqrt(2.0f * ls);
                 float mean[3];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) x3[k] = (x3[k] + ls * sv[g][k]) + sq2ls * z1v[g][k];
+                for (int k = 0; k < 3; ++k) x3[k] = (x3[k] + ls * sv[k]) + sq2ls * z1v[k];
                 if (p < 2) {   // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
                     const float nn = usqrt((x3[0] * x3[0] + x3[1] * x3[1]) + x3[2] * x3[2]);
                     x3[0] = udiv(x3[0], nn); x3[1] = udiv(x3[1], nn); x3[2] = udiv(x3[2], nn);
@@ -256,9 +256,9 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
                 const float gs = prev.g * prev.sqrt_dt;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    const float drift = 0.0f - g2 * sv[g][k];
+                    const float drift = 0.0f - g2 * sv[k];
                     mean[k] = x3[k] + drift * prev.dt;
-                    x3[k] = mean[k] + gs * z2v[g][k];
+                    x3[k] = mean[k] + gs * z2v[k];
                 }
                 gram_schmidt6_quad(x3, p, lane);
                 const float* cen = a.center + (size_t)(r / a.kper) * 3;
@@ -308,10 +308,10 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
         PC_MARK(12);
     }
     if (i == a.steps) return;  // finalize launch: no score evaluation
-    if (wid > 0 && a.z1 == nullptr) {
-        // draws for the update of step i (applied by launch i+1), made while wave 0 updates:
+    if (wid >= NT && a.z1 == nullptr) {
+        // draws for the update of step i (applied by launch i+1), made while waves 0..NT-1 update:
         // 2 streams x 3 blocks of 4 normals per row, streams 2i (corrector) and 2i+1 (predictor)
-        for (int e = tid - 64; e < ROWS * 6; e += (WV - 1) * 64) {
+        for (int e = tid - 64 * NT; e < ROWS * 6; e += (WV - NT) * 64) {
             const int c = e / 6, st = (e - c * 6) / 3, blk = e - c * 6 - st * 3;
             const int r = r0 + c;
             if (r < a.rows) {
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             }
         }
     }
-    stage_small_weights<NT, WV, 64>(a.w, sm);
+    stage_small_weights<NT, WV, 64 * NT>(a.w, sm);
     if constexpr (SPLIT)
         head_trunk_split<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
     else
@@ -390,13 +390,19 @@ extern "C" size_t gp_pc_workspace_size(int rows) {
 #ifndef PC_SPLIT_NT2_MIN
 #define PC_SPLIT_NT2_MIN 4097   // rows from which the split kernel takes 32-candidate tiles (> 256 tiles of 16)
 #endif
+#ifndef PC_SPLIT_NT4_MIN
+#define PC_SPLIT_NT4_MIN 8193   // ... and 64-candidate tiles (> 256 tiles of 32)
+#endif
 static int pc_pick_nt(int rows, bool split) {
     // exact fp32 (scripts/kbench.py): 16 candidates x 8 waves per workgroup beats 32 x 4 at every
     // size (R=25,600: 125 vs 153 us/step): 112 VGPRs leave room for two workgroups per CU, while
     // the 32-wide tile needs 373 registers (one wave per SIMD).
     // split-f16: each workgroup streams the 1 MB of GEMM weights once per step whatever its width,
     // so 32-candidate tiles halve the weight stream per candidate once there are enough tiles.
-    return split && rows >= PC_SPLIT_NT2_MIN ? 2 : 1;
+    // One workgroup per CU either way (the LDS of a 32- or 64-candidate tile), so the tile width is
+    // the smallest that keeps the launch within one pass of the 256 CUs, or the widest above that.
+    if (!split) return 1;
+    return rows >= PC_SPLIT_NT4_MIN ? 4 : (rows >= PC_SPLIT_NT2_MIN ? 2 : 1);
 }
 
 // Candidates per PC-step workgroup that gp_pc_sample picks for `rows` (split: head weights with
@@ -443,7 +449,9 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
                                     step_tab[5 * i + 4]};
         if (i > 0) prev = PCStep{step_tab[5 * (i - 1)], step_tab[5 * (i - 1) + 1], step_tab[5 * (i - 1) + 2],
                                  step_tab[5 * (i - 1) + 3], step_tab[5 * (i - 1) + 4]};
-        if (nt == 2 && split)
+        if (nt == 4)
+            hipLaunchKernelGGL((pc_step_kernel<4, PC_WV1, true>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+        else if (nt == 2 && split)
             hipLaunchKernelGGL((pc_step_kernel<2, PC_WV1, true>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else if (nt == 2)
             hipLaunchKernelGGL((pc_step_kernel<2, PC_WV2, false>), grid, dim3(PC_WV2 * 64), 0, stream, a, i, cur, prev);

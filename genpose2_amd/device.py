@@ -48,8 +48,20 @@ class EncoderModel:
         self.device = device
         buf, offs = pack.pack_encoder(sd)
         self.wbuf = torch.from_numpy(buf).to(device)
-        self.offsets = np.ascontiguousarray(offs.reshape(-1), np.int64)
+        self._table = np.ascontiguousarray(offs, np.int64)     # [5][2][3][4] (gp_encoder_forward)
         self._ws: Optional[torch.Tensor] = None
+        self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
+
+    def set_arith(self, arith: str) -> None:
+        """GEMM arithmetic of SA levels 2-3: "split_f16" (f16 hi/lo MFMA products with per-column
+        activation scaling, sa_split_kernel) or "f32" (exact fp32 MFMA)."""
+        if arith not in ("split_f16", "f32"):
+            raise ValueError(f"unknown encoder arithmetic {arith!r} (split_f16 | f32)")
+        t = self._table.copy()
+        if arith == "f32":
+            t[..., 2] = -1
+        self.arith = arith
+        self.offsets = np.ascontiguousarray(t.reshape(-1), np.int64)
 
     def workspace(self, b: int, n: int) -> torch.Tensor:
         need = int(self.lib.gp_encoder_workspace_size(b, n))

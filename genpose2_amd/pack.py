@@ -46,21 +46,34 @@ def pad_vec(b: np.ndarray, n: int) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- encoder
+ENC_SPLIT_LEVELS = (2, 3)   # levels whose layers 1-2 also get split-f16 planes (sa_split_kernel)
+
+
+def pad32(v: int) -> int:
+    return (v + 31) // 32 * 32
+
+
 def pack_encoder(sd: weights.StateDict) -> Tuple[np.ndarray, np.ndarray]:
-    """All SA layers, BN folded, into one flat float32 buffer + int64 offsets [5][2][3][2].
+    """All SA layers, BN folded, into one flat float32 buffer + int64 table [5][2][3][4]:
+    [0] offset of the fp32 A fragments, [1] offset of the bias (padded to 32), [2] offset of the
+    split-f16 planes (levels 2-3, layers 1-2; -1 elsewhere), [3] their power-of-two exponent.
 
     Layer 0 of each branch has its input channels permuted from the reference's
     [xyz(3) | feats(C)] (pointnet2_utils.py:287-289) to [feats(C) | xyz(3) | 0...] with
-    K padded to C + 16, matching the kernel's gathered B operand."""
+    K padded to C + 16, matching the kernel's gathered B operand. The split planes
+    (pack_h16_fragments) pad every output count and input depth to 32, the chunk of
+    v_mfma_f32_16x16x32_f16 (level 2: 196 channels -> 224)."""
     folded = weights.encoder_layers(sd)
     chunks: List[np.ndarray] = []
-    offsets = np.full((5, 2, 3, 2), -1, np.int64)
+    offsets = np.full((5, 2, 3, 4), -1, np.int64)
     pos = 0
 
     def add(a: np.ndarray) -> int:
         nonlocal pos
         o = pos
-        a = np.ascontiguousarray(a, np.float32).reshape(-1)
+        a = np.ascontiguousarray(a).reshape(-1)
+        if a.dtype != np.float32:
+            a = a.view(np.float32)     # int32 words of the f16 planes, stored bit for bit
         chunks.append(a)
         pos += a.size
         # keep every tensor 16-byte aligned
@@ -82,7 +95,13 @@ def pack_encoder(sd: weights.StateDict) -> Tuple[np.ndarray, np.ndarray]:
                 else:
                     packed = pack_a_fragments(W)
                 offsets[lv, br.branch, i, 0] = add(packed)
-                offsets[lv, br.branch, i, 1] = add(pad_vec(b, pad16(W.shape[0])))
+                offsets[lv, br.branch, i, 1] = add(pad_vec(b, pad32(W.shape[0])))
+                if lv in ENC_SPLIT_LEVELS and i >= 1:
+                    wq = np.zeros((pad32(W.shape[0]), pad32(W.shape[1])), np.float32)
+                    wq[:W.shape[0], :W.shape[1]] = W
+                    e = split_exponent(W)
+                    offsets[lv, br.branch, i, 2] = add(pack_h16_fragments(wq, e))
+                    offsets[lv, br.branch, i, 3] = e
     return np.concatenate(chunks), offsets
 
 

@@ -30,7 +30,7 @@ enum { GP_OK = 0, GP_ERR_INVALID = -1, GP_ERR_LAUNCH = -2, GP_ERR_UNSUPPORTED = 
 const char *gp_last_error(void);
 /* ABI version of this header. */
 int gp_abi_version(void);
-#define GP_ABI_VERSION 3
+#define GP_ABI_VERSION 4
 
 /* ===================================================================== operator level
  * Drop-in forward ops of `pointnet2_cuda` (same argument meaning and layouts). */
@@ -60,8 +60,11 @@ int gp_group_points(int b, int c, int n, int npoints, int nsample, const float *
 
 /* ===================================================================== fused encoder
  * Pointnet2ClsMSG(0) with the Light config (networks/pts_encoder/pointnet2.py:211-252).
- * `wbuf` holds all packed, BN-folded layers; `layer_off` (HOST, int64 [5][2][3][2]) gives the
- * float offsets of (weights, bias) of layer i of branch b of level l in `wbuf` (-1 = absent). */
+ * `wbuf` holds all packed, BN-folded layers; `layer_off` (HOST, int64 [5][2][3][4]) gives, for
+ * layer i of branch b of level l, {float offset of the fp32 A fragments, float offset of the bias
+ * (padded to 32), float offset of the split-f16 hi/lo planes or -1, their power-of-two exponent}
+ * (-1 = absent). Levels 2-3 run as split-f16 MFMA (per-column activation scaling) when all four of
+ * their layer-1/2 plane offsets are given, exact fp32 MFMA otherwise. ABI 4. */
 size_t gp_encoder_workspace_size(int b, int n);
 /* HOST out: byte offsets in the workspace of, per level l<4: fps idx (b,M_l) int32,
  * new_xyz (b,M_l,3) fp32, ball idx branch0/1 (b,M_l,ns) int32; and per level l<5 the level

@@ -44,8 +44,8 @@ def rotation_error_stats(pose: np.ndarray, ref: np.ndarray) -> dict:
     return {"max": float(e.max()), "p999": float(np.percentile(e, 99.9)), "mean": float(e.mean())}
 
 
-def check_pc_calibrated(pose: np.ndarray, g, factor: float = 2.0) -> dict:
-    """Parity bar of the large PC fixtures, calibrated on the reference itself.
+def check_calibrated(pose: np.ndarray, g, factor: float = 2.0) -> dict:
+    """Parity bar of the large fixtures, calibrated on the reference itself.
 
     At these sizes the reference's own fp32 trajectories differ from its float64 run by far more than
     the north-star 1e-4 (the untrained score net amplifies rounding along the trajectory; e.g. at
@@ -53,7 +53,8 @@ def check_pc_calibrated(pose: np.ndarray, g, factor: float = 2.0) -> dict:
     implementation can be held closer to the reference than the reference is to exact arithmetic, so
     the bar is: the implementation's error against the float64 reference run is within `factor` x
     the reference fp32's own error, in max, 99.9th percentile and mean over every rotation entry;
-    translations likewise in max absolute error."""
+    translations likewise in max absolute error. (ODE, T0=0.55: the reference's own fp32 error at
+    R=12,800 is 4.7e-5 max, so the bar there is 9.3e-5 -- inside the north-star 1e-4.)"""
     ref64 = g["pred_pose64"]
     ours = rotation_error_stats(pose, ref64)
     refs = rotation_error_stats(g["pred_pose"], ref64)
@@ -63,3 +64,6 @@ def check_pc_calibrated(pose: np.ndarray, g, factor: float = 2.0) -> dict:
         assert ours[k] <= factor * refs[k], (k, ours, refs)
     assert t_ours <= factor * t_ref, (t_ours, t_ref)
     return {"ours_vs_ref64": ours, "ref32_vs_ref64": refs, "trans_ours": t_ours, "trans_ref32": t_ref}
+
+
+check_pc_calibrated = check_calibrated

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     from genpose2_amd import _lib
     assert set(_lib.EXPORTED) == declared   # the ctypes binding covers exactly the header
     lib = _lib.load()
-    assert lib.gp_abi_version() == 3
+    assert lib.gp_abi_version() == 4
     assert lib.gp_encoder_workspace_size(64, 1024) > 0 and lib.gp_pc_workspace_size(3200) >= 3200 * 36
 
 
@@ -80,14 +80,29 @@ def test_split_f16_packing_layout_and_bounds(score_sd):
 
 
 def test_encoder_packing_covers_every_layer(score_sd):
-    from genpose2_amd import arch, pack
+    from genpose2_amd import arch, pack, weights
     buf, off = pack.pack_encoder(score_sd)
     for lv, brs in enumerate(arch.sa_branches()):
         for br in brs:
             n = len(br.widths) - 1
-            assert (off[lv, br.branch, :n] >= 0).all() and (off[lv, br.branch, n:] == -1).all()
-            assert (off[lv, br.branch, :n] % 4 == 0).all()    # 16-byte aligned
-    assert off.max() < buf.size
+            assert (off[lv, br.branch, :n, :2] >= 0).all() and (off[lv, br.branch, n:] == -1).all()
+            assert (off[lv, br.branch, :n, :2] % 4 == 0).all()    # 16-byte aligned
+            for i in range(n):   # split-f16 planes: levels 2-3, layers 1-2
+                has = lv in pack.ENC_SPLIT_LEVELS and i >= 1
+                assert (off[lv, br.branch, i, 2] >= 0) == has
+                if has:
+                    assert off[lv, br.branch, i, 2] % 4 == 0
+                    W, _ = weights.encoder_layers(score_sd)[lv][br.branch][i]
+                    e = int(off[lv, br.branch, i, 3])
+                    n_pad, k_pad = pack.pad32(W.shape[0]), pack.pad32(W.shape[1])
+                    words = buf[off[lv, br.branch, i, 2]:][: n_pad * k_pad].view(np.int32)
+                    pl = words.view(np.float16).reshape(n_pad // 16, k_pad // 32, 2, 4, 16, 2, 4)
+                    # [T][c][plane][q][i][half][j4] -> W[16T + i][32c + 16 half + 4q + j4] * 2^e
+                    full = pl.transpose(2, 0, 4, 1, 5, 3, 6).reshape(2, n_pad, k_pad).astype(np.float64)
+                    rec = (full[0] + full[1]) / 2.0 ** e
+                    assert np.abs(rec[:W.shape[0], :W.shape[1]] - W).max() <= 2.0 ** -21 * np.abs(W).max()
+                    assert not rec[W.shape[0]:].any() and not rec[:, W.shape[1]:].any()
+    assert off[..., :3].max() < buf.size
 
 
 def test_pc_step_table_matches_reference_formula():

@@ -149,12 +149,14 @@ def test_pc_large_rows_calibrated(score_sd):
 
 
 def test_ode_large_rows(score_sd):
-    """R = 4800, the shipped ODE setting (T0=0.55, RK45): identical nfev, 1e-4 / 1e-5."""
+    """R = 4800, the shipped ODE setting (T0=0.55, RK45): identical nfev, the calibrated bar against the
+    float64 reference, and 1e-4 / 1e-5 against the fp32 reference."""
     import large_noise
     g = golden("large_ode_r4800")
     _, _, B, K, _, T0, _ = large_noise.CASES["ode_r4800"]
     pts, center, prior, _, _ = large_noise.inputs("ode_r4800")
     pose, q, _, ex = oracle.pred_func(score_sd, pts, center, K, None, "ode", prior, T0=T0)
     assert ex["nfev"] == int(g["nfev"])
+    large_noise.check_calibrated(pose, g)
     assert np.abs(pose[..., :6] - g["pred_pose"][..., :6]).max() < 1e-4
     assert rel(pose[..., 6:], g["pred_pose"][..., 6:]) < 1e-5
