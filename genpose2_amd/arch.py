@@ -67,6 +67,41 @@ def level_out_channels(level: int) -> int:
     return sum(m[-1] for m in MLPS[level])
 
 
+# ---------------------------------------------------------------- DINO-pointwise fused encoder
+# Pointnet2ClsMSGFus(input_channels=384) (pointnet2.py:255-388; selected by --dino pointwise,
+# posenet.py:75-77): the Light SA levels with 384 per-point image-feature channels entering level 0,
+# a relative-PE transformer block after every level (attention.py:414-533, bias 648-735) and a gated
+# fusion of the (index-interpolated) image features before levels 1..4 (attention.py:224-325).
+DINO_DIM = 384
+FUS_HEADS = 8             # TransformerBlockWithRelativePE(channel_out, num_heads=8)
+FUS_FF_MULT = 4           # linear1: d -> 4d
+FUS_PE_HID = 16           # distance / direction encoders: Linear(1|3, 16) -> ReLU -> Linear(16, 8)
+FUS_REDUCTION = 4         # GatedAttentionFusion reduction_ratio
+FUS_SPATIAL_K = 7         # spatial attention Conv1d(2, 1, 7, padding=3)
+LN_EPS = 1e-5             # nn.LayerNorm default
+
+
+def fus_sa_branches() -> List[List[SABranch]]:
+    """sa_branches() with the 384 image-feature channels entering level 0 (pointnet2.py:281-285:
+    channel_in starts at input_channels and is the previous level's channel_out afterwards)."""
+    levels = []
+    c_in = DINO_DIM
+    for lv in range(N_LEVELS):
+        branches, off = [], 0
+        for b, mlp in enumerate(MLPS[lv]):
+            branches.append(SABranch(lv, b, NPOINTS[lv], RADII[lv][b], NSAMPLES[lv][b],
+                                     (c_in + 3,) + tuple(mlp), off))
+            off += mlp[-1]
+        levels.append(branches)
+        c_in = off
+    return levels
+
+
+def fus_level_points(level: int, n_points: int) -> int:
+    """Points (tokens) of level `level`'s output: npoint, or 1 after GroupAll."""
+    return NPOINTS[level] if NPOINTS[level] is not None else 1
+
+
 # ---------------------------------------------------------------- score / energy net
 POSE_DIM = 9          # rot_matrix: 6D rotation + translation (genpose_utils.py:21-38)
 POSE_HID = 256        # pose_encoder 9->256->256

@@ -19,24 +19,78 @@ import numpy as np
 from . import arch
 
 StateDict = Dict[str, np.ndarray]
-_KIND_ID = {"score": 1, "energy": 2, "scale": 3}
+_KIND_ID = {"score": 1, "energy": 2, "scale": 3, "score_pointwise": 4, "energy_pointwise": 5}
 
 
 # ---------------------------------------------------------------- manifest
-def manifest(kind: str) -> List[Tuple[str, Tuple[int, ...], str]]:
-    """(key, shape, init rule) for every tensor of the model selected by ``kind``."""
+def _bn(prefix: str, n: int) -> List[Tuple[str, Tuple[int, ...], str]]:
+    out = [(f"{prefix}.{nm}", (n,), rule) for nm, rule in
+           (("weight", "bn_gamma"), ("bias", "bn_beta"), ("running_mean", "bn_mean"), ("running_var", "bn_var"))]
+    return out + [(f"{prefix}.num_batches_tracked", (), "zero_i64")]
+
+
+def _sa_manifest(levels) -> List[Tuple[str, Tuple[int, ...], str]]:
     out: List[Tuple[str, Tuple[int, ...], str]] = []
-    if kind in ("score", "energy"):
-        for lv, branches in enumerate(arch.sa_branches()):
-            for br in branches:
-                w = br.widths
-                for i in range(len(w) - 1):
-                    p = f"pts_encoder.SA_modules.{lv}.mlps.{br.branch}.layer{i}"
-                    out.append((f"{p}.conv.weight", (w[i + 1], w[i], 1, 1), "conv"))
-                    for nm, rule in (("weight", "bn_gamma"), ("bias", "bn_beta"),
-                                     ("running_mean", "bn_mean"), ("running_var", "bn_var")):
-                        out.append((f"{p}.bn.bn.{nm}", (w[i + 1],), rule))
-                    out.append((f"{p}.bn.bn.num_batches_tracked", (), "zero_i64"))
+    for lv, branches in enumerate(levels):
+        for br in branches:
+            w = br.widths
+            for i in range(len(w) - 1):
+                p = f"pts_encoder.SA_modules.{lv}.mlps.{br.branch}.layer{i}"
+                out.append((f"{p}.conv.weight", (w[i + 1], w[i], 1, 1), "conv"))
+                out += _bn(f"{p}.bn.bn", w[i + 1])
+    return out
+
+
+def fus_encoder_manifest() -> List[Tuple[str, Tuple[int, ...], str]]:
+    """Pointnet2ClsMSGFus(384) (pointnet2.py:255-336): SA levels, per-level relative-PE encoders
+    (attention.py:648-671) and transformer blocks (attention.py:414-506, :495-503), and the gated
+    fusions of levels 1..4 (attention.py:224-279; C = the previous level's channels)."""
+    out = _sa_manifest(arch.fus_sa_branches())
+    H, P = arch.FUS_HEADS, arch.FUS_PE_HID
+    for lv in range(arch.N_LEVELS):
+        d = arch.level_out_channels(lv)
+        r = f"pts_encoder.relative_pos_encoders.{lv}"
+        out += [(f"{r}.distance_encoder.0.weight", (P, 1), "linear"), (f"{r}.distance_encoder.0.bias", (P,), "linear_bias:1"),
+                (f"{r}.distance_encoder.2.weight", (H, P), "linear"), (f"{r}.distance_encoder.2.bias", (H,), f"linear_bias:{P}"),
+                (f"{r}.direction_encoder.0.weight", (P, 3), "linear"), (f"{r}.direction_encoder.0.bias", (P,), "linear_bias:3"),
+                (f"{r}.direction_encoder.2.weight", (H, P), "linear"), (f"{r}.direction_encoder.2.bias", (H,), f"linear_bias:{P}"),
+                (f"{r}.fusion.weight", (H, 2 * H), "linear"), (f"{r}.fusion.bias", (H,), f"linear_bias:{2 * H}")]
+    for lv in range(arch.N_LEVELS):
+        d = arch.level_out_channels(lv)
+        t = f"pts_encoder.transformer_blocks.{lv}"
+        for nm in ("wq", "wk", "wv", "wo"):
+            out += [(f"{t}.self_attn.{nm}.weight", (d, d), "linear"), (f"{t}.self_attn.{nm}.bias", (d,), f"linear_bias:{d}")]
+        f = arch.FUS_FF_MULT * d
+        out += [(f"{t}.linear1.weight", (f, d), "linear"), (f"{t}.linear1.bias", (f,), f"linear_bias:{d}"),
+                (f"{t}.linear2.weight", (d, f), "linear"), (f"{t}.linear2.bias", (d,), f"linear_bias:{f}"),
+                (f"{t}.norm1.weight", (d,), "ln_gamma"), (f"{t}.norm1.bias", (d,), "ln_beta"),
+                (f"{t}.norm2.weight", (d,), "ln_gamma"), (f"{t}.norm2.bias", (d,), "ln_beta")]
+    for k in range(1, arch.N_LEVELS):
+        c, o = arch.level_out_channels(k - 1), arch.DINO_DIM
+        c2, cr = 2 * c, (2 * c) // arch.FUS_REDUCTION
+        g = f"pts_encoder.feature_fusions.{k - 1}"
+        out += [(f"{g}.channel_attention.1.weight", (cr, c2, 1), "conv1d"), (f"{g}.channel_attention.1.bias", (cr,), f"linear_bias:{c2}"),
+                (f"{g}.channel_attention.3.weight", (c, cr, 1), "conv1d"), (f"{g}.channel_attention.3.bias", (c,), f"linear_bias:{cr}"),
+                (f"{g}.spatial_attention.0.weight", (1, 2, arch.FUS_SPATIAL_K), "conv1d"),
+                (f"{g}.gate.0.weight", (c, c2, 1), "conv1d"), (f"{g}.gate.0.bias", (c,), f"linear_bias:{c2}")]
+        out += _bn(f"{g}.gate.1", c)
+        out += [(f"{g}.original_transform.0.weight", (c, o, 1), "conv1d"),
+                (f"{g}.original_transform.0.bias", (c,), f"linear_bias:{o}")]
+        out += _bn(f"{g}.original_transform.1", c)
+        for m in ("downsample", "output_conv"):
+            out += [(f"{g}.{m}.0.weight", (c, c, 1), "conv1d"), (f"{g}.{m}.0.bias", (c,), f"linear_bias:{c}")]
+            out += _bn(f"{g}.{m}.1", c)
+    return out
+
+
+def manifest(kind: str) -> List[Tuple[str, Tuple[int, ...], str]]:
+    """(key, shape, init rule) for every tensor of the model selected by ``kind``.
+    ``*_pointwise``: the --dino pointwise model's point-cloud path (Pointnet2ClsMSGFus encoder + the
+    same heads; the DINOv3 backbone and ImgEncoder that produce the per-point features are not part
+    of it)."""
+    out: List[Tuple[str, Tuple[int, ...], str]] = []
+    if kind in ("score", "energy", "score_pointwise", "energy_pointwise"):
+        out += fus_encoder_manifest() if kind.endswith("_pointwise") else _sa_manifest(arch.sa_branches())
         n = "pose_score_net"
         out += [(f"{n}.pose_encoder.0.weight", (arch.POSE_HID, arch.POSE_DIM), "linear"),
                 (f"{n}.pose_encoder.0.bias", (arch.POSE_HID,), "linear_bias:9"),
@@ -72,6 +126,13 @@ def _draw(rng: np.random.Generator, shape, rule: str) -> np.ndarray:
     if rule == "linear":          # torch nn.Linear default: U(+-1/sqrt(fan_in))
         a = 1.0 / np.sqrt(shape[1])
         return rng.uniform(-a, a, size=shape)
+    if rule == "conv1d":          # nn.Conv1d default: U(+-1/sqrt(in * kernel))
+        a = 1.0 / np.sqrt(int(np.prod(shape[1:])))
+        return rng.uniform(-a, a, size=shape)
+    if rule == "ln_gamma":
+        return rng.uniform(0.8, 1.2, size=shape)
+    if rule == "ln_beta":
+        return rng.uniform(-0.1, 0.1, size=shape)
     if rule.startswith("linear_bias:"):
         a = 1.0 / np.sqrt(int(rule.split(":")[1]))
         return rng.uniform(-a, a, size=shape)

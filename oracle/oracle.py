@@ -526,3 +526,143 @@ def get_energy(sd, pts: np.ndarray, pts_center: np.ndarray, pose_samples: np.nda
     rows[:, 6:] -= np.repeat(pts_center.astype(F32), K, axis=0)
     t = np.full((B * K, 1), F32(T), dtype=F32)
     return energy_forward(sd, np.repeat(feat, K, 0), rows, t).reshape(B, K, 2)
+
+
+# ============================================================ DINO-pointwise fused encoder (Pointnet2ClsMSGFus)
+def _t(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=F32))
+
+
+def sa_level(sd, prefix: str, lv: int, branches, xyz: np.ndarray, feats: Optional[np.ndarray]):
+    """One PointnetSAModuleMSG level (pointnet2_modules.py:19-124) over (B,N,3) xyz and (B,C,N) features:
+    FPS + gather, ball query + group per branch, SharedMLP, max-pool. Returns (new_xyz | None, (B,C_out,M))."""
+    npoint = arch.NPOINTS[lv]
+    if npoint is not None:
+        fidx = furthest_point_sample(xyz, npoint)
+        new_xyz = gather_operation(xyz.transpose(0, 2, 1), fidx).transpose(0, 2, 1).copy()
+    else:
+        fidx, new_xyz = None, None
+    outs = []
+    for br in branches:
+        if npoint is not None:
+            idx = ball_query(br.radius, br.nsample, xyz, new_xyz)
+            gx = grouping_operation(xyz.transpose(0, 2, 1), idx) - new_xyz.transpose(0, 2, 1)[..., None]
+            grouped = gx if feats is None else np.concatenate([gx, grouping_operation(feats, idx)], axis=1)
+        else:
+            gx = xyz.transpose(0, 2, 1)[:, :, None, :]
+            grouped = gx if feats is None else np.concatenate([gx, feats[:, :, None, :]], axis=1)
+        h = grouped.astype(F32)
+        for i in range(len(br.widths) - 1):
+            h = _conv_bn_relu(h, sd, f"{prefix}SA_modules.{lv}.mlps.{br.branch}.layer{i}")
+        outs.append(h.max(axis=3))
+    return new_xyz, fidx, np.concatenate(outs, axis=1).astype(F32)
+
+
+def relative_bias(sd, prefix: str, xyz: np.ndarray) -> np.ndarray:
+    """EfficientRelativePositionalEncoding.forward (attention.py:680-735): rel[b,i,j] = xyz[j] - xyz[i];
+    distance / direction encoders (Linear -> ReLU -> Linear), fusion Linear(16, 8) -> (B, 8, N, N)."""
+    import torch
+    import torch.nn.functional as tf
+    w = lambda k: _t(sd[f"{prefix}.{k}"])  # noqa: E731
+    x = _t(xyz)
+    rel = x.unsqueeze(1) - x.unsqueeze(2)
+    dist = torch.norm(rel, dim=-1, keepdim=True)
+    db = tf.linear(torch.relu(tf.linear(dist, w("distance_encoder.0.weight"), w("distance_encoder.0.bias"))),
+                   w("distance_encoder.2.weight"), w("distance_encoder.2.bias"))
+    direction = rel / (torch.norm(rel, dim=-1, keepdim=True) + 1e-7)
+    ob = tf.linear(torch.relu(tf.linear(direction, w("direction_encoder.0.weight"), w("direction_encoder.0.bias"))),
+                   w("direction_encoder.2.weight"), w("direction_encoder.2.bias"))
+    fused = tf.linear(torch.cat([db, ob], dim=-1), w("fusion.weight"), w("fusion.bias"))
+    return fused.permute(0, 3, 1, 2).contiguous().numpy()
+
+
+def transformer_block(sd, prefix: str, x: np.ndarray, bias: Optional[np.ndarray]) -> np.ndarray:
+    """TransformerBlockWithRelativePE.forward (attention.py:505-533) over MultiheadAttentionWithRelativePE
+    (attention.py:436-488), eval mode (dropout = identity). x (B, C, N) -> (B, C, N)."""
+    import math
+    import torch
+    import torch.nn.functional as tf
+    w = lambda k: _t(sd[f"{prefix}.{k}"])  # noqa: E731
+    xt = _t(x).transpose(1, 2).contiguous()
+    Bn, Nn, C = xt.shape
+    H = arch.FUS_HEADS
+    hd = C // H
+
+    def heads(nm):
+        return tf.linear(xt, w(f"self_attn.{nm}.weight"), w(f"self_attn.{nm}.bias")).view(Bn, Nn, H, hd).transpose(1, 2)
+    q, k, v = heads("wq"), heads("wk"), heads("wv")
+    s = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(hd)
+    if bias is not None:
+        s = s + _t(bias)
+    o = torch.matmul(torch.softmax(s, dim=-1), v).transpose(1, 2).contiguous().view(Bn, Nn, C)
+    o = tf.linear(o, w("self_attn.wo.weight"), w("self_attn.wo.bias"))
+    xt = tf.layer_norm(xt + o, (C,), w("norm1.weight"), w("norm1.bias"), arch.LN_EPS)
+    f = tf.linear(torch.relu(tf.linear(xt, w("linear1.weight"), w("linear1.bias"))), w("linear2.weight"), w("linear2.bias"))
+    xt = tf.layer_norm(xt + f, (C,), w("norm2.weight"), w("norm2.bias"), arch.LN_EPS)
+    return xt.transpose(1, 2).contiguous().numpy()
+
+
+def _conv1d_bn(x, sd, prefix, act):
+    """Conv1d(k=1, bias) -> BatchNorm1d(eval) -> act (attention.py:262-281 Sequentials)."""
+    import torch
+    import torch.nn.functional as tf
+    w = lambda k: _t(sd[f"{prefix}.{k}"])  # noqa: E731
+    y = tf.conv1d(x, w("0.weight"), w("0.bias"))
+    y = tf.batch_norm(y, w("1.running_mean"), w("1.running_var"), w("1.weight"), w("1.bias"), training=False,
+                      eps=arch.BN_EPS)
+    return act(y)
+
+
+def gated_fusion(sd, prefix: str, cur: np.ndarray, orig: np.ndarray) -> np.ndarray:
+    """GatedAttentionFusion.forward (attention.py:284-325): cur (B, C, N), orig (B, 384, N) -> (B, C, N)."""
+    import torch
+    import torch.nn.functional as tf
+    w = lambda k: _t(sd[f"{prefix}.{k}"])  # noqa: E731
+    c, o = _t(cur), _t(orig)
+    ot = _conv1d_bn(o, sd, f"{prefix}.original_transform", torch.relu)
+    ca = torch.mean(torch.cat([c, ot], dim=1), dim=2, keepdim=True)          # AdaptiveAvgPool1d(1)
+    ca = torch.relu(tf.conv1d(ca, w("channel_attention.1.weight"), w("channel_attention.1.bias")))
+    ca = torch.sigmoid(tf.conv1d(ca, w("channel_attention.3.weight"), w("channel_attention.3.bias")))
+    sp_in = torch.cat([torch.max(c, dim=1, keepdim=True)[0], torch.mean(c, dim=1, keepdim=True)], dim=1)
+    sp = torch.sigmoid(tf.conv1d(sp_in, w("spatial_attention.0.weight"), None, padding=arch.FUS_SPATIAL_K // 2))
+    att = ot * ca * sp
+    g = _conv1d_bn(torch.cat([c, att], dim=1), sd, f"{prefix}.gate", torch.sigmoid)
+    fused = g * c + (1 - g) * att
+    return _conv1d_bn(fused, sd, f"{prefix}.output_conv", torch.relu).numpy()
+
+
+def interp_points(x: np.ndarray, n_out: int) -> np.ndarray:
+    """F.interpolate(x, size=n_out, mode="linear", align_corners=False) along the point index
+    (pointnet2.py:344-350): x (B, C, N)."""
+    import torch.nn.functional as tf
+    return tf.interpolate(_t(x), size=n_out, mode="linear", align_corners=False).numpy()
+
+
+def fus_encoder_forward(sd, pts: np.ndarray, rgb_feat: np.ndarray, return_levels: bool = False):
+    """Pointnet2ClsMSGFus.forward (pointnet2.py:331-380), eval mode: pts (B,N,3), rgb_feat (B,N,384) -> (B,1024).
+    The reference's gather of `features` at the end of each level (:370-377) feeds nothing and is omitted."""
+    p = "pts_encoder."
+    xyz = np.ascontiguousarray(pts[..., :3], dtype=F32)
+    orig = np.ascontiguousarray(rgb_feat.transpose(0, 2, 1), dtype=F32)    # (B, 384, N)
+    feats = orig
+    levels = []
+    for lv, branches in enumerate(arch.fus_sa_branches()):
+        rec = {}
+        if lv > 0:
+            if orig.shape[2] != feats.shape[2]:
+                orig = interp_points(orig, feats.shape[2])
+            feats = gated_fusion(sd, f"{p}feature_fusions.{lv - 1}", feats, orig)
+            rec["fused"] = feats
+        new_xyz, fidx, feats = sa_level(sd, p, lv, branches, xyz, feats)
+        rec.update(sa=feats, fps_idx=fidx)
+        bias = relative_bias(sd, f"{p}relative_pos_encoders.{lv}", new_xyz) if new_xyz is not None else None
+        feats = transformer_block(sd, f"{p}transformer_blocks.{lv}", feats, bias)
+        rec["tf"] = feats
+        if lv == 3:
+            rec["bias"] = bias
+        levels.append(rec)
+        if new_xyz is not None:
+            xyz = new_xyz
+    out = feats[:, :, 0]
+    return (out, levels) if return_levels else out

@@ -320,3 +320,15 @@ def test_load_checkpoint_reference_format(tmp_path, prefix):
             np.testing.assert_array_equal(pack.pack_encoder(sd)[0], pack.pack_encoder(ref)[0])
     with pytest.raises(ValueError):
         weights.load_checkpoint(str(tmp_path / "missing.pth"))
+
+
+def test_fus_manifest_matches_reference_layout():
+    """The fused encoder's manifest equals the reference Pointnet2ClsMSGFus(384) state dict (keys and
+    shapes; golden_fus_layout.json, written by tests/golden/make_golden_fus.py)."""
+    import json
+    from conftest import GOLDEN
+    from genpose2_amd import weights
+    with open(os.path.join(GOLDEN, "golden_fus_layout.json")) as f:
+        lay = json.load(f)
+    mine = {k[len("pts_encoder."):]: list(s) for k, s, _ in weights.fus_encoder_manifest()}
+    assert mine == lay

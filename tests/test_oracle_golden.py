@@ -160,3 +160,23 @@ def test_ode_large_rows(score_sd):
     large_noise.check_calibrated(pose, g)
     assert np.abs(pose[..., :6] - g["pred_pose"][..., :6]).max() < 1e-4
     assert rel(pose[..., 6:], g["pred_pose"][..., 6:]) < 1e-5
+
+
+def test_fus_encoder_levels():
+    """Pointnet2ClsMSGFus (DINO-pointwise fused encoder) restatement vs the reference's own module
+    (golden_fus.npz, tests/golden/make_golden_fus.py): per-level SA output, fused input, transformer
+    output, the level-3 relative-PE bias and the final feature."""
+    import make_golden_fus as mf
+    from genpose2_amd import synthetic, weights
+    g = golden("fus")
+    sd = weights.synthetic_state_dict("score_pointwise")
+    pts, _ = synthetic.make_batch(mf.CID, mf.B, mf.N)
+    feat, levels = oracle.fus_encoder_forward(sd, pts, mf.rgb_features(mf.B, mf.N), return_levels=True)
+    for lv in range(5):
+        if levels[lv]["fps_idx"] is not None:
+            assert np.array_equal(levels[lv]["fps_idx"], g[f"l{lv}_fps"])
+        for k in ("sa", "tf", "fused"):
+            if f"l{lv}_{k}" in g:
+                assert rel(levels[lv][k][0], g[f"l{lv}_{k}"]) < 1e-5, (lv, k)
+    assert rel(levels[3]["bias"][0], g["l3_bias"]) < 1e-6
+    assert rel(feat, g["feat"]) < 1e-5
