@@ -45,6 +45,18 @@ _SIGS: Dict[str, tuple] = {
     "gp_encoder_workspace_layout": (c_int, [c_int, c_int, c_int64_p]),
     "gp_encoder_forward": (c_int, [c_void_p, c_int64_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p,
                                    c_void_p]),
+    "gp_encoder_fps": (c_int, [c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p]),
+    "gp_sa_level": (c_int, [c_void_p, c_int64_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t,
+                            c_void_p, c_void_p]),
+    "gp_linear": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "gp_add_layernorm": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
+    "gp_relpe_bias_bytes": (c_size_t, [c_int, c_int]),
+    "gp_relpe_bias": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "gp_mha_attention": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "gp_interp_points": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "gp_fusion_attend": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p]),
+    "gp_fusion_mix": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "gp_head_object_proj": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_int, c_void_p, c_void_p]),
     "gp_head_time_proj": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_int, c_void_p, c_void_p]),
     "gp_score_eval": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_float, c_void_p, c_int, c_int,

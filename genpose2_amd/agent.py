@@ -53,15 +53,32 @@ class PoseNet:
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(self.cfg.noise_seed)
         self.weights_source = f"synthetic(seed={self.cfg.seed})"
-        self._build(weights.synthetic_state_dict(self.cfg.agent_type, seed=self.cfg.seed))
+        self._build(weights.synthetic_state_dict(self.weights_kind, seed=self.cfg.seed))
+
+    @property
+    def pointwise(self) -> bool:
+        """--dino pointwise: the Pointnet2ClsMSGFus encoder (posenet.py:75-77) over per-point features."""
+        return self.cfg.dino == "pointwise" and self.cfg.agent_type in ("score", "energy")
+
+    @property
+    def weights_kind(self) -> str:
+        return self.cfg.agent_type + ("_pointwise" if self.pointwise else "")
 
     # ------------------------------------------------------------------ model construction
     def _build(self, sd: weights.StateDict) -> None:
-        weights.check_keys(sd, self.cfg.agent_type)
+        if self.pointwise:
+            # a --dino pointwise checkpoint also holds the frozen DINOv3 backbone and the ImgEncoder
+            # (posenet.py:56-69); they produce data["point_rgb_feat"] upstream of this path
+            sd = {k: v for k, v in sd.items() if not k.startswith(("dino.", "img_encoder."))}
+        weights.check_keys(sd, self.weights_kind)
         self.state_dict = sd
         self._pc_cache = {}                        # T -> (step table, tproj) of these weights
         if self.cfg.agent_type in ("score", "energy"):
-            self.encoder = dev.EncoderModel(sd, self.device)
+            if self.pointwise:
+                from .fus_encoder import FusEncoderModel
+                self.encoder = FusEncoderModel(sd, self.device)
+            else:
+                self.encoder = dev.EncoderModel(sd, self.device)
             self.heads = dev.HeadModel(sd, self.device)
             self.scale = None
         else:
@@ -106,6 +123,13 @@ class PoseNet:
         return c
 
     def _encode(self, data) -> torch.Tensor:
+        if self.pointwise:
+            # posenet.py:136-197 gathers DINOv3 patch features at each point; that stage (and its weights)
+            # is upstream of this path: the caller supplies its output
+            if data.get("point_rgb_feat") is None:
+                raise KeyError("dino 'pointwise' needs data['point_rgb_feat'] (B, N, 384): the per-point DINOv3 "
+                               "features of posenet.py:136-197")
+            return self.encoder.forward(data["pts"], data["point_rgb_feat"])
         return self.encoder.forward(data["pts"])
 
     @torch.no_grad()

@@ -902,229 +902,290 @@ static int launch_pair(SAArgs a0, SAArgs a1, int B, hipStream_t st) {
 // planes or -1, split exponent}.
 static inline const int64_t* enc_layer(const int64_t* tab, int l, int br, int i) { return tab + ((l * 2 + br) * 3 + i) * 4; }
 
-extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N,
-                                  void* workspace, size_t workspace_bytes, float* feat, hipStream_t st) {
-    GP_REQUIRE(wbuf && layer_off && pts && workspace && feat, "encoder_forward: null pointer");
-    GP_REQUIRE(B >= 1 && N >= kNpoint[0] && N <= 8192, "encoder_forward: need 1<=b and 512<=n<=8192 (b=%d n=%d)",
-               B, N);
-    const EncLayout L = enc_layout(B, N);
-    GP_REQUIRE(workspace_bytes >= L.total, "encoder_forward: workspace %zu < %zu", workspace_bytes, L.total);
-    char* ws = static_cast<char*>(workspace);
+// Per-call view of the encoder workspace (enc_layout) and the packed layer table.
+struct EncCtx {
+    const float* wbuf;
+    const int64_t* tab;
+    const float* pts;
+    int B, N;
+    char* ws;
+    EncLayout L;
     int* fidx[4];
     float* nxyz[4];
     int nin[4], mout[4];
+};
+
+static EncCtx enc_ctx(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N, void* workspace) {
+    EncCtx c;
+    c.wbuf = wbuf;
+    c.tab = layer_off;
+    c.pts = pts;
+    c.B = B;
+    c.N = N;
+    c.ws = static_cast<char*>(workspace);
+    c.L = enc_layout(B, N);
     for (int l = 0; l < 4; ++l) {
-        fidx[l] = reinterpret_cast<int*>(ws + L.fps[l]);
-        nxyz[l] = reinterpret_cast<float*>(ws + L.nxyz[l]);
-        nin[l] = l == 0 ? N : kNpoint[l - 1];
-        mout[l] = kNpoint[l];
+        c.fidx[l] = reinterpret_cast<int*>(c.ws + c.L.fps[l]);
+        c.nxyz[l] = reinterpret_cast<float*>(c.ws + c.L.nxyz[l]);
+        c.nin[l] = l == 0 ? N : kNpoint[l - 1];
+        c.mout[l] = kNpoint[l];
     }
-    // FPS level 0 here; levels 1-3 run beside the level-0 / level-1 MLP launches (FpsSide)
-    int rc = gp_launch_fps_chain(pts, B, 1, nin, mout, fidx, nxyz, st);
-    if (rc) return rc;
-    for (int l = 0; l < 5; ++l) {
-        const float* xyz_prev = l == 0 ? pts : nxyz[l - 1];
-        const int n_prev = l == 0 ? N : kNpoint[l - 1];
-        int* b0 = nullptr;
-        int* b1 = nullptr;
-        if (l < 4) {
-            b0 = reinterpret_cast<int*>(ws + L.ball[l][0]);
-            b1 = reinterpret_cast<int*>(ws + L.ball[l][1]);
-            rc = gp_launch_ball_query2(B, n_prev, kNpoint[l], kRadius[l][0], kRadius[l][1], kNs[0], kNs[1], nxyz[l],
-                                       xyz_prev, b0, b1, st);
-            if (rc) return rc;
+    return c;
+}
+
+// One SA level l (ball query, per-point layer 0, layers 1-2 + max-pool) over the FPS results already
+// in the workspace. feat_prev (B, n_prev, c_prev) point-major or null (c_prev = 0); out (B, M_l, C_l).
+// side: FPS levels that ride along as extra workgroups of the narrow launches (gp_encoder_forward),
+// or null when the FPS chain ran whole beforehand (gp_encoder_fps).
+static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_prev, float* out, bool side,
+                        hipStream_t st) {
+    const int B = c.B;
+    const float* wbuf = c.wbuf;
+    const int64_t* layer_off = c.tab;
+    const float* xyz_prev = l == 0 ? c.pts : c.nxyz[l - 1];
+    const int n_prev = l == 0 ? c.N : kNpoint[l - 1];
+    int rc = GP_OK;
+    int* b0 = nullptr;
+    int* b1 = nullptr;
+    if (l < 4) {
+        b0 = reinterpret_cast<int*>(c.ws + c.L.ball[l][0]);
+        b1 = reinterpret_cast<int*>(c.ws + c.L.ball[l][1]);
+        rc = gp_launch_ball_query2(B, n_prev, kNpoint[l], kRadius[l][0], kRadius[l][1], kNs[0], kNs[1], c.nxyz[l],
+                                   xyz_prev, b0, b1, st);
+        if (rc) return rc;
+    }
+    // layer 0 once per input point for both branches (levels 0-3)
+    float* qbuf = l < 4 ? reinterpret_cast<float*>(c.ws + c.L.proj[l]) : nullptr;
+    if (l < 4) {
+        int q_off = 0;
+        SAArgs pp[2];
+        for (int br = 0; br < 2; ++br) {
+            SAArgs& pa = pp[br];
+            pa = {};
+            pa.n_prev = n_prev;
+            pa.c_prev = c_prev;
+            pa.m = 1;
+            pa.ns = n_prev;
+            pa.cols = n_prev;
+            pa.xyz_prev = xyz_prev;
+            pa.feat_prev = feat_prev;
+            pa.nlayers = 1;
+            const int64_t* o = enc_layer(layer_off, l, br, 0);
+            GP_REQUIRE(o[0] >= 0 && o[1] >= 0, "encoder: missing layer %d/%d/0", l, br);
+            pa.w[0] = wbuf + o[0];
+            pa.bias[0] = wbuf + o[1];
+            pa.kg[0] = (pa.c_prev + 16) / 16;
+            pa.nt[0] = pad16(kWidths[l][br][1]) / 16;
+            pa.proj_out = qbuf;
+            pa.q_stride = proj_stride(l);
+            pa.q_off = q_off;
+            pa.tag = 16 + l * 2 + br;
+            q_off += pad16(kWidths[l][br][1]);
         }
-        // layer 0 once per input point for both branches (levels 0-3)
-        float* qbuf = l < 4 ? reinterpret_cast<float*>(ws + L.proj[l]) : nullptr;
-        if (l < 4) {
-            int q_off = 0;
-            SAArgs pp[2];
-            for (int br = 0; br < 2; ++br) {
-                SAArgs& pa = pp[br];
-                pa = {};
-                pa.n_prev = n_prev;
-                pa.c_prev = l == 0 ? 0 : kCout[l - 1];
-                pa.m = 1;
-                pa.ns = n_prev;
-                pa.cols = n_prev;
-                pa.xyz_prev = xyz_prev;
-                pa.feat_prev = l == 0 ? nullptr : reinterpret_cast<const float*>(ws + L.feat[l - 1]);
-                pa.nlayers = 1;
-                const int64_t* o = enc_layer(layer_off, l, br, 0);
-                GP_REQUIRE(o[0] >= 0 && o[1] >= 0, "encoder_forward: missing layer %d/%d/0", l, br);
-                pa.w[0] = wbuf + o[0];
-                pa.bias[0] = wbuf + o[1];
-                pa.kg[0] = (pa.c_prev + 16) / 16;
-                pa.nt[0] = pad16(kWidths[l][br][1]) / 16;
-                pa.proj_out = qbuf;
-                pa.q_stride = proj_stride(l);
-                pa.q_off = q_off;
-                pa.tag = 16 + l * 2 + br;
-                q_off += pad16(kWidths[l][br][1]);
-            }
-            rc = launch_pair<4>(pp[0], pp[1], B, st);
-            if (rc) return rc;
+        rc = launch_pair<4>(pp[0], pp[1], B, st);
+        if (rc) return rc;
+    }
+    if (l == 4) {  // group-all pools with atomicMax when a centroid spans workgroups
+        if (hipMemsetAsync(out, 0, sizeof(float) * B * kCout[4], st) != hipSuccess)
+            return gp_check_launch("encoder memset");
+    }
+    if (l <= 1) {   // narrow levels: one launch, wave-independent centroids
+        NarrowArgs na[2];
+        int out_off = 0, q_off = 0;
+        for (int br = 0; br < 2; ++br) {
+            NarrowArgs& n = na[br];
+            n = {};
+            n.qin = qbuf;
+            n.q_stride = proj_stride(l);
+            n.q_off = q_off;
+            q_off += pad16(kWidths[l][br][1]);
+            n.n_prev = n_prev;
+            const int64_t* o0 = enc_layer(layer_off, l, br, 0);
+            const int64_t* o1 = enc_layer(layer_off, l, br, 1);
+            const int64_t* o2 = enc_layer(layer_off, l, br, 2);
+            GP_REQUIRE(o1[0] >= 0 && o2[0] >= 0, "encoder: missing layers of %d/%d", l, br);
+            n.w0 = wbuf + o0[0];
+            n.c_out_total = kCout[l];
+            n.kg0 = (c_prev + 16) / 16;
+            n.gx = c_prev / 16;
+            n.w1 = wbuf + o1[0];
+            n.b1 = wbuf + o1[1];
+            n.w2 = wbuf + o2[0];
+            n.b2 = wbuf + o2[1];
+            n.nbr = br == 0 ? b0 : b1;
+            n.cent = c.nxyz[l];
+            n.m = kNpoint[l];
+            n.ns = kNs[br];
+            n.nobj = B;
+            n.out = out;
+            n.out_off = out_off;
+            out_off += kWidths[l][br][3];
         }
-        float* out = l < 4 ? reinterpret_cast<float*>(ws + L.feat[l]) : feat;
-        if (l == 4) {  // group-all pools with atomicMax when a centroid spans workgroups
-            if (hipMemsetAsync(out, 0, sizeof(float) * B * kCout[4], st) != hipSuccess)
-                return gp_check_launch("encoder memset");
-        }
-        if (l <= 1) {   // narrow levels: one launch, wave-independent centroids
-            NarrowArgs na[2];
-            int out_off = 0, q_off = 0;
-            for (int br = 0; br < 2; ++br) {
-                NarrowArgs& n = na[br];
-                n = {};
-                n.qin = qbuf;
-                n.q_stride = proj_stride(l);
-                n.q_off = q_off;
-                q_off += pad16(kWidths[l][br][1]);
-                n.n_prev = n_prev;
-                const int64_t* o0 = enc_layer(layer_off, l, br, 0);
-                const int64_t* o1 = enc_layer(layer_off, l, br, 1);
-                const int64_t* o2 = enc_layer(layer_off, l, br, 2);
-                GP_REQUIRE(o1[0] >= 0 && o2[0] >= 0, "encoder_forward: missing layers of %d/%d", l, br);
-                n.w0 = wbuf + o0[0];
-                n.c_out_total = kCout[l];
-                const int c_prev = l == 0 ? 0 : kCout[l - 1];
-                n.kg0 = (c_prev + 16) / 16;
-                n.gx = c_prev / 16;
-                n.w1 = wbuf + o1[0];
-                n.b1 = wbuf + o1[1];
-                n.w2 = wbuf + o2[0];
-                n.b2 = wbuf + o2[1];
-                n.nbr = br == 0 ? b0 : b1;
-                n.cent = nxyz[l];
-                n.m = kNpoint[l];
-                n.ns = kNs[br];
-                n.nobj = B;
-                n.out = out;
-                n.out_off = out_off;
-                out_off += kWidths[l][br][3];
-            }
-            FpsSide fs = {};
+        FpsSide fs = {};   // nobj = 0: the FPS row of workgroups returns at once
+        if (side) {
             fs.nlev = l == 0 ? 1 : 2;          // level 0 launch: FPS level 1; level 1 launch: FPS levels 2, 3
-            fs.in = nxyz[l];
+            fs.in = c.nxyz[l];
             fs.nobj = B;
             for (int k = 0; k < fs.nlev; ++k) {
                 const int lv = l == 0 ? 1 : 2 + k;
-                fs.n[k] = nin[lv];
-                fs.m[k] = mout[lv];
-                const FpsGeom g = fps_geom(nin[lv]);
+                fs.n[k] = c.nin[lv];
+                fs.m[k] = c.mout[lv];
+                const FpsGeom g = fps_geom(c.nin[lv]);
                 fs.nb[k] = g.nb;
                 fs.jbits[k] = g.jbits;
-                fs.idx[k] = fidx[lv];
-                fs.nxyz[k] = nxyz[lv];
+                fs.idx[k] = c.fidx[lv];
+                fs.nxyz[k] = c.nxyz[lv];
             }
-            const dim3 grid(std::max(512, B), 3);
-            if (l == 0) {
-                const size_t lds = std::max({narrow_lds(1, 1, 2), narrow_lds(2, 2, 4), fps_side_lds(fs)});
-                hipLaunchKernelGGL((sa_narrow_kernel<1, 1, 2, 1, 2, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
-                                   na[1], fs);
-            } else {
-                const size_t lds = std::max({narrow_lds(4, 4, 8), narrow_lds(4, 6, 8), fps_side_lds(fs)});
-                hipLaunchKernelGGL((sa_narrow_kernel<4, 4, 8, 1, 4, 6, 8, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
-                                   na[1], fs);
-            }
-            rc = gp_check_launch("sa_narrow_kernel");
-            if (rc) return rc;
-            continue;
         }
-        // levels 2-3: split-f16 kernel when the table carries the planes (pack.pack_encoder)
-        if ((l == 2 || l == 3) && enc_layer(layer_off, l, 0, 1)[2] >= 0 && enc_layer(layer_off, l, 0, 2)[2] >= 0 &&
-            enc_layer(layer_off, l, 1, 1)[2] >= 0 && enc_layer(layer_off, l, 1, 2)[2] >= 0) {
-            constexpr int CT = 4;
-            SplitArgs sp[2];
-            int off_out = 0;
-            for (int br = 0; br < 2; ++br) {
-                SplitArgs& a = sp[br];
-                a = {};
-                a.n_prev = n_prev;
-                a.m = kNpoint[l];
-                a.ns = kNs[br];
-                a.cols = a.m * a.ns;
-                a.qin = qbuf;
-                a.q_stride = proj_stride(l);
-                a.q_off = br == 0 ? 0 : pad16(kWidths[l][0][1]);
-                const int64_t* o0 = enc_layer(layer_off, l, br, 0);
-                const int c_prev = kCout[l - 1];
-                a.w0 = wbuf + o0[0];
-                a.kg0 = (c_prev + 16) / 16;
-                a.gx = c_prev / 16;
-                a.nbr = br == 0 ? b0 : b1;
-                a.cent = nxyz[l];
-                for (int i = 0; i < 2; ++i) {
-                    const int64_t* o = enc_layer(layer_off, l, br, i + 1);
-                    a.w[i] = wbuf + o[2];
-                    a.bias[i] = wbuf + o[1];
-                    a.ew[i] = (int)o[3];
-                }
-                a.out = out;
-                a.c_out_total = kCout[l];
-                a.out_off = off_out;
-                off_out += kWidths[l][br][3];
-                GP_REQUIRE(a.cols % (16 * CT) == 0 && (16 * CT) % a.ns == 0,
-                           "encoder_forward: level %d columns %d do not tile by %d", l, a.cols, 16 * CT);
-            }
-            const dim3 grid(std::max(sp[0].cols, sp[1].cols) / (16 * CT), B, 2), blk(SPLIT_WV * 64);
-            if (l == 2) {
-                const size_t lds = sa_split_lds<CT, 4, 7>();
-                hipLaunchKernelGGL((sa_split_kernel<CT, 4, 7, 8, 7, 8>), grid, blk, lds, st, sp[0], sp[1]);
-            } else {
-                const size_t lds = std::max(sa_split_lds<CT, 8, 8>(), sa_split_lds<CT, 8, 12>());
-                hipLaunchKernelGGL((sa_split_kernel<CT, 8, 8, 16, 12, 16>), grid, blk, lds, st, sp[0], sp[1]);
-            }
-            rc = gp_check_launch("sa_split_kernel");
-            if (rc) return rc;
-            continue;
+        const dim3 grid(std::max(512, B), 3);
+        if (l == 0) {
+            const size_t lds = std::max({narrow_lds(1, 1, 2), narrow_lds(2, 2, 4), fps_side_lds(fs)});
+            hipLaunchKernelGGL((sa_narrow_kernel<1, 1, 2, 1, 2, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
+                               na[1], fs);
+        } else {
+            const size_t lds = std::max({narrow_lds(4, 4, 8), narrow_lds(4, 6, 8), fps_side_lds(fs)});
+            hipLaunchKernelGGL((sa_narrow_kernel<4, 4, 8, 1, 4, 6, 8, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
+                               na[1], fs);
         }
-        int out_off = 0;
-        SAArgs sa[2];
+        return gp_check_launch("sa_narrow_kernel");
+    }
+    // levels 2-3: split-f16 kernel when the table carries the planes (pack.pack_encoder)
+    if ((l == 2 || l == 3) && enc_layer(layer_off, l, 0, 1)[2] >= 0 && enc_layer(layer_off, l, 0, 2)[2] >= 0 &&
+        enc_layer(layer_off, l, 1, 1)[2] >= 0 && enc_layer(layer_off, l, 1, 2)[2] >= 0) {
+        constexpr int CT = 4;
+        SplitArgs sp[2];
+        int off_out = 0;
         for (int br = 0; br < 2; ++br) {
-            SAArgs& a = sa[br];
+            SplitArgs& a = sp[br];
             a = {};
             a.n_prev = n_prev;
-            a.c_prev = l == 0 ? 0 : kCout[l - 1];
-            a.m = l < 4 ? kNpoint[l] : 1;
-            a.ns = l < 4 ? kNs[br] : n_prev;
+            a.m = kNpoint[l];
+            a.ns = kNs[br];
             a.cols = a.m * a.ns;
-            a.xyz_prev = xyz_prev;
-            a.feat_prev = l == 0 ? nullptr : reinterpret_cast<const float*>(ws + L.feat[l - 1]);
-            a.cent = l < 4 ? nxyz[l] : nullptr;
-            a.nbr = l < 4 ? (br == 0 ? b0 : b1) : nullptr;
-            a.nlayers = l < 4 ? 3 : 2;
-            for (int i = 0; i < a.nlayers; ++i) {
-                const int64_t* o = enc_layer(layer_off, l, br, i);
-                GP_REQUIRE(o[0] >= 0 && o[1] >= 0, "encoder_forward: missing layer %d/%d/%d", l, br, i);
-                a.w[i] = wbuf + o[0];
+            a.qin = qbuf;
+            a.q_stride = proj_stride(l);
+            a.q_off = br == 0 ? 0 : pad16(kWidths[l][0][1]);
+            const int64_t* o0 = enc_layer(layer_off, l, br, 0);
+            a.w0 = wbuf + o0[0];
+            a.kg0 = (c_prev + 16) / 16;
+            a.gx = c_prev / 16;
+            a.nbr = br == 0 ? b0 : b1;
+            a.cent = c.nxyz[l];
+            for (int i = 0; i < 2; ++i) {
+                const int64_t* o = enc_layer(layer_off, l, br, i + 1);
+                a.w[i] = wbuf + o[2];
                 a.bias[i] = wbuf + o[1];
-                const int kin = i == 0 ? a.c_prev + 16 : pad16(kWidths[l][br][i]);
-                a.kg[i] = kin / 16;
-                a.nt[i] = pad16(kWidths[l][br][i + 1]) / 16;
+                a.ew[i] = (int)o[3];
             }
             a.out = out;
-            a.tag = l * 2 + br;
-            if (l < 4) {
-                a.qin = qbuf;
-                a.q_stride = proj_stride(l);
-                a.q_off = br == 0 ? 0 : pad16(kWidths[l][0][1]);
-            }
             a.c_out_total = kCout[l];
-            a.out_off = out_off;
-            out_off += kWidths[l][br][a.nlayers];
-            if (a.ns % 16 != 0) {
-                gp_set_error("encoder_forward: nsample %d not a multiple of 16", a.ns);
-                return GP_ERR_UNSUPPORTED;
-            }
+            a.out_off = off_out;
+            off_out += kWidths[l][br][3];
+            GP_REQUIRE(a.cols % (16 * CT) == 0 && (16 * CT) % a.ns == 0,
+                       "encoder: level %d columns %d do not tile by %d", l, a.cols, 16 * CT);
         }
-        // levels 2-3 at 32 columns (LDS ping-pong <= 80 KiB: 2-3 workgroups per CU), GroupAll split
-        // over 2 workgroups per (object, branch) with atomicMax pooling; both branches per launch
-        // levels 3-4: one pass of up to 8 tiles per wave per layer (2 workgroups per CU either way);
-        // level 2 keeps 4-tile passes: its 131 VGPRs fit 3 workgroups per CU, a 7-tile pass's 191 only
-        // 2 (measured 725 vs 764 us)
-        rc = l == 2 ? launch_pair<2, 4>(sa[0], sa[1], B, st) : launch_pair<2, 8>(sa[0], sa[1], B, st);
+        const dim3 grid(std::max(sp[0].cols, sp[1].cols) / (16 * CT), B, 2), blk(SPLIT_WV * 64);
+        if (l == 2) {
+            const size_t lds = sa_split_lds<CT, 4, 7>();
+            hipLaunchKernelGGL((sa_split_kernel<CT, 4, 7, 8, 7, 8>), grid, blk, lds, st, sp[0], sp[1]);
+        } else {
+            const size_t lds = std::max(sa_split_lds<CT, 8, 8>(), sa_split_lds<CT, 8, 12>());
+            hipLaunchKernelGGL((sa_split_kernel<CT, 8, 8, 16, 12, 16>), grid, blk, lds, st, sp[0], sp[1]);
+        }
+        return gp_check_launch("sa_split_kernel");
+    }
+    int out_off = 0;
+    SAArgs sa[2];
+    for (int br = 0; br < 2; ++br) {
+        SAArgs& a = sa[br];
+        a = {};
+        a.n_prev = n_prev;
+        a.c_prev = c_prev;
+        a.m = l < 4 ? kNpoint[l] : 1;
+        a.ns = l < 4 ? kNs[br] : n_prev;
+        a.cols = a.m * a.ns;
+        a.xyz_prev = xyz_prev;
+        a.feat_prev = feat_prev;
+        a.cent = l < 4 ? c.nxyz[l] : nullptr;
+        a.nbr = l < 4 ? (br == 0 ? b0 : b1) : nullptr;
+        a.nlayers = l < 4 ? 3 : 2;
+        for (int i = 0; i < a.nlayers; ++i) {
+            const int64_t* o = enc_layer(layer_off, l, br, i);
+            GP_REQUIRE(o[0] >= 0 && o[1] >= 0, "encoder: missing layer %d/%d/%d", l, br, i);
+            a.w[i] = wbuf + o[0];
+            a.bias[i] = wbuf + o[1];
+            const int kin = i == 0 ? a.c_prev + 16 : pad16(kWidths[l][br][i]);
+            a.kg[i] = kin / 16;
+            a.nt[i] = pad16(kWidths[l][br][i + 1]) / 16;
+        }
+        a.out = out;
+        a.tag = l * 2 + br;
+        if (l < 4) {
+            a.qin = qbuf;
+            a.q_stride = proj_stride(l);
+            a.q_off = br == 0 ? 0 : pad16(kWidths[l][0][1]);
+        }
+        a.c_out_total = kCout[l];
+        a.out_off = out_off;
+        out_off += kWidths[l][br][a.nlayers];
+        if (a.ns % 16 != 0) {
+            gp_set_error("encoder: nsample %d not a multiple of 16", a.ns);
+            return GP_ERR_UNSUPPORTED;
+        }
+    }
+    // levels 2-3 at 32 columns (LDS ping-pong <= 80 KiB: 2-3 workgroups per CU), GroupAll split
+    // over 2 workgroups per (object, branch) with atomicMax pooling; both branches per launch
+    // levels 3-4: one pass of up to 8 tiles per wave per layer (2 workgroups per CU either way);
+    // level 2 keeps 4-tile passes: its 131 VGPRs fit 3 workgroups per CU, a 7-tile pass's 191 only
+    // 2 (measured 725 vs 764 us)
+    return l == 2 ? launch_pair<2, 4>(sa[0], sa[1], B, st) : launch_pair<2, 8>(sa[0], sa[1], B, st);
+}
+
+static int enc_check(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N, void* workspace,
+                     size_t workspace_bytes) {
+    GP_REQUIRE(wbuf && layer_off && pts && workspace, "encoder: null pointer");
+    GP_REQUIRE(B >= 1 && N >= kNpoint[0] && N <= 8192, "encoder: need 1<=b and 512<=n<=8192 (b=%d n=%d)", B, N);
+    const size_t need = enc_layout(B, N).total;
+    GP_REQUIRE(workspace_bytes >= need, "encoder: workspace %zu < %zu", workspace_bytes, need);
+    return GP_OK;
+}
+
+extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N,
+                                  void* workspace, size_t workspace_bytes, float* feat, hipStream_t st) {
+    int rc = enc_check(wbuf, layer_off, pts, B, N, workspace, workspace_bytes);
+    if (rc) return rc;
+    GP_REQUIRE(feat, "encoder_forward: null feat");
+    const EncCtx c = enc_ctx(wbuf, layer_off, pts, B, N, workspace);
+    // FPS level 0 here; levels 1-3 run beside the level-0 / level-1 MLP launches (FpsSide)
+    rc = gp_launch_fps_chain(pts, B, 1, c.nin, c.mout, (int* const*)c.fidx, (float* const*)c.nxyz, st);
+    if (rc) return rc;
+    for (int l = 0; l < 5; ++l) {
+        const float* fprev = l == 0 ? nullptr : reinterpret_cast<const float*>(c.ws + c.L.feat[l - 1]);
+        float* out = l < 4 ? reinterpret_cast<float*>(c.ws + c.L.feat[l]) : feat;
+        rc = run_sa_level(c, l, l == 0 ? 0 : kCout[l - 1], fprev, out, true, st);
         if (rc) return rc;
     }
     return GP_OK;
+}
+
+extern "C" int gp_encoder_fps(const float* pts, int B, int N, void* workspace, size_t workspace_bytes, hipStream_t st) {
+    const float dummy = 0.f;
+    const int64_t tab = 0;
+    int rc = enc_check(&dummy, &tab, pts, B, N, workspace, workspace_bytes);
+    if (rc) return rc;
+    const EncCtx c = enc_ctx(nullptr, nullptr, pts, B, N, workspace);
+    return gp_launch_fps_chain(pts, B, 4, c.nin, c.mout, (int* const*)c.fidx, (float* const*)c.nxyz, st);
+}
+
+extern "C" int gp_sa_level(const float* wbuf, const int64_t* layer_off, int level, int c_prev, const float* pts, int B,
+                           int N, const float* feat_prev, void* workspace, size_t workspace_bytes, float* out,
+                           hipStream_t st) {
+    int rc = enc_check(wbuf, layer_off, pts, B, N, workspace, workspace_bytes);
+    if (rc) return rc;
+    GP_REQUIRE(level >= 0 && level < 5 && out, "sa_level: level %d out of range or null out", level);
+    GP_REQUIRE(level == 0 ? (c_prev % 16 == 0 && c_prev >= 0 && c_prev <= 1024) : c_prev == kCout[level - 1],
+               "sa_level: level %d takes c_prev = %d (got %d)", level, level ? kCout[level - 1] : 0, c_prev);
+    GP_REQUIRE(c_prev == 0 || feat_prev, "sa_level: c_prev %d needs feat_prev", c_prev);
+    const EncCtx c = enc_ctx(wbuf, layer_off, pts, B, N, workspace);
+    return run_sa_level(c, level, c_prev, feat_prev, out, false, st);
 }

@@ -1,0 +1,443 @@
+// Blocks of the DINO-pointwise fused encoder (Pointnet2ClsMSGFus, networks/pts_encoder/pointnet2.py:255-388)
+// that sit between its SA levels, for gfx950:
+//   * token linears (nn.Linear / Conv1d k=1, BN folded on the host) as exact-fp32 MFMA GEMMs;
+//   * residual + LayerNorm (TransformerBlockWithRelativePE, attention.py:505-533);
+//   * the relative-PE bias of EfficientRelativePositionalEncoding (attention.py:680-735), all 8 heads of
+//     a point pair from one evaluation of its distance / direction MLPs;
+//   * biased multi-head attention (MultiheadAttentionWithRelativePE, attention.py:436-488) with the
+//     head's K and V staged in LDS and torch's two-pass softmax order (max, then exp / sum);
+//   * GatedAttentionFusion's channel / spatial attention and gating (attention.py:284-325).
+// Token tensors are point-major (b, n, C): the reference's (b, C, n) transposed, so one token's channels
+// are contiguous and every linear is a row-major GEMM over b*n rows.
+#include "gp_common.h"
+
+constexpr int FUS_THREADS = 256;
+constexpr int FUS_HEADS = 8;
+
+__device__ __forceinline__ float sigmoidf(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+// ============================================================================ token linear (MFMA)
+// y[r, o] = act(sum_k x[r, k] w[o, k] + bias[o]). 4 waves as 2 (tokens) x 2 (outputs); a wave owns TM
+// token tiles x TN output tiles of 16. MFMA A = w rows (output channels), B = x rows (tokens): lane
+// (q, r) feeds float4 k-slices 16g + 4q .. +3 of row r of both, so one 16-deep k-group is 4 MFMAs per
+// tile pair and the accumulator holds 4 consecutive output channels of one token (a float4 store).
+template <int TM, int TN, int ACT>
+__global__ __launch_bounds__(FUS_THREADS) void linear_kernel(const float* __restrict__ x, int ldx, int m, int k,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ bias, int n,
+                                                             float* __restrict__ y, int ldy) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int q = lane >> 4, r = lane & 15;
+    const int tok0 = blockIdx.x * (32 * TM) + (wid & 1) * (16 * TM);
+    const int ot0 = blockIdx.y * (2 * TN) + (wid >> 1) * TN;   // first output tile of this wave
+    const int ntile = n >> 4;
+    const float* xp[TM];
+    const float* wp[TN];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) xp[t] = x + (size_t)min(tok0 + 16 * t + r, m - 1) * ldx + 4 * q;
+#pragma unroll
+    for (int u = 0; u < TN; ++u) wp[u] = w + (size_t)(16 * min(ot0 + u, ntile - 1) + r) * k + 4 * q;
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+        for (int t = 0; t < TM; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int KG = k >> 4;
+    f32x4 xa[TM], wa[TN];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) xa[t] = ld4(xp[t]);
+#pragma unroll
+    for (int u = 0; u < TN; ++u) wa[u] = ld4(wp[u]);
+    for (int g = 0; g < KG; ++g) {
+        f32x4 xb[TM], wb[TN];
+        const int gn = (g + 1 < KG ? g + 1 : g) * 16;
+#pragma unroll
+        for (int t = 0; t < TM; ++t) xb[t] = ld4(xp[t] + gn);
+#pragma unroll
+        for (int u = 0; u < TN; ++u) wb[u] = ld4(wp[u] + gn);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int u = 0; u < TN; ++u)
+#pragma unroll
+                for (int t = 0; t < TM; ++t) acc[u][t] = mfma4(wa[u][j], xa[t][j], acc[u][t]);
+#pragma unroll
+        for (int t = 0; t < TM; ++t) xa[t] = xb[t];
+#pragma unroll
+        for (int u = 0; u < TN; ++u) wa[u] = wb[u];
+    }
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+        const int T = ot0 + u;
+        if (T >= ntile) continue;
+        const f32x4 bv = bias ? ld4(bias + 16 * T + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+            const int tok = tok0 + 16 * t + r;
+            if (tok >= m) continue;
+            f32x4 v = acc[u][t] + bv;
+            if (ACT == 1) v = relu4(v);
+            if (ACT == 2) v = f32x4{sigmoidf(v.x), sigmoidf(v.y), sigmoidf(v.z), sigmoidf(v.w)};
+            st4(y + (size_t)tok * ldy + 16 * T + 4 * q, v);
+        }
+    }
+}
+
+template <int TN, int ACT>
+static void launch_linear(const float* x, int ldx, int m, int k, const float* w, const float* bias, int n, float* y,
+                          int ldy, hipStream_t st) {
+    constexpr int TM = 2;
+    const dim3 grid((m + 32 * TM - 1) / (32 * TM), ((n >> 4) + 2 * TN - 1) / (2 * TN));
+    hipLaunchKernelGGL((linear_kernel<TM, TN, ACT>), grid, dim3(FUS_THREADS), 0, st, x, ldx, m, k, w, bias, n, y, ldy);
+}
+
+template <int TN>
+static void launch_linear_act(int act, const float* x, int ldx, int m, int k, const float* w, const float* bias, int n,
+                              float* y, int ldy, hipStream_t st) {
+    if (act == 0) launch_linear<TN, 0>(x, ldx, m, k, w, bias, n, y, ldy, st);
+    else if (act == 1) launch_linear<TN, 1>(x, ldx, m, k, w, bias, n, y, ldy, st);
+    else launch_linear<TN, 2>(x, ldx, m, k, w, bias, n, y, ldy, st);
+}
+
+extern "C" int gp_linear(const float* x, int ldx, int m, int k, const float* w, const float* bias, int n, int act,
+                         float* y, int ldy, hipStream_t st) {
+    GP_REQUIRE(x && w && y && m >= 0, "linear: null pointer");
+    GP_REQUIRE(k >= 16 && k % 16 == 0 && n >= 16 && n % 16 == 0, "linear: k=%d and n=%d must be multiples of 16", k, n);
+    GP_REQUIRE(ldx >= k && ldy >= n && ldx % 4 == 0 && ldy % 4 == 0, "linear: strides ldx=%d ldy=%d", ldx, ldy);
+    GP_REQUIRE(((uintptr_t)x | (uintptr_t)w | (uintptr_t)y | (uintptr_t)bias) % 16 == 0,
+               "linear: pointers must be 16-byte aligned");
+    GP_REQUIRE(act >= 0 && act <= 2, "linear: act %d", act);
+    if (!m) return GP_OK;
+    // output tiles per wave: the widest that divides n into whole workgroup columns
+    if (n % 128 == 0) launch_linear_act<4>(act, x, ldx, m, k, w, bias, n, y, ldy, st);
+    else if (n % 96 == 0) launch_linear_act<3>(act, x, ldx, m, k, w, bias, n, y, ldy, st);
+    else if (n % 64 == 0) launch_linear_act<2>(act, x, ldx, m, k, w, bias, n, y, ldy, st);
+    else launch_linear_act<1>(act, x, ldx, m, k, w, bias, n, y, ldy, st);
+    return gp_check_launch("linear_kernel");
+}
+
+// ============================================================================ residual + LayerNorm
+// One wave per row (d <= 1024: up to 16 values per lane in registers), torch's biased variance.
+__global__ __launch_bounds__(FUS_THREADS) void add_layernorm_kernel(const float* __restrict__ x,
+                                                                    const float* __restrict__ r, int m, int d,
+                                                                    const float* __restrict__ gamma,
+                                                                    const float* __restrict__ beta, float eps,
+                                                                    float* __restrict__ y) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (FUS_THREADS / 64) + (threadIdx.x >> 6);
+    if (row >= m) return;
+    const float* xr = x + (size_t)row * d;
+    const float* rr = r + (size_t)row * d;
+    float v[16];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int c = lane + 64 * i;
+        v[i] = c < d ? xr[c] + rr[c] : 0.f;
+        s += v[i];
+    }
+    const float mean = wave_sum(s) / (float)d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int c = lane + 64 * i;
+        const float u = c < d ? v[i] - mean : 0.f;
+        s2 += u * u;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)d + eps);
+    float* yr = y + (size_t)row * d;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int c = lane + 64 * i;
+        if (c < d) yr[c] = ((v[i] - mean) * rstd) * gamma[c] + beta[c];
+    }
+}
+
+extern "C" int gp_add_layernorm(const float* x, const float* r, int m, int d, const float* gamma, const float* beta,
+                                float eps, float* y, hipStream_t st) {
+    GP_REQUIRE(x && r && gamma && beta && y && m >= 0, "add_layernorm: null pointer");
+    GP_REQUIRE(d >= 1 && d <= 1024, "add_layernorm: d=%d not in [1, 1024]", d);
+    if (!m) return GP_OK;
+    hipLaunchKernelGGL(add_layernorm_kernel, dim3((m + 3) / 4), dim3(FUS_THREADS), 0, st, x, r, m, d, gamma, beta, eps,
+                       y);
+    return gp_check_launch("add_layernorm_kernel");
+}
+
+// ============================================================================ relative-PE bias
+// Packed pe (gp_relpe_bias in genpose_hip.h): distance Linear(1,16)/ReLU/Linear(16,8), direction
+// Linear(3,16)/ReLU/Linear(16,8), fusion Linear(16,8) over [distance | direction]. One thread per
+// pair (i, j) evaluates all 8 heads; for each head consecutive threads write consecutive j.
+__global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __restrict__ pe,
+                                                                 const float* __restrict__ xyz, int n,
+                                                                 float* __restrict__ bias) {
+#pragma clang fp contract(off)
+    __shared__ float sp[512];
+    for (int i = threadIdx.x; i < 504; i += FUS_THREADS) sp[i] = pe[i];
+    __syncthreads();
+    const int b = blockIdx.y;
+    const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
+    if (e >= (long long)n * n) return;
+    const int i = (int)(e / n), j = (int)(e - (long long)i * n);
+    const float* pi = xyz + ((size_t)b * n + i) * 3;
+    const float* pj = xyz + ((size_t)b * n + j) * 3;
+    const float rx = pj[0] - pi[0], ry = pj[1] - pi[1], rz = pj[2] - pi[2];   // xyz[j] - xyz[i]
+    const float dist = sqrtf((rx * rx + ry * ry) + rz * rz);
+    const float den = dist + 1e-7f;
+    const float dx = rx / den, dy = ry / den, dz = rz / den;
+    float hd[16], ho[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        hd[u] = fmaxf(dist * sp[u] + sp[16 + u], 0.f);
+        const float* w = sp + 168 + 3 * u;
+        ho[u] = fmaxf(((dx * w[0] + dy * w[1]) + dz * w[2]) + sp[216 + u], 0.f);
+    }
+    float cat[16];
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        float a = 0.f, c = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            a += hd[u] * sp[32 + 16 * h + u];
+            c += ho[u] * sp[232 + 16 * h + u];
+        }
+        cat[h] = a + sp[160 + h];
+        cat[8 + h] = c + sp[360 + h];
+    }
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        float f = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) f += cat[u] * sp[368 + 16 * h + u];
+        bias[(((size_t)b * FUS_HEADS + h) * n + i) * n + j] = f + sp[496 + h];
+    }
+}
+
+extern "C" size_t gp_relpe_bias_bytes(int b, int n) { return sizeof(float) * (size_t)b * FUS_HEADS * n * n; }
+
+extern "C" int gp_relpe_bias(const float* pe, const float* xyz, int b, int n, float* bias, hipStream_t st) {
+    GP_REQUIRE(pe && xyz && bias && b >= 0 && n >= 1 && n <= 4096, "relpe_bias: bad arguments");
+    if (!b) return GP_OK;
+    const long long pairs = (long long)n * n;
+    hipLaunchKernelGGL(relpe_bias_kernel, dim3((unsigned)((pairs + FUS_THREADS - 1) / FUS_THREADS), b),
+                       dim3(FUS_THREADS), 0, st, pe, xyz, n, bias);
+    return gp_check_launch("relpe_bias_kernel");
+}
+
+// ============================================================================ biased attention
+// Workgroup = (64 queries, head, object); 4 lanes per query, each holding HD4 = hd/4 channels of q and
+// of the output. The head's K and V (n x hd) are staged in LDS; every quad of a wave reads the same key
+// row (broadcast). Softmax as torch evaluates it: pass 1 the row max of s = q.k / sqrt(hd) + bias,
+// pass 2 p = exp(s - max), sum and sum p v; out = (sum p v) / sum.
+template <int HD4>
+__global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restrict__ qkv,
+                                                          const float* __restrict__ bias, int n, int d,
+                                                          float* __restrict__ out) {
+#pragma clang fp contract(off)
+    constexpr int HD = 4 * HD4;
+    extern __shared__ __attribute__((aligned(16))) float kv[];
+    float* sk = kv;
+    float* sv = kv + (size_t)n * HD;
+    const int h = blockIdx.y, b = blockIdx.z;
+    const size_t ld = 3 * (size_t)d;
+    const float* base = qkv + (size_t)b * n * ld;
+    for (int e = threadIdx.x; e < n * HD; e += FUS_THREADS) {
+        const int j = e / HD, c = e - (e / HD) * HD;
+        sk[e] = base[(size_t)j * ld + d + h * HD + c];
+        sv[e] = base[(size_t)j * ld + 2 * d + h * HD + c];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int part = lane & 3;
+    const int i = blockIdx.x * 64 + (threadIdx.x >> 2);
+    const int ii = i < n ? i : n - 1;
+    float qv[HD4], o[HD4];
+    const float* qp = base + (size_t)ii * ld + h * HD + part * HD4;
+#pragma unroll
+    for (int c = 0; c < HD4; ++c) {
+        qv[c] = qp[c];
+        o[c] = 0.f;
+    }
+    const float scale = sqrtf((float)HD);
+    const float* brow = bias ? bias + (((size_t)b * FUS_HEADS + h) * n + ii) * n : nullptr;
+    auto score = [&](int j) {
+        const float* kr = sk + (size_t)j * HD + part * HD4;
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < HD4; ++c) s += qv[c] * kr[c];
+        // quad sum (lanes 4t..4t+3), the same order in every lane
+        s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
+        s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
+        s = s / scale;
+        return brow ? s + brow[j] : s;
+    };
+    float mx = -INFINITY;
+    for (int j = 0; j < n; ++j) mx = fmaxf(mx, score(j));
+    float l = 0.f;
+    for (int j = 0; j < n; ++j) {
+        const float p = expf(score(j) - mx);
+        l += p;
+        const float* vr = sv + (size_t)j * HD + part * HD4;
+#pragma unroll
+        for (int c = 0; c < HD4; ++c) o[c] += p * vr[c];
+    }
+    if (i < n) {
+        float* op = out + ((size_t)b * n + i) * d + h * HD + part * HD4;
+#pragma unroll
+        for (int c = 0; c < HD4; ++c) op[c] = o[c] / l;
+    }
+}
+
+extern "C" int gp_mha_attention(const float* qkv, const float* bias, int b, int n, int d, float* out, hipStream_t st) {
+    GP_REQUIRE(qkv && out && b >= 0 && n >= 1, "mha_attention: bad arguments");
+    GP_REQUIRE(d % (4 * FUS_HEADS) == 0, "mha_attention: d=%d must be a multiple of 32", d);
+    if (!b) return GP_OK;
+    const int hd = d / FUS_HEADS;
+    const size_t lds = sizeof(float) * 2 * (size_t)n * hd;
+    GP_REQUIRE(lds <= 64 * 1024, "mha_attention: K/V of a head (%zu bytes) exceed 64 KiB", lds);
+    const dim3 grid((n + 63) / 64, FUS_HEADS, b);
+    switch (hd / 4) {
+        case 3: hipLaunchKernelGGL(mha_kernel<3>, grid, dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out); break;
+        case 8: hipLaunchKernelGGL(mha_kernel<8>, grid, dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out); break;
+        case 16: hipLaunchKernelGGL(mha_kernel<16>, grid, dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out); break;
+        case 32: hipLaunchKernelGGL(mha_kernel<32>, grid, dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out); break;
+        default: gp_set_error("mha_attention: head dim %d not in {12, 32, 64, 128}", hd); return GP_ERR_UNSUPPORTED;
+    }
+    return gp_check_launch("mha_kernel");
+}
+
+// ============================================================================ gated fusion
+// F.interpolate(linear, align_corners=False) along points (upsample_linear1d's source index and lambda).
+__global__ __launch_bounds__(FUS_THREADS) void interp_points_kernel(const float* __restrict__ x, int n_in, int c,
+                                                                    int n_out, float* __restrict__ y) {
+#pragma clang fp contract(off)
+    const int b = blockIdx.y;
+    const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
+    if (e >= (long long)n_out * c) return;
+    const int o = (int)(e / c), ch = (int)(e - (long long)o * c);
+    const float scale = (float)n_in / (float)n_out;
+    float src = scale * ((float)o + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+    int i0 = (int)src;
+    i0 = i0 < n_in - 1 ? i0 : n_in - 1;
+    const int i1 = i0 + (i0 < n_in - 1 ? 1 : 0);
+    float l1 = src - (float)i0;
+    l1 = fminf(fmaxf(l1, 0.f), 1.f);
+    const float l0 = 1.0f - l1;
+    const float* xb = x + (size_t)b * n_in * c;
+    y[((size_t)b * n_out + o) * c + ch] = l0 * xb[(size_t)i0 * c + ch] + l1 * xb[(size_t)i1 * c + ch];
+}
+
+extern "C" int gp_interp_points(const float* x, int b, int n_in, int c, int n_out, float* y, hipStream_t st) {
+    GP_REQUIRE(x && y && b >= 0 && n_in >= 1 && n_out >= 1 && c >= 1, "interp_points: bad arguments");
+    if (!b) return GP_OK;
+    const long long e = (long long)n_out * c;
+    hipLaunchKernelGGL(interp_points_kernel, dim3((unsigned)((e + FUS_THREADS - 1) / FUS_THREADS), b),
+                       dim3(FUS_THREADS), 0, st, x, n_in, c, n_out, y);
+    return gp_check_launch("interp_points_kernel");
+}
+
+// One workgroup per object: channel attention (AdaptiveAvgPool1d -> Conv1d -> ReLU -> Conv1d -> sigmoid)
+// of [cur | ot], spatial attention (sigmoid(Conv1d(2,1,7,pad 3)) over [max_c cur ; mean_c cur]), and
+// gcat = [cur | (ot * ca) * sp].
+__global__ __launch_bounds__(FUS_THREADS) void fusion_attend_kernel(const float* __restrict__ cur,
+                                                                    const float* __restrict__ ot, int n, int c,
+                                                                    const float* __restrict__ ca1_w,
+                                                                    const float* __restrict__ ca1_b,
+                                                                    const float* __restrict__ ca3_w,
+                                                                    const float* __restrict__ ca3_b,
+                                                                    const float* __restrict__ sp_w,
+                                                                    float* __restrict__ gcat) {
+#pragma clang fp contract(off)
+    __shared__ float colmean[2048];
+    __shared__ float hid[512];
+    __shared__ float ca[1024];
+    __shared__ float tmax[1024], tmean[1024], sp[1024];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const float* cb = cur + (size_t)b * n * c;
+    const float* ob = ot + (size_t)b * n * c;
+    const int c2 = 2 * c, cr = c2 / 4;
+    for (int ch = tid; ch < c2; ch += FUS_THREADS) {
+        const float* src = ch < c ? cb + ch : ob + (ch - c);
+        float s = 0.f;
+        for (int t = 0; t < n; ++t) s += src[(size_t)t * c];
+        colmean[ch] = s / (float)n;
+    }
+    // per-token max / mean over channels (a wave per token)
+    for (int t = wid; t < n; t += FUS_THREADS / 64) {
+        float mxv = -INFINITY, s = 0.f;
+        for (int ch = lane; ch < c; ch += 64) {
+            const float v = cb[(size_t)t * c + ch];
+            mxv = fmaxf(mxv, v);
+            s += v;
+        }
+        for (int off = 32; off >= 1; off >>= 1) mxv = fmaxf(mxv, __shfl_xor(mxv, off, 64));
+        s = wave_sum(s);
+        if (lane == 0) {
+            tmax[t] = mxv;
+            tmean[t] = s / (float)c;
+        }
+    }
+    __syncthreads();
+    for (int o = tid; o < cr; o += FUS_THREADS) {
+        const float* wr = ca1_w + (size_t)o * c2;
+        float s = 0.f;
+        for (int k = 0; k < c2; ++k) s += wr[k] * colmean[k];
+        hid[o] = fmaxf(s + ca1_b[o], 0.f);
+    }
+    for (int t = tid; t < n; t += FUS_THREADS) {
+        float s = 0.f;
+        for (int u = 0; u < 7; ++u) {
+            const int tt = t + u - 3;
+            if (tt >= 0 && tt < n) s += sp_w[u] * tmax[tt] + sp_w[7 + u] * tmean[tt];
+        }
+        sp[t] = sigmoidf(s);
+    }
+    __syncthreads();
+    for (int o = tid; o < c; o += FUS_THREADS) {
+        const float* wr = ca3_w + (size_t)o * cr;
+        float s = 0.f;
+        for (int k = 0; k < cr; ++k) s += wr[k] * hid[k];
+        ca[o] = sigmoidf(s + ca3_b[o]);
+    }
+    __syncthreads();
+    float* gb = gcat + (size_t)b * n * c2;
+    for (long long e = tid; e < (long long)n * c; e += FUS_THREADS) {
+        const int t = (int)(e / c), ch = (int)(e - (long long)t * c);
+        gb[(size_t)t * c2 + ch] = cb[e];
+        gb[(size_t)t * c2 + c + ch] = (ob[e] * ca[ch]) * sp[t];
+    }
+}
+
+extern "C" int gp_fusion_attend(const float* cur, const float* ot, int b, int n, int c, const float* ca1_w,
+                                const float* ca1_b, const float* ca3_w, const float* ca3_b, const float* sp_w,
+                                float* gcat, hipStream_t st) {
+    GP_REQUIRE(cur && ot && ca1_w && ca1_b && ca3_w && ca3_b && sp_w && gcat && b >= 0, "fusion_attend: null pointer");
+    GP_REQUIRE(n >= 1 && n <= 1024 && c >= 4 && c <= 1024 && c % 2 == 0, "fusion_attend: n=%d c=%d out of range", n, c);
+    if (!b) return GP_OK;
+    hipLaunchKernelGGL(fusion_attend_kernel, dim3(b), dim3(FUS_THREADS), 0, st, cur, ot, n, c, ca1_w, ca1_b, ca3_w,
+                       ca3_b, sp_w, gcat);
+    return gp_check_launch("fusion_attend_kernel");
+}
+
+__global__ __launch_bounds__(FUS_THREADS) void fusion_mix_kernel(const float* __restrict__ g,
+                                                                 const float* __restrict__ gcat, long long total,
+                                                                 int c, float* __restrict__ out) {
+#pragma clang fp contract(off)
+    const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
+    if (e >= total) return;
+    const long long r = e / c;
+    const int ch = (int)(e - r * c);
+    const float gv = g[e];
+    const float* row = gcat + (size_t)r * 2 * c;
+    out[e] = gv * row[ch] + (1.0f - gv) * row[c + ch];
+}
+
+extern "C" int gp_fusion_mix(const float* g, const float* gcat, int rows, int c, float* out, hipStream_t st) {
+    GP_REQUIRE(g && gcat && out && rows >= 0 && c >= 1, "fusion_mix: bad arguments");
+    const long long total = (long long)rows * c;
+    if (!total) return GP_OK;
+    hipLaunchKernelGGL(fusion_mix_kernel, dim3((unsigned)((total + FUS_THREADS - 1) / FUS_THREADS)), dim3(FUS_THREADS),
+                       0, st, g, gcat, total, c, out);
+    return gp_check_launch("fusion_mix_kernel");
+}

@@ -1,0 +1,188 @@
+"""DINO-pointwise fused encoder (``Pointnet2ClsMSGFus(384)``, networks/pts_encoder/pointnet2.py:255-388)
+on device.
+
+The reference selects it with ``--dino pointwise`` (posenet.py:75-77): its point-cloud input is
+``concat([pts, rgb_feat])`` with ``rgb_feat (B, N, 384)`` the per-point DINOv3 features gathered at the
+points' image patches (posenet.py:136-197). The DINOv3 backbone and ImgEncoder need weights that are not
+available, so this model starts from ``rgb_feat``; everything after it runs here:
+
+* SA levels: ``gp_encoder_fps`` + ``gp_sa_level`` (the Light levels with 384 image channels entering
+  level 0);
+* after every level, TransformerBlockWithRelativePE (attention.py:491-533): fused QKV ``gp_linear``,
+  the EfficientRelativePositionalEncoding bias (``gp_relpe_bias``, attention.py:680-735),
+  ``gp_mha_attention``, ``gp_linear`` (wo), ``gp_add_layernorm``, the FFN (``gp_linear`` x2), LayerNorm;
+* before levels 1..4, GatedAttentionFusion (attention.py:284-325) of the level input with the image
+  features interpolated along the point index (pointnet2.py:343-354): ``gp_interp_points``, the
+  BN-folded original_transform / gate / output_conv as ``gp_linear``, ``gp_fusion_attend``,
+  ``gp_fusion_mix``. Dropout is the identity (eval).
+
+Token tensors are point-major (B, n, C). The reference's dead gather of ``features`` at the end of each
+level (pointnet2.py:370-377) is not executed.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib, arch, pack, weights
+from ._lib import check
+from .device import require_device_tensor, stream_handle
+
+_ACT = {"none": 0, "relu": 1, "sigmoid": 2}
+
+
+def _vp(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(None if t is None else t.data_ptr())
+
+
+def pack_relpe(sd: weights.StateDict, prefix: str) -> np.ndarray:
+    """The 512-float layout gp_relpe_bias reads (include/genpose_hip.h)."""
+    g = lambda k: np.asarray(sd[f"{prefix}.{k}"], np.float32).reshape(-1)  # noqa: E731
+    out = np.zeros(512, np.float32)
+    parts = [g("distance_encoder.0.weight"), g("distance_encoder.0.bias"), g("distance_encoder.2.weight"),
+             g("distance_encoder.2.bias"), g("direction_encoder.0.weight"), g("direction_encoder.0.bias"),
+             g("direction_encoder.2.weight"), g("direction_encoder.2.bias"), g("fusion.weight"), g("fusion.bias")]
+    v = np.concatenate(parts)
+    assert v.size == 504
+    out[:504] = v
+    return out
+
+
+def pack_fus_blocks(sd: weights.StateDict) -> Dict[str, np.ndarray]:
+    """Transformer, relative-PE and gated-fusion parameters, row-major fp32 (BN folded into the fusion convs)."""
+    out: Dict[str, np.ndarray] = {}
+    p = "pts_encoder."
+    for lv in range(arch.N_LEVELS):
+        t = f"{p}transformer_blocks.{lv}"
+        out[f"tf{lv}.qkv.w"] = np.concatenate([sd[f"{t}.self_attn.{n}.weight"] for n in ("wq", "wk", "wv")])
+        out[f"tf{lv}.qkv.b"] = np.concatenate([sd[f"{t}.self_attn.{n}.bias"] for n in ("wq", "wk", "wv")])
+        out[f"tf{lv}.wo.w"], out[f"tf{lv}.wo.b"] = sd[f"{t}.self_attn.wo.weight"], sd[f"{t}.self_attn.wo.bias"]
+        for k in ("linear1", "linear2", "norm1", "norm2"):
+            out[f"tf{lv}.{k}.w"], out[f"tf{lv}.{k}.b"] = sd[f"{t}.{k}.weight"], sd[f"{t}.{k}.bias"]
+        out[f"pe{lv}"] = pack_relpe(sd, f"{p}relative_pos_encoders.{lv}")
+    for k in range(1, arch.N_LEVELS):
+        g = f"{p}feature_fusions.{k - 1}"
+        for m in ("original_transform", "gate", "output_conv"):
+            out[f"fu{k}.{m}.w"], out[f"fu{k}.{m}.b"] = weights.fold_conv1d_bn(sd, f"{g}.{m}")
+        out[f"fu{k}.ca1.w"] = sd[f"{g}.channel_attention.1.weight"][:, :, 0]
+        out[f"fu{k}.ca1.b"] = sd[f"{g}.channel_attention.1.bias"]
+        out[f"fu{k}.ca3.w"] = sd[f"{g}.channel_attention.3.weight"][:, :, 0]
+        out[f"fu{k}.ca3.b"] = sd[f"{g}.channel_attention.3.bias"]
+        out[f"fu{k}.sp.w"] = sd[f"{g}.spatial_attention.0.weight"].reshape(2, arch.FUS_SPATIAL_K)
+    return {k: np.ascontiguousarray(v, np.float32) for k, v in out.items()}
+
+
+class FusEncoderModel:
+    """Pointnet2ClsMSGFus(384) on device: forward(pts (B,N,3), rgb_feat (B,N,384)) -> (B, 1024)."""
+
+    def __init__(self, sd: weights.StateDict, device: torch.device):
+        self.lib = _lib.load()
+        self.device = device
+        buf, offs = pack.pack_encoder(sd, arch.fus_sa_branches())
+        self.wbuf = torch.from_numpy(buf).to(device)
+        self.offsets = np.ascontiguousarray(offs.reshape(-1), np.int64)
+        self.t = {k: torch.from_numpy(v).to(device) for k, v in pack_fus_blocks(sd).items()}
+        self._ws: Optional[torch.Tensor] = None
+        self._bias: Optional[torch.Tensor] = None
+
+    def _s(self):
+        return ctypes.c_void_p(stream_handle(self.device))
+
+    # ------------------------------------------------------------ primitives
+    def linear(self, x: torch.Tensor, w: str, act: str = "none", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        W, b = self.t[f"{w}.w"], self.t[f"{w}.b"]
+        lead, k = x.shape[:-1], x.shape[-1]
+        m = int(np.prod(lead)) if lead else 1
+        n = W.shape[0]
+        y = torch.empty(lead + (n,), dtype=torch.float32, device=self.device) if out is None else out
+        check(self.lib.gp_linear(_vp(x), k, m, k, _vp(W), _vp(b), n, _ACT[act], _vp(y), n, self._s()), f"linear {w}")
+        return y
+
+    def add_ln(self, x: torch.Tensor, r: torch.Tensor, name: str) -> torch.Tensor:
+        d = x.shape[-1]
+        y = torch.empty_like(x)
+        check(self.lib.gp_add_layernorm(_vp(x), _vp(r), x.numel() // d, d, _vp(self.t[f"{name}.w"]),
+                                        _vp(self.t[f"{name}.b"]), ctypes.c_float(arch.LN_EPS), _vp(y), self._s()),
+              f"add_layernorm {name}")
+        return y
+
+    def transformer(self, lv: int, x: torch.Tensor, xyz: Optional[torch.Tensor]) -> torch.Tensor:
+        """TransformerBlockWithRelativePE.forward (attention.py:505-533), eval mode."""
+        B, n, d = x.shape
+        bias = None
+        if xyz is not None:
+            need = int(self.lib.gp_relpe_bias_bytes(B, n)) // 4
+            if self._bias is None or self._bias.numel() < need:
+                self._bias = torch.empty(need, dtype=torch.float32, device=self.device)
+            bias = self._bias
+            check(self.lib.gp_relpe_bias(_vp(self.t[f"pe{lv}"]), _vp(xyz), B, n, _vp(bias), self._s()), "relpe_bias")
+        qkv = self.linear(x, f"tf{lv}.qkv")
+        att = torch.empty_like(x)
+        check(self.lib.gp_mha_attention(_vp(qkv), _vp(bias), B, n, d, _vp(att), self._s()), "mha_attention")
+        x1 = self.add_ln(x, self.linear(att, f"tf{lv}.wo"), f"tf{lv}.norm1")
+        f = self.linear(self.linear(x1, f"tf{lv}.linear1", "relu"), f"tf{lv}.linear2")
+        return self.add_ln(x1, f, f"tf{lv}.norm2")
+
+    def fusion(self, k: int, cur: torch.Tensor, orig: torch.Tensor) -> torch.Tensor:
+        """GatedAttentionFusion.forward (attention.py:284-325) with orig already at cur's point count."""
+        B, n, c = cur.shape
+        ot = self.linear(orig, f"fu{k}.original_transform", "relu")
+        gcat = torch.empty((B, n, 2 * c), dtype=torch.float32, device=self.device)
+        t = self.t
+        check(self.lib.gp_fusion_attend(_vp(cur), _vp(ot), B, n, c, _vp(t[f"fu{k}.ca1.w"]), _vp(t[f"fu{k}.ca1.b"]),
+                                        _vp(t[f"fu{k}.ca3.w"]), _vp(t[f"fu{k}.ca3.b"]), _vp(t[f"fu{k}.sp.w"]),
+                                        _vp(gcat), self._s()), "fusion_attend")
+        g = self.linear(gcat, f"fu{k}.gate", "sigmoid")
+        fused = torch.empty_like(cur)
+        check(self.lib.gp_fusion_mix(_vp(g), _vp(gcat), B * n, c, _vp(fused), self._s()), "fusion_mix")
+        return self.linear(fused, f"fu{k}.output_conv", "relu")
+
+    def interp(self, x: torch.Tensor, n_out: int) -> torch.Tensor:
+        B, n_in, c = x.shape
+        y = torch.empty((B, n_out, c), dtype=torch.float32, device=self.device)
+        check(self.lib.gp_interp_points(_vp(x), B, n_in, c, n_out, _vp(y), self._s()), "interp_points")
+        return y
+
+    # ------------------------------------------------------------ forward
+    def workspace(self, b: int, n: int) -> torch.Tensor:
+        need = int(self.lib.gp_encoder_workspace_size(b, n))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def forward(self, pts: torch.Tensor, rgb_feat: torch.Tensor, return_levels: bool = False):
+        pts = require_device_tensor(pts, "pts")
+        rgb_feat = require_device_tensor(rgb_feat, "rgb_feat")
+        B, N, C = pts.shape
+        if C != 3:
+            pts = pts[..., :3].contiguous()
+        if tuple(rgb_feat.shape) != (B, N, arch.DINO_DIM):
+            raise ValueError(f"rgb_feat must be ({B}, {N}, {arch.DINO_DIM}), got {tuple(rgb_feat.shape)}")
+        ws = self.workspace(B, N)
+        check(self.lib.gp_encoder_fps(_vp(pts), B, N, _vp(ws), ws.numel(), self._s()), "encoder_fps")
+        off = np.zeros(25, np.int64)
+        check(self.lib.gp_encoder_workspace_layout(B, N, off.ctypes.data_as(_lib.c_int64_p)))
+        orig, feats = rgb_feat, rgb_feat
+        levels: List[dict] = []
+        for lv in range(arch.N_LEVELS):
+            rec = {}
+            if lv > 0:
+                if orig.shape[1] != feats.shape[1]:
+                    orig = self.interp(orig, feats.shape[1])
+                feats = self.fusion(lv, feats, orig)
+                rec["fused"] = feats
+            m = arch.NPOINTS[lv] if lv < 4 else 1
+            cout = arch.level_out_channels(lv)
+            sa = torch.empty((B, m, cout), dtype=torch.float32, device=self.device)
+            check(self.lib.gp_sa_level(_vp(self.wbuf), self.offsets.ctypes.data_as(_lib.c_int64_p), lv, feats.shape[2],
+                                       _vp(pts), B, N, _vp(feats), _vp(ws), ws.numel(), _vp(sa), self._s()),
+                  f"sa_level {lv}")
+            xyz = ws[off[lv * 5 + 1]:].view(torch.float32)[: B * m * 3].view(B, m, 3) if lv < 4 else None
+            feats = self.transformer(lv, sa, xyz)
+            rec.update(sa=sa, tf=feats)
+            levels.append(rec)
+        out = feats.reshape(B, arch.PTS_FEAT_DIM)
+        return (out, levels) if return_levels else out

@@ -53,7 +53,7 @@ def pad32(v: int) -> int:
     return (v + 31) // 32 * 32
 
 
-def pack_encoder(sd: weights.StateDict) -> Tuple[np.ndarray, np.ndarray]:
+def pack_encoder(sd: weights.StateDict, levels=None) -> Tuple[np.ndarray, np.ndarray]:
     """All SA layers, BN folded, into one flat float32 buffer + int64 table [5][2][3][4]:
     [0] offset of the fp32 A fragments, [1] offset of the bias (padded to 32), [2] offset of the
     split-f16 planes (levels 2-3, layers 1-2; -1 elsewhere), [3] their power-of-two exponent.
@@ -63,7 +63,8 @@ def pack_encoder(sd: weights.StateDict) -> Tuple[np.ndarray, np.ndarray]:
     K padded to C + 16, matching the kernel's gathered B operand. The split planes
     (pack_h16_fragments) pad every output count and input depth to 32, the chunk of
     v_mfma_f32_16x16x32_f16 (level 2: 196 channels -> 224)."""
-    folded = weights.encoder_layers(sd)
+    levels = arch.sa_branches() if levels is None else levels
+    folded = weights.encoder_layers(sd, levels)
     chunks: List[np.ndarray] = []
     offsets = np.full((5, 2, 3, 4), -1, np.int64)
     pos = 0
@@ -83,8 +84,8 @@ def pack_encoder(sd: weights.StateDict) -> Tuple[np.ndarray, np.ndarray]:
             pos += padn
         return o
 
-    for lv, branches in enumerate(arch.sa_branches()):
-        c_prev = 0 if lv == 0 else arch.level_out_channels(lv - 1)
+    for lv, branches in enumerate(levels):
+        c_prev = branches[0].widths[0] - 3      # input feature channels (the level-0 image features: 384)
         for br in branches:
             for i, (W, b) in enumerate(folded[lv][br.branch]):
                 if i == 0:

@@ -38,6 +38,8 @@ def model_tensors(agent) -> List[torch.Tensor]:
     out = []
     if getattr(agent, "encoder", None) is not None:
         out.append(agent.encoder.wbuf)
+        if hasattr(agent.encoder, "t"):      # fused encoder (--dino pointwise): transformer / fusion blocks
+            out += [agent.encoder.t[k] for k in sorted(agent.encoder.t)]
         out += [agent.heads.up.t[k] for k in sorted(agent.heads.up.t)]
     if getattr(agent, "scale", None) is not None:
         out += [agent.scale.up.t[k] for k in sorted(agent.scale.up.t)]
@@ -52,8 +54,15 @@ def packed_host_tensors(kind: str, sd) -> List[torch.Tensor]:
         p = pack.pack_scale(sd)
         return [torch.from_numpy(np.ascontiguousarray(p[k])) for k in sorted(p)]
     p = pack.pack_heads(sd)
-    return [torch.from_numpy(pack.pack_encoder(sd)[0])] + [torch.from_numpy(np.ascontiguousarray(p[k]))
-                                                           for k in sorted(p)]
+    if kind.endswith("_pointwise"):
+        from . import arch
+        from .fus_encoder import pack_fus_blocks
+        f = pack_fus_blocks(sd)
+        enc = [torch.from_numpy(pack.pack_encoder(sd, arch.fus_sa_branches())[0])] + \
+            [torch.from_numpy(f[k]) for k in sorted(f)]
+    else:
+        enc = [torch.from_numpy(pack.pack_encoder(sd)[0])]
+    return enc + [torch.from_numpy(np.ascontiguousarray(p[k])) for k in sorted(p)]
 
 
 def gather_outputs(outputs: Dict[str, Optional[torch.Tensor]], total: int, dst: Optional[int] = None

@@ -203,10 +203,11 @@ def fold_conv_bn(sd: StateDict, prefix: str) -> Tuple[np.ndarray, np.ndarray]:
     return (w * scale[:, None]).astype(np.float32), (be - mu * scale).astype(np.float32)
 
 
-def encoder_layers(sd: StateDict) -> List[List[List[Tuple[np.ndarray, np.ndarray]]]]:
-    """[level][branch][layer] -> (W_folded (out,in), b_folded (out,))."""
+def encoder_layers(sd: StateDict, levels=None) -> List[List[List[Tuple[np.ndarray, np.ndarray]]]]:
+    """[level][branch][layer] -> (W_folded (out,in), b_folded (out,)); `levels` = arch.sa_branches() (default)
+    or arch.fus_sa_branches() (the fused encoder's SA levels)."""
     out = []
-    for lv, branches in enumerate(arch.sa_branches()):
+    for lv, branches in enumerate(arch.sa_branches() if levels is None else levels):
         lvl = []
         for br in branches:
             layers = []
@@ -236,3 +237,16 @@ def head_params(sd: StateDict) -> Dict[str, np.ndarray]:
     p["h2_w"] = np.stack([sd[f"{n}.{h}.2.weight"] for h in arch.HEAD_NAMES])  # (3,3,256)
     p["h2_b"] = np.stack([sd[f"{n}.{h}.2.bias"] for h in arch.HEAD_NAMES])    # (3,3)
     return {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in p.items()}
+
+
+def fold_conv1d_bn(sd: StateDict, prefix: str) -> Tuple[np.ndarray, np.ndarray]:
+    """Conv1d k=1 with bias -> BatchNorm1d(eval) (the Sequential(Conv1d, BatchNorm1d, act) blocks of
+    GatedAttentionFusion, attention.py:262-281) folded in float64: W' = s W, b' = s (b - mean) + beta."""
+    w = sd[f"{prefix}.0.weight"].astype(np.float64)[:, :, 0]
+    b = sd[f"{prefix}.0.bias"].astype(np.float64)
+    g = sd[f"{prefix}.1.weight"].astype(np.float64)
+    be = sd[f"{prefix}.1.bias"].astype(np.float64)
+    mu = sd[f"{prefix}.1.running_mean"].astype(np.float64)
+    var = sd[f"{prefix}.1.running_var"].astype(np.float64)
+    s = g / np.sqrt(var + arch.BN_EPS)
+    return (w * s[:, None]).astype(np.float32), (s * (b - mu) + be).astype(np.float32)

@@ -30,7 +30,7 @@ enum { GP_OK = 0, GP_ERR_INVALID = -1, GP_ERR_LAUNCH = -2, GP_ERR_UNSUPPORTED = 
 const char *gp_last_error(void);
 /* ABI version of this header. */
 int gp_abi_version(void);
-#define GP_ABI_VERSION 4
+#define GP_ABI_VERSION 5
 
 /* ===================================================================== operator level
  * Drop-in forward ops of `pointnet2_cuda` (same argument meaning and layouts). */
@@ -73,6 +73,58 @@ int gp_encoder_workspace_layout(int b, int n, int64_t *offsets);
 /* pts (b,n,3) un-centred points -> feat (b,1024). */
 int gp_encoder_forward(const float *wbuf, const int64_t *layer_off, const float *pts, int b, int n,
                        void *workspace, size_t workspace_bytes, float *feat, hipStream_t stream);
+/* Level-by-level form (the fused encoders, whose levels take features computed between levels):
+ * gp_encoder_fps runs the FPS chain of all four levels into the workspace (fps idx + new_xyz, as
+ * gp_encoder_workspace_layout places them); gp_sa_level then runs SA level `level`
+ * (PointnetSAModuleMSG.forward, pointnet2_modules.py:19-124: ball query of both radii, group, the
+ * BN-folded SharedMLPs, max-pool) on its input features feat_prev (b, n_prev, c_prev) point-major
+ * (NULL with c_prev = 0 at level 0) -> out (b, M_level, C_level) point-major (level 4: (b, 1024)).
+ * c_prev: level 0 any multiple of 16 (Pointnet2ClsMSGFus: 384, pointnet2.py:281-285), level l > 0
+ * the previous level's channels. `wbuf`/`layer_off` as gp_encoder_forward, packed for those widths. */
+int gp_encoder_fps(const float *pts, int b, int n, void *workspace, size_t workspace_bytes,
+                   hipStream_t stream);
+int gp_sa_level(const float *wbuf, const int64_t *layer_off, int level, int c_prev, const float *pts,
+                int b, int n, const float *feat_prev, void *workspace, size_t workspace_bytes,
+                float *out, hipStream_t stream);
+
+/* ===================================================================== fused-encoder blocks
+ * The DINO-pointwise encoder Pointnet2ClsMSGFus (pointnet2.py:255-388) between SA levels:
+ * TransformerBlockWithRelativePE (attention.py:491-533) with the EfficientRelativePositionalEncoding
+ * bias (attention.py:648-735), and GatedAttentionFusion (attention.py:224-325). Token tensors are
+ * point-major (b, n, C) fp32, i.e. the reference's (b, C, n) transposed. */
+/* y[r, :] = act(x[r, :k] . w^T + bias), r < m; w (n, k) row-major (nn.Linear / Conv1d k=1 layout),
+ * k and n multiples of 16; ldx / ldy = row strides of x / y (>= k / n). act: 0 none, 1 ReLU,
+ * 2 sigmoid. Exact fp32 MFMA (v_mfma_f32_16x16x4_f32). */
+int gp_linear(const float *x, int ldx, int m, int k, const float *w, const float *bias, int n,
+              int act, float *y, int ldy, hipStream_t stream);
+/* y = LayerNorm(x + r) over the last dim d (gamma, beta, eps), m rows; y may alias x. */
+int gp_add_layernorm(const float *x, const float *r, int m, int d, const float *gamma,
+                     const float *beta, float eps, float *y, hipStream_t stream);
+/* Relative-PE bias of EfficientRelativePositionalEncoding (8 heads): xyz (b, n, 3) ->
+ * bias (b, 8, n, n), bias[b,h,i,j] from rel = xyz[j] - xyz[i]. pe (host-packed, 512 floats):
+ * [0:16) dist.0.w, [16:32) dist.0.b, [32:160) dist.2.w (8x16), [160:168) dist.2.b,
+ * [168:216) dir.0.w (16x3), [216:232) dir.0.b, [232:360) dir.2.w, [360:368) dir.2.b,
+ * [368:496) fusion.w (8x16), [496:504) fusion.b. */
+size_t gp_relpe_bias_bytes(int b, int n);
+int gp_relpe_bias(const float *pe, const float *xyz, int b, int n, float *bias, hipStream_t stream);
+/* Multi-head attention with an additive bias (MultiheadAttentionWithRelativePE core,
+ * attention.py:436-488, eval): qkv (b, n, 3d) rows [q | k | v] (heads of d/8 channels),
+ * bias (b, 8, n, n) or NULL -> out (b, n, d) = softmax(q k^T / sqrt(d/8) + bias) v per head. */
+int gp_mha_attention(const float *qkv, const float *bias, int b, int n, int d, float *out,
+                     hipStream_t stream);
+/* F.interpolate(mode="linear", align_corners=False) along the point index: x (b, n_in, c) ->
+ * y (b, n_out, c) (pointnet2.py:344-350). */
+int gp_interp_points(const float *x, int b, int n_in, int c, int n_out, float *y, hipStream_t stream);
+/* GatedAttentionFusion's attention stage (attention.py:298-313) per object: cur (b, n, c), ot (b, n, c)
+ * (original_transform output) -> gcat (b, n, 2c) = [cur | ot * ca * sp] with ca = channel attention
+ * of mean_n [cur | ot] (ca1: (2c/4, 2c) + bias, ReLU, ca3: (c, 2c/4) + bias, sigmoid) and sp =
+ * sigmoid(conv1d_7([max_c cur ; mean_c cur])) (sp_w: (2, 7), zero padding 3). c <= 1024, n <= 1024. */
+int gp_fusion_attend(const float *cur, const float *ot, int b, int n, int c, const float *ca1_w,
+                     const float *ca1_b, const float *ca3_w, const float *ca3_b, const float *sp_w,
+                     float *gcat, hipStream_t stream);
+/* fused = g * cur + (1 - g) * att with cur = gcat[:, :c], att = gcat[:, c:] (attention.py:318-320):
+ * g (rows, c), gcat (rows, 2c) -> out (rows, c). */
+int gp_fusion_mix(const float *g, const float *gcat, int rows, int c, float *out, hipStream_t stream);
 
 /* ===================================================================== score / energy heads
  * PoseScoreNet / PoseEnergyNet with Rx_Ry_and_T heads (scorenet.py:109-275, energynet.py:32-208),

@@ -1,0 +1,240 @@
+"""DINO-pointwise fused encoder (Pointnet2ClsMSGFus) on a real MI355X, through the C ABI.
+
+Each block is held to a CPU fp32 statement of the same op (torch CPU / the oracle), and the whole encoder
+to the reference's own per-level outputs (golden_fus.npz, tests/golden/make_golden_fus.py). Tolerances:
+FPS indices bit-exact; fp32 block outputs within 1e-5 of max|ref| (attention and LayerNorm chains
+2e-5); the full encoder within 1e-5 of max|ref| per level.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as tf
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def rel(a, b):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else b
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _vp(t):
+    return ctypes.c_void_p(None if t is None else t.data_ptr())
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from genpose2_amd import _lib
+    return _lib.load()
+
+
+@pytest.fixture(scope="module")
+def fus_sd():
+    from genpose2_amd import weights
+    return weights.synthetic_state_dict("score_pointwise", seed=0)
+
+
+@pytest.fixture(scope="module")
+def fus_model(fus_sd):
+    from genpose2_amd.fus_encoder import FusEncoderModel
+    return FusEncoderModel(fus_sd, torch.device(DEV))
+
+
+# ---------------------------------------------------------------- blocks
+@pytest.mark.parametrize("m,k,n,act,pad", [(100, 96, 288, 0, 0), (4096, 256, 1024, 1, 0), (37, 384, 96, 2, 0),
+                                           (513, 1024, 192, 1, 32), (64, 2048, 1024, 0, 16), (1, 1024, 3072, 0, 0)])
+def test_linear_vs_torch(lib, m, k, n, act, pad):
+    from genpose2_amd._lib import check
+    g = torch.Generator().manual_seed(m + k + n)
+    x = torch.randn(m, k + pad, generator=g)
+    w = torch.randn(n, k, generator=g) / k ** 0.5
+    b = torch.randn(n, generator=g)
+    ref = tf.linear(x[:, :k].double(), w.double(), b.double())
+    ref = [ref, torch.relu(ref), torch.sigmoid(ref)][act].float()
+    y = torch.zeros(m, n + pad, device=DEV)
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    check(lib.gp_linear(_vp(xd), k + pad, m, k, _vp(wd), _vp(bd), n, act, _vp(y), n + pad, _s()), "linear")
+    torch.cuda.synchronize()
+    assert rel(y[:, :n], ref) < 1e-5
+    if pad:
+        assert torch.all(y[:, n:] == 0)          # ldy: nothing written past n
+
+
+def test_add_layernorm_vs_torch(lib):
+    from genpose2_amd._lib import check
+    for m, d in ((777, 96), (300, 1024), (5, 512), (64, 256)):
+        g = torch.Generator().manual_seed(d)
+        x, r = torch.randn(m, d, generator=g) * 3, torch.randn(m, d, generator=g)
+        gam, bet = torch.rand(d, generator=g) + 0.5, torch.randn(d, generator=g) * 0.1
+        ref = tf.layer_norm(x + r, (d,), gam, bet, 1e-5)
+        y = torch.empty(m, d, device=DEV)
+        xd, rd, gd, bd = (t.to(DEV) for t in (x, r, gam, bet))    # held: the call only enqueues
+        check(lib.gp_add_layernorm(_vp(xd), _vp(rd), m, d, _vp(gd), _vp(bd), ctypes.c_float(1e-5), _vp(y), _s()),
+              "add_layernorm")
+        torch.cuda.synchronize()
+        assert rel(y, ref) < 2e-6, (m, d)
+
+
+@pytest.mark.parametrize("n", [64, 100, 512])
+def test_relpe_bias_vs_oracle(lib, fus_sd, n):
+    from genpose2_amd._lib import check
+    from genpose2_amd.fus_encoder import pack_relpe
+    from oracle import oracle
+    rng = np.random.default_rng(n)
+    xyz = rng.uniform(-0.1, 0.1, size=(2, n, 3)).astype(np.float32)
+    xyz[1, 5] = xyz[1, 3]                          # a duplicate point: zero distance off the diagonal
+    p = "pts_encoder.relative_pos_encoders.1"
+    ref = oracle.relative_bias(fus_sd, p, xyz)
+    out = torch.empty(2, 8, n, n, device=DEV)
+    pe = torch.from_numpy(pack_relpe(fus_sd, p)).to(DEV)
+    xyz_d = torch.from_numpy(xyz).to(DEV)
+    check(lib.gp_relpe_bias(_vp(pe), _vp(xyz_d), 2, n, _vp(out), _s()), "relpe_bias")
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("n,d,with_bias", [(512, 96, True), (256, 256, True), (128, 512, True), (64, 1024, True),
+                                           (1, 1024, False), (77, 256, True)])
+def test_mha_attention_vs_torch(lib, n, d, with_bias):
+    from genpose2_amd._lib import check
+    B, H = 2, 8
+    hd = d // H
+    g = torch.Generator().manual_seed(n + d)
+    qkv = torch.randn(B, n, 3 * d, generator=g)
+    bias = torch.randn(B, H, n, n, generator=g) * 0.5 if with_bias else None
+    q, k, v = (qkv[..., i * d:(i + 1) * d].reshape(B, n, H, hd).transpose(1, 2).double() for i in range(3))
+    s = torch.matmul(q, k.transpose(-2, -1)) / np.sqrt(hd)
+    if bias is not None:
+        s = s + bias.double()
+    ref = torch.matmul(torch.softmax(s, -1), v).transpose(1, 2).reshape(B, n, d).float()
+    out = torch.empty(B, n, d, device=DEV)
+    qkv_d, bias_d = qkv.to(DEV), (None if bias is None else bias.to(DEV))
+    check(lib.gp_mha_attention(_vp(qkv_d), _vp(bias_d), B, n, d, _vp(out), _s()), "mha_attention")
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 2e-5
+
+
+@pytest.mark.parametrize("n_in,n_out,c", [(1024, 512, 384), (512, 256, 384), (300, 77, 40), (64, 64, 8)])
+def test_interp_points_vs_torch(lib, n_in, n_out, c):
+    from genpose2_amd._lib import check
+    x = torch.randn(2, n_in, c, generator=torch.Generator().manual_seed(n_in))
+    ref = tf.interpolate(x.transpose(1, 2), size=n_out, mode="linear", align_corners=False).transpose(1, 2)
+    y = torch.empty(2, n_out, c, device=DEV)
+    xd = x.to(DEV)
+    check(lib.gp_interp_points(_vp(xd), 2, n_in, c, n_out, _vp(y), _s()), "interp_points")
+    torch.cuda.synchronize()
+    assert rel(y, ref) < 1e-6
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+def test_gated_fusion_vs_oracle(fus_model, fus_sd, k):
+    """GatedAttentionFusion of level k (C = level k-1's channels) vs the oracle restatement."""
+    from genpose2_amd import arch
+    from oracle import oracle
+    c = arch.level_out_channels(k - 1)
+    n = arch.NPOINTS[k - 1]
+    rng = np.random.default_rng(k)
+    cur = np.maximum(rng.normal(size=(2, n, c)), 0).astype(np.float32)
+    orig = rng.normal(size=(2, n, 384)).astype(np.float32)
+    got = fus_model.fusion(k, torch.from_numpy(cur).to(DEV), torch.from_numpy(orig).to(DEV))
+    ref = oracle.gated_fusion(fus_sd, f"pts_encoder.feature_fusions.{k - 1}", cur.transpose(0, 2, 1),
+                              orig.transpose(0, 2, 1)).transpose(0, 2, 1)
+    torch.cuda.synchronize()
+    assert rel(got, ref) < 1e-5
+
+
+# ---------------------------------------------------------------- SA levels by the level API
+def test_sa_level_api_equals_encoder_forward():
+    """gp_encoder_fps + gp_sa_level, level by level, reproduces gp_encoder_forward bit for bit (Light encoder)."""
+    from genpose2_amd import _lib, arch, synthetic, weights
+    from genpose2_amd.device import EncoderModel
+    enc = EncoderModel(weights.synthetic_state_dict("score"), torch.device(DEV))
+    pts_np, _ = synthetic.make_batch(81, 5, 1024)
+    pts = torch.from_numpy(pts_np).to(DEV)
+    ref, ws_ref = enc.forward(pts, return_workspace=True)
+    ref_levels = [{k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in d.items()}
+                  for d in enc.levels(5, 1024, ws_ref)]
+    ref = ref.clone()
+    lib = _lib.load()
+    ws = torch.empty(int(lib.gp_encoder_workspace_size(5, 1024)), dtype=torch.uint8, device=DEV)
+    _lib.check(lib.gp_encoder_fps(_vp(pts), 5, 1024, _vp(ws), ws.numel(), _s()))
+    feat = None
+    for lv in range(5):
+        m = arch.NPOINTS[lv] if lv < 4 else 1
+        out = torch.empty(5, m, arch.level_out_channels(lv), device=DEV)
+        _lib.check(lib.gp_sa_level(_vp(enc.wbuf), enc.offsets.ctypes.data_as(_lib.c_int64_p), lv,
+                                   0 if feat is None else feat.shape[2], _vp(pts), 5, 1024, _vp(feat), _vp(ws),
+                                   ws.numel(), _vp(out), _s()), f"sa_level {lv}")
+        if lv < 4:
+            assert torch.equal(out, ref_levels[lv]["features"]), lv
+        feat = out
+    torch.cuda.synchronize()
+    assert torch.equal(feat.reshape(5, -1), ref)
+
+
+# ---------------------------------------------------------------- whole encoder vs the reference
+def test_fus_encoder_vs_reference_golden(fus_model):
+    import make_golden_fus as mf
+    from genpose2_amd import synthetic
+    g = golden("fus")
+    pts, _ = synthetic.make_batch(mf.CID, mf.B, mf.N)
+    feat = mf.rgb_features(mf.B, mf.N)
+    out, levels = fus_model.forward(torch.from_numpy(pts).to(DEV), torch.from_numpy(feat).to(DEV),
+                                    return_levels=True)
+    torch.cuda.synchronize()
+    errs = {}
+    for lv in range(5):
+        for k in ("sa", "tf", "fused"):
+            if f"l{lv}_{k}" in g:
+                errs[(lv, k)] = rel(levels[lv][k][0].cpu().numpy().T, g[f"l{lv}_{k}"])
+    print("fused encoder per-level rel errors", errs, "final", rel(out, g["feat"]))
+    assert max(errs.values()) < 1e-5, errs
+    assert rel(out, g["feat"]) < 1e-5
+
+
+def test_pointwise_agent_pred_func():
+    """PoseNet(dino='pointwise'): pred_func encodes with the fused encoder from data['point_rgb_feat'], sets
+    data['pts_feat'] / data['rgb_feat'] = None like the reference, and samples with the pointwise heads; the
+    features equal the fused encoder's, the poses equal the PC oracle on those features (injected noise)."""
+    import make_golden_fus as mf
+    from genpose2_amd import synthetic, weights
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    from oracle import oracle
+    B, K, T = 2, 4, 20
+    pts, center = synthetic.make_batch(mf.CID, B, 1024)
+    rgb = mf.rgb_features(B, 1024)
+    agent = PoseNet(GenPoseConfig(device=DEV, sampling_steps=T, dino="pointwise")).eval()
+    rng = np.random.default_rng(3)
+    prior = rng.standard_normal((B * K, 9)).astype(np.float32)
+    z1 = rng.standard_normal((T, B * K, 9)).astype(np.float32)
+    z2 = rng.standard_normal((T, B * K, 9)).astype(np.float32)
+    agent.noise_feed = NoiseFeed(torch.from_numpy(prior), torch.from_numpy(z1), torch.from_numpy(z2))
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV),
+            "point_rgb_feat": torch.from_numpy(rgb).to(DEV)}
+    pose, _ = agent.pred_func(data, repeat_num=K)
+    torch.cuda.synchronize()
+    assert data["rgb_feat"] is None
+    sd = weights.synthetic_state_dict("score_pointwise")
+    ofeat = oracle.fus_encoder_forward(sd, pts, rgb)
+    assert rel(data["pts_feat"], ofeat) < 1e-5
+    fr, cr = np.repeat(ofeat, K, 0), np.repeat(center, K, 0)
+    sig = np.float32(0.01 * 5000.0)
+    _, res = oracle.pc_sample(lambda x, t: oracle.score_forward(sd, fr, x, t), (prior * sig).astype(np.float32), cr,
+                              T, z1, z2)
+    got = pose.cpu().numpy().reshape(B * K, 9)
+    assert np.abs(got[:, :6] - res[:, :6]).max() < 1e-4
+    assert rel(got[:, 6:], res[:, 6:]) < 1e-5
+    with pytest.raises(KeyError):
+        agent.pred_func({"pts": data["pts"], "pts_center": data["pts_center"]}, repeat_num=K)
