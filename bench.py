@@ -234,6 +234,9 @@ def main():
                     help="ode: the shipped evaluation's sampler (scripts/eval_single.sh: --sampler_mode ode "
                          "--T0 0.55, sampling_steps unset); reports B*K*nfev/s")
     ap.add_argument("--t0", type=float, default=0.55)
+    ap.add_argument("--dino", choices=["none", "pointwise"], default="none",
+                    help="pointwise: the DINO-pointwise fused encoder (Pointnet2ClsMSGFus) for the score and energy "
+                         "models, fed synthetic per-point image features (B, N, 384) resident in HBM")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: encode batch k+1 on a side stream while batch k samples (every timed step "
                          "still encodes and samples one batch; the first encode is not overlapped). "
@@ -254,7 +257,7 @@ def main():
     B, N, K, T = cfgd["B"], cfgd["N"], cfgd["K"], cfgd["T"]
     ode = args.sampler == "ode"
     cfg = GenPoseConfig(device=str(dev), sampling_steps=None if ode else T, eval_repeat_num=K,
-                        noise_seed=1234 + rank, sampler_mode=[args.sampler])
+                        noise_seed=1234 + rank, sampler_mode=[args.sampler], dino=args.dino)
     score = PoseNet(cfg).eval()
     broadcast_weights(score, ws)
     energy = PoseNet(cfg.copy(agent_type="energy")).eval() if cfgd["energy"] else None
@@ -264,6 +267,9 @@ def main():
             broadcast_weights(a, ws)
     pts, center = synthetic.make_batch(args.config, B, N, first_object=rank * B)
     data0 = {"pts": torch.from_numpy(pts).to(dev), "pts_center": torch.from_numpy(center).to(dev)}
+    if args.dino == "pointwise":   # per-point DINOv3 features (posenet.py:136-197 output), synthetic
+        rgb = np.random.Generator(np.random.PCG64(4242 + rank)).standard_normal((B, N, 384), dtype=np.float32)
+        data0["point_rgb_feat"] = torch.from_numpy(rgb).to(dev)
 
     stream = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(device=dev)
@@ -293,7 +299,7 @@ def main():
         if energy is not None:
             # the energy encoder needs only the points: overlap it with the score sampler
             # (as genpose2_amd.runner.EvaluationPipeline does)
-            edata = {"pts": data0["pts"], "pts_center": data0["pts_center"]}
+            edata = {k: data0[k] for k in ("pts", "pts_center", "point_rgb_feat") if k in data0}
 
             def start_energy_encoder():
                 side.wait_stream(stream)
@@ -398,7 +404,8 @@ def main():
             "data": "synthetic (seeded point clouds, seeded synthetic weights; no checkpoint exists for dino=none)",
             "config": {"workload": f"config{args.config}: B={B} objects/GPU, N={N} pts, K={K} candidates, T={T} PC "
                                    f"steps, {'ScoreNet+EnergyNet+ranking/aggregation' if cfgd['energy'] else 'ScoreNet'}"
-                                   f"{' + ScaleNet' if cfgd['scale'] else ''} (encoder + sampler per step)",
+                                   f"{' + ScaleNet' if cfgd['scale'] else ''} (encoder + sampler per step)"
+                                   f"{', DINO-pointwise fused encoders' if args.dino == 'pointwise' else ''}",
                        "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)",
                        "encoder_pipelined": bool(args.pipeline)},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -414,7 +421,7 @@ def main():
         }
         if ode_info is not None:
             out["ode"] = ode_info
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and args.dino == "none":
             threads = args.cpu_threads or cpu_threads_default()
             out["cpu_baseline"] = (cpu_baseline(cfgd, args.config, threads, args.cpu_sample_objects)
                                    if ws == 1 else None)

@@ -167,7 +167,9 @@ extern "C" int gp_add_layernorm(const float* x, const float* r, int m, int d, co
 // ============================================================================ relative-PE bias
 // Packed pe (gp_relpe_bias in genpose_hip.h): distance Linear(1,16)/ReLU/Linear(16,8), direction
 // Linear(3,16)/ReLU/Linear(16,8), fusion Linear(16,8) over [distance | direction]. One thread per
-// pair (i, j) evaluates all 8 heads; for each head consecutive threads write consecutive j.
+// pair evaluates all 8 heads. Stored key-major, bias[b][h][j][i] (query i, key j): the attention
+// kernel's lanes are queries, so for each key a wave reads 64 consecutive floats; consecutive
+// threads here take consecutive queries i, so the writes are coalesced too.
 __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __restrict__ pe,
                                                                  const float* __restrict__ xyz, int n,
                                                                  float* __restrict__ bias) {
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __
     const int b = blockIdx.y;
     const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
     if (e >= (long long)n * n) return;
-    const int i = (int)(e / n), j = (int)(e - (long long)i * n);
+    const int j = (int)(e / n), i = (int)(e - (long long)j * n);
     const float* pi = xyz + ((size_t)b * n + i) * 3;
     const float* pj = xyz + ((size_t)b * n + j) * 3;
     const float rx = pj[0] - pi[0], ry = pj[1] - pi[1], rz = pj[2] - pi[2];   // xyz[j] - xyz[i]
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __
         float f = 0.f;
 #pragma unroll
         for (int u = 0; u < 16; ++u) f += cat[u] * sp[368 + 16 * h + u];
-        bias[(((size_t)b * FUS_HEADS + h) * n + i) * n + j] = f + sp[496 + h];
+        bias[(((size_t)b * FUS_HEADS + h) * n + j) * n + i] = f + sp[496 + h];
     }
 }
 
@@ -225,51 +227,55 @@ extern "C" int gp_relpe_bias(const float* pe, const float* xyz, int b, int n, fl
 }
 
 // ============================================================================ biased attention
-// Workgroup = (64 queries, head, object); 4 lanes per query, each holding HD4 = hd/4 channels of q and
-// of the output. The head's K and V (n x hd) are staged in LDS; every quad of a wave reads the same key
-// row (broadcast). Softmax as torch evaluates it: pass 1 the row max of s = q.k / sqrt(hd) + bias,
-// pass 2 p = exp(s - max), sum and sum p v; out = (sum p v) / sum.
-template <int HD4>
+// Workgroup = (QPW queries, head, object); LPQ lanes per query, each holding HD/LPQ channels of q and of
+// the output (LPQ = 1 for head dims <= 32: no cross-lane sum per key). The head's K and V (n x hd) are
+// staged in LDS; all queries of a wave read the same key row (broadcast). The bias is key-major, so
+// for each key the wave's queries read consecutive floats. Softmax as torch evaluates it: pass 1 the
+// row max of s = q.k / sqrt(hd) + bias, pass 2 p = exp(s - max), sum p and sum p v; out = sum p v / sum.
+// (q.k / sqrt(hd) is taken as q.k * (1 / sqrt(hd)): within an ulp of torch's division.)
+template <int HD, int LPQ>
 __global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restrict__ qkv,
                                                           const float* __restrict__ bias, int n, int d,
                                                           float* __restrict__ out) {
 #pragma clang fp contract(off)
-    constexpr int HD = 4 * HD4;
+    constexpr int HL = HD / LPQ;                  // channels per lane
+    constexpr int QPW = FUS_THREADS / LPQ;        // queries per workgroup
+    static_assert(HL % 4 == 0 || HL == 12 || HL == 3, "float4 slices");
     extern __shared__ __attribute__((aligned(16))) float kv[];
     float* sk = kv;
     float* sv = kv + (size_t)n * HD;
     const int h = blockIdx.y, b = blockIdx.z;
     const size_t ld = 3 * (size_t)d;
     const float* base = qkv + (size_t)b * n * ld;
-    for (int e = threadIdx.x; e < n * HD; e += FUS_THREADS) {
-        const int j = e / HD, c = e - (e / HD) * HD;
-        sk[e] = base[(size_t)j * ld + d + h * HD + c];
-        sv[e] = base[(size_t)j * ld + 2 * d + h * HD + c];
+    for (int e = threadIdx.x; e < n * (HD / 4); e += FUS_THREADS) {
+        const int j = e / (HD / 4), c4 = e - j * (HD / 4);
+        st4(sk + (size_t)j * HD + 4 * c4, ld4(base + (size_t)j * ld + d + h * HD + 4 * c4));
+        st4(sv + (size_t)j * HD + 4 * c4, ld4(base + (size_t)j * ld + 2 * d + h * HD + 4 * c4));
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int part = lane & 3;
-    const int i = blockIdx.x * 64 + (threadIdx.x >> 2);
+    const int part = LPQ > 1 ? (threadIdx.x & (LPQ - 1)) : 0;
+    const int i = blockIdx.x * QPW + threadIdx.x / LPQ;
     const int ii = i < n ? i : n - 1;
-    float qv[HD4], o[HD4];
-    const float* qp = base + (size_t)ii * ld + h * HD + part * HD4;
+    float qv[HL], o[HL];
+    const float* qp = base + (size_t)ii * ld + h * HD + part * HL;
 #pragma unroll
-    for (int c = 0; c < HD4; ++c) {
+    for (int c = 0; c < HL; ++c) {
         qv[c] = qp[c];
         o[c] = 0.f;
     }
-    const float scale = sqrtf((float)HD);
-    const float* brow = bias ? bias + (((size_t)b * FUS_HEADS + h) * n + ii) * n : nullptr;
+    const float inv = 1.0f / sqrtf((float)HD);
+    const float* bcol = bias ? bias + ((size_t)b * FUS_HEADS + h) * n * n + ii : nullptr;   // + j * n
     auto score = [&](int j) {
-        const float* kr = sk + (size_t)j * HD + part * HD4;
+        const float* kr = sk + (size_t)j * HD + part * HL;
         float s = 0.f;
 #pragma unroll
-        for (int c = 0; c < HD4; ++c) s += qv[c] * kr[c];
-        // quad sum (lanes 4t..4t+3), the same order in every lane
-        s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
-        s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
-        s = s / scale;
-        return brow ? s + brow[j] : s;
+        for (int c = 0; c < HL; ++c) s += qv[c] * kr[c];
+        if constexpr (LPQ == 4) {   // quad sum (lanes 4t..4t+3), the same order in every lane
+            s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
+            s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
+        }
+        s = s * inv;
+        return bcol ? s + bcol[(size_t)j * n] : s;
     };
     float mx = -INFINITY;
     for (int j = 0; j < n; ++j) mx = fmaxf(mx, score(j));
@@ -277,32 +283,37 @@ __global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restric
     for (int j = 0; j < n; ++j) {
         const float p = expf(score(j) - mx);
         l += p;
-        const float* vr = sv + (size_t)j * HD + part * HD4;
+        const float* vr = sv + (size_t)j * HD + part * HL;
 #pragma unroll
-        for (int c = 0; c < HD4; ++c) o[c] += p * vr[c];
+        for (int c = 0; c < HL; ++c) o[c] += p * vr[c];
     }
     if (i < n) {
-        float* op = out + ((size_t)b * n + i) * d + h * HD + part * HD4;
+        float* op = out + ((size_t)b * n + i) * d + h * HD + part * HL;
+        const float rl = 1.0f / l;
 #pragma unroll
-        for (int c = 0; c < HD4; ++c) op[c] = o[c] / l;
+        for (int c = 0; c < HL; ++c) op[c] = o[c] * rl;
     }
 }
 
 extern "C" int gp_mha_attention(const float* qkv, const float* bias, int b, int n, int d, float* out, hipStream_t st) {
     GP_REQUIRE(qkv && out && b >= 0 && n >= 1, "mha_attention: bad arguments");
     GP_REQUIRE(d % (4 * FUS_HEADS) == 0, "mha_attention: d=%d must be a multiple of 32", d);
+    GP_REQUIRE(((uintptr_t)qkv | (uintptr_t)out) % 16 == 0, "mha_attention: pointers must be 16-byte aligned");
     if (!b) return GP_OK;
     const int hd = d / FUS_HEADS;
     const size_t lds = sizeof(float) * 2 * (size_t)n * hd;
     GP_REQUIRE(lds <= 64 * 1024, "mha_attention: K/V of a head (%zu bytes) exceed 64 KiB", lds);
-    const dim3 grid((n + 63) / 64, FUS_HEADS, b);
-    switch (hd / 4) {
-        case 3: hipLaunchKernelGGL(mha_kernel<3>, grid, dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out); break;
-        case 8: hipLaunchKernelGGL(mha_kernel<8>, grid, dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out); break;
-        case 16: hipLaunchKernelGGL(mha_kernel<16>, grid, dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out); break;
-        case 32: hipLaunchKernelGGL(mha_kernel<32>, grid, dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out); break;
+#define GP_MHA(HD, LPQ)                                                                                    \
+    hipLaunchKernelGGL((mha_kernel<HD, LPQ>), dim3((n + FUS_THREADS / LPQ - 1) / (FUS_THREADS / LPQ), FUS_HEADS, b), \
+                       dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out)
+    switch (hd) {
+        case 12: GP_MHA(12, 1); break;
+        case 32: GP_MHA(32, 1); break;
+        case 64: GP_MHA(64, 4); break;
+        case 128: GP_MHA(128, 4); break;
         default: gp_set_error("mha_attention: head dim %d not in {12, 32, 64, 128}", hd); return GP_ERR_UNSUPPORTED;
     }
+#undef GP_MHA
     return gp_check_launch("mha_kernel");
 }
 

@@ -101,7 +101,8 @@ int gp_linear(const float *x, int ldx, int m, int k, const float *w, const float
 int gp_add_layernorm(const float *x, const float *r, int m, int d, const float *gamma,
                      const float *beta, float eps, float *y, hipStream_t stream);
 /* Relative-PE bias of EfficientRelativePositionalEncoding (8 heads): xyz (b, n, 3) ->
- * bias (b, 8, n, n), bias[b,h,i,j] from rel = xyz[j] - xyz[i]. pe (host-packed, 512 floats):
+ * bias (b, 8, n, n) KEY-MAJOR: bias[b][h][j][i] is the reference's relative_bias[b, h, i, j]
+ * (query i, key j, rel = xyz[j] - xyz[i]). pe (host-packed, 512 floats):
  * [0:16) dist.0.w, [16:32) dist.0.b, [32:160) dist.2.w (8x16), [160:168) dist.2.b,
  * [168:216) dir.0.w (16x3), [216:232) dir.0.b, [232:360) dir.2.w, [360:368) dir.2.b,
  * [368:496) fusion.w (8x16), [496:504) fusion.b. */
@@ -109,7 +110,8 @@ size_t gp_relpe_bias_bytes(int b, int n);
 int gp_relpe_bias(const float *pe, const float *xyz, int b, int n, float *bias, hipStream_t stream);
 /* Multi-head attention with an additive bias (MultiheadAttentionWithRelativePE core,
  * attention.py:436-488, eval): qkv (b, n, 3d) rows [q | k | v] (heads of d/8 channels),
- * bias (b, 8, n, n) or NULL -> out (b, n, d) = softmax(q k^T / sqrt(d/8) + bias) v per head. */
+ * bias (b, 8, n, n) key-major as gp_relpe_bias writes it, or NULL ->
+ * out (b, n, d) = softmax(q k^T / sqrt(d/8) + bias) v per head. */
 int gp_mha_attention(const float *qkv, const float *bias, int b, int n, int d, float *out,
                      hipStream_t stream);
 /* F.interpolate(mode="linear", align_corners=False) along the point index: x (b, n_in, c) ->

@@ -101,7 +101,7 @@ def test_relpe_bias_vs_oracle(lib, fus_sd, n):
     xyz_d = torch.from_numpy(xyz).to(DEV)
     check(lib.gp_relpe_bias(_vp(pe), _vp(xyz_d), 2, n, _vp(out), _s()), "relpe_bias")
     torch.cuda.synchronize()
-    assert rel(out, ref) < 1e-5
+    assert rel(out.transpose(2, 3), ref) < 1e-5      # stored key-major
 
 
 @pytest.mark.parametrize("n,d,with_bias", [(512, 96, True), (256, 256, True), (128, 512, True), (64, 1024, True),
@@ -119,7 +119,7 @@ def test_mha_attention_vs_torch(lib, n, d, with_bias):
         s = s + bias.double()
     ref = torch.matmul(torch.softmax(s, -1), v).transpose(1, 2).reshape(B, n, d).float()
     out = torch.empty(B, n, d, device=DEV)
-    qkv_d, bias_d = qkv.to(DEV), (None if bias is None else bias.to(DEV))
+    qkv_d, bias_d = qkv.to(DEV), (None if bias is None else bias.transpose(2, 3).contiguous().to(DEV))
     check(lib.gp_mha_attention(_vp(qkv_d), _vp(bias_d), B, n, d, _vp(out), _s()), "mha_attention")
     torch.cuda.synchronize()
     assert rel(out, ref) < 2e-5
