@@ -490,6 +490,26 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     PC_MARK(6);
 }
 
+// ============================================================================ tile width
+#ifndef PC_SPLIT_NT2_MIN
+#define PC_SPLIT_NT2_MIN 4097   // rows from which the split kernels take 32-candidate tiles (> 256 tiles of 16)
+#endif
+#ifndef PC_SPLIT_NT4_MIN
+#define PC_SPLIT_NT4_MIN 8193   // ... and 64-candidate tiles (> 256 tiles of 32)
+#endif
+// Column tiles (16 candidates each) per workgroup of the per-candidate head kernels (PC step, ODE stages).
+// exact fp32 (scripts/kbench.py): 16 candidates x 8 waves per workgroup beats 32 x 4 at every size
+// (R=25,600: 125 vs 153 us/step): 112 VGPRs leave room for two workgroups per CU, while the 32-wide
+// tile needs 373 registers (one wave per SIMD).
+// split-f16: each workgroup streams the 1 MB of GEMM weights once per launch whatever its width, so
+// wider tiles cut the weight stream per candidate once there are enough tiles. One workgroup per CU
+// either way (the LDS of a 32- or 64-candidate tile), so the tile width is the smallest that keeps the
+// launch within one pass of the 256 CUs, or the widest above that.
+static inline int head_pick_nt(int rows, bool split) {
+    if (!split) return 1;
+    return rows >= PC_SPLIT_NT4_MIN ? 4 : (rows >= PC_SPLIT_NT2_MIN ? 2 : 1);
+}
+
 // ============================================================================ pose helpers
 template <typename T>
 __device__ __forceinline__ T tsqrt(T v);

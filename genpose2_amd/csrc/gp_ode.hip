@@ -58,13 +58,17 @@ struct OdeStageArgs {
 };
 
 // MODE 0: stage derivative. MODE 1: last stage of an attempt (y_new, K_6, error partials).
-template <int MODE, bool SPLIT>
+// NT column tiles of 16 candidates per workgroup (head_pick_nt: 32 / 64 candidates from 4097 / 8193 rows
+// with the split-f16 trunk, as the PC step).
+template <int MODE, bool SPLIT, int NT>
 __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a) {
-    __shared__ HeadSmem<1, EVAL_WV> sm;
-    __shared__ int obj[16];
-    __shared__ double y0s[16 * 9], y1s[16 * 9], esq[16 * 9];
+    constexpr int ROWS = 16 * NT;
+    constexpr int NTH = EVAL_WV * 64;
+    __shared__ HeadSmem<NT, EVAL_WV> sm;
+    __shared__ int obj[ROWS];
+    __shared__ double y0s[ROWS * 9], y1s[ROWS * 9], esq[NTH];
     const int tid = threadIdx.x;
-    const int r0 = blockIdx.x * 16;
+    const int r0 = blockIdx.x * ROWS;
     const double* y = a.y;
     const double* kin[ODE_NK];
 #pragma unroll
@@ -87,8 +91,8 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         kout = a.kbuf[c->kidx[a.stage]];
         ynew = a.ybuf[c->yi ^ 1];
     }
-    stage_small_weights<1, EVAL_WV>(a.w, sm);
-    for (int i = tid; i < 256; i += EVAL_WV * 64) {
+    stage_small_weights<NT, EVAL_WV>(a.w, sm);
+    for (int i = tid; i < ROWS * 16; i += NTH) {
         const int c = i >> 4, j = i & 15;
         const int r = r0 + c;
         float xv = 0.f;
@@ -111,19 +115,19 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         }
         sm.xin[i] = xv;
     }
-    if (tid < 16) {
+    if (tid < ROWS) {
         const int r = r0 + tid;
         obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
     }
     if constexpr (SPLIT)
-        head_trunk_split<1, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
+        head_trunk_split<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
     else
-        head_trunk<1, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
-    if (tid < 144) {
+        head_trunk<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
+    double sq = 0.0;   // this thread's (err/scale)^2 terms, its elements in increasing order
+    for (int e9 = tid; e9 < ROWS * 9; e9 += NTH) {
 #pragma clang fp contract(off)
-        const int c = tid / 9, o = tid - c * 9;
+        const int c = e9 / 9, o = e9 - c * 9;
         const int r = r0 + c;
-        double sq = 0.0;
         if (r < a.rows) {
             const size_t e = (size_t)r * 9 + o;
             const float s = fdiv(head_out(sm, c, o), fadd(sigma, 1e-7f));
@@ -137,19 +141,43 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
                 const double y0 = y0s[c * 9 + o], y1 = y1s[c * 9 + o];
                 const double sc = a.atol + fmax(fabs(y0), fabs(y1)) * a.rtol;
                 const double er = (acc * h) / sc;
-                sq = er * er;
+                sq += er * er;
             }
         }
-        if (MODE == 1) esq[tid] = sq;
     }
     if (MODE == 1) {
+        // workgroup partial in a fixed order: per-thread sums, xor tree per wave, waves in order
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off, 64);
+        if ((tid & 63) == 0) esq[tid >> 6] = sq;
         __syncthreads();
         if (tid == 0) {
             double t = 0.0;
-            for (int i = 0; i < 144; ++i) t += esq[i];
+            for (int v = 0; v < EVAL_WV; ++v) t += esq[v];
             a.part[blockIdx.x] = t;
         }
     }
+}
+
+// Stage-kernel launch of `nt` column tiles per workgroup (1 for the exact-fp32 trunk).
+template <int MODE>
+static void ode_launch_stage(const OdeStageArgs& a, int nt, hipStream_t st) {
+    const int nwg = (a.rows + 16 * nt - 1) / (16 * nt);
+    const dim3 grid(nwg), blk(EVAL_WV * 64);
+    if (!a.w.pe2_h)
+        hipLaunchKernelGGL((ode_stage_kernel<MODE, false, 1>), grid, blk, 0, st, a);
+    else if (nt == 4)
+        hipLaunchKernelGGL((ode_stage_kernel<MODE, true, 4>), grid, blk, 0, st, a);
+    else if (nt == 2)
+        hipLaunchKernelGGL((ode_stage_kernel<MODE, true, 2>), grid, blk, 0, st, a);
+    else
+        hipLaunchKernelGGL((ode_stage_kernel<MODE, true, 1>), grid, blk, 0, st, a);
+}
+
+static int ode_nt(const gp_head_weights* w, int rows) { return head_pick_nt(rows, w->pe2_h != nullptr); }
+static int ode_nwg(const gp_head_weights* w, int rows) {
+    const int nt = ode_nt(w, rows);
+    return (rows + 16 * nt - 1) / (16 * nt);
 }
 
 // Sum of part[0..n) by a 256-thread workgroup in a fixed order (strided per-thread sums, xor
@@ -375,10 +403,7 @@ extern "C" int gp_ode_rhs(const gp_head_weights* w, const float* pobj, float t32
     a.kper = k;
     int rc = ode_launch_times(w, &t32, 1, workspace, stream);
     if (rc) return rc;
-    if (a.w.pe2_h)
-        hipLaunchKernelGGL((ode_stage_kernel<0, true>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
-    else
-        hipLaunchKernelGGL((ode_stage_kernel<0, false>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
+    ode_launch_stage<0>(a, ode_nt(w, rows), stream);
     return gp_check_launch("ode_stage_kernel");
 }
 
@@ -392,7 +417,7 @@ extern "C" int gp_ode_attempt(const gp_head_weights* w, const float* pobj, const
                "ode_attempt: bad arguments");
     GP_REQUIRE(workspace_bytes >= gp_ode_workspace_size(rows), "ode_attempt: workspace too small");
     for (int j = 0; j < ODE_NK; ++j) GP_REQUIRE(kslots[j] != nullptr, "ode_attempt: null K slot");
-    const int nwg = (rows + 15) / 16;
+    const int nwg = ode_nwg(w, rows), nt = ode_nt(w, rows);
     const float* tproj = static_cast<const float*>(workspace);
     double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + ode_part_offset());
     int rc = ode_launch_times(w, t32_6, 6, workspace, stream);
@@ -415,10 +440,7 @@ extern "C" int gp_ode_attempt(const gp_head_weights* w, const float* pobj, const
         a.nk = s;
         for (int j = 0; j < s; ++j) a.a[j] = tableau_a[s * 6 + j];
         a.kout = kslots[s];
-        if (a.w.pe2_h)
-            hipLaunchKernelGGL((ode_stage_kernel<0, true>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
-        else
-            hipLaunchKernelGGL((ode_stage_kernel<0, false>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+        ode_launch_stage<0>(a, nt, stream);
     }
     // y_new = y + (sum_{j<6} B_j K_j) h ; K_6 = f(t + h, y_new) ; error partials
     a.tproj = tproj + (size_t)5 * 768;
@@ -430,10 +452,7 @@ extern "C" int gp_ode_attempt(const gp_head_weights* w, const float* pobj, const
     a.kout = kslots[6];
     a.ynew = ynew;
     a.part = part;
-    if (a.w.pe2_h)
-        hipLaunchKernelGGL((ode_stage_kernel<1, true>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
-    else
-        hipLaunchKernelGGL((ode_stage_kernel<1, false>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    ode_launch_stage<1>(a, nt, stream);
     hipLaunchKernelGGL(ode_norm_kernel, dim3(1), dim3(256), 0, stream, (const double*)part, nwg,
                        (double)rows * 9.0, err_out);
     return gp_check_launch("ode_stage_kernel<final>");
@@ -614,7 +633,7 @@ extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, 
     OdeCtl* ctl = reinterpret_cast<OdeCtl*>(ws);
     float* tproj6 = reinterpret_cast<float*>(ws + auto_tproj_off());
     double* part = reinterpret_cast<double*>(ws + auto_part_off());
-    const int nwg = (rows + 15) / 16;
+    const int nwg = ode_nwg(w, rows), nt = ode_nt(w, rows);
     OdeConsts kc = {t_bound, direction, rtol, atol, sig_min, base, diff_scale, (double)rows * 9.0, nwg};
     OdeCtl* cin = ctl + (n & 1);
     OdeCtl* cout = ctl + ((n + 1) & 1);
@@ -641,19 +660,13 @@ extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, 
         a.stage = s;
         a.nk = s;
         for (int j = 0; j < s; ++j) a.a[j] = tableau_a[s * 6 + j];
-        if (a.w.pe2_h)
-            hipLaunchKernelGGL((ode_stage_kernel<0, true>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
-        else
-            hipLaunchKernelGGL((ode_stage_kernel<0, false>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+        ode_launch_stage<0>(a, nt, stream);
     }
     a.stage = 6;
     a.nk = 6;
     for (int j = 0; j < 6; ++j) a.a[j] = b[j];
     for (int j = 0; j < ODE_NK; ++j) a.e[j] = e[j];
     a.part = part;
-    if (a.w.pe2_h)
-        hipLaunchKernelGGL((ode_stage_kernel<1, true>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
-    else
-        hipLaunchKernelGGL((ode_stage_kernel<1, false>), dim3(nwg), dim3(EVAL_WV * 64), 0, stream, a);
+    ode_launch_stage<1>(a, nt, stream);
     return gp_check_launch("ode_stage_kernel<auto>");
 }

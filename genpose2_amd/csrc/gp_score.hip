@@ -387,23 +387,7 @@ extern "C" size_t gp_pc_workspace_size(int rows) {
     return sizeof(float) * ((size_t)rows * 9 * 5 + 2 * ntiles) + 256;
 }
 
-#ifndef PC_SPLIT_NT2_MIN
-#define PC_SPLIT_NT2_MIN 4097   // rows from which the split kernel takes 32-candidate tiles (> 256 tiles of 16)
-#endif
-#ifndef PC_SPLIT_NT4_MIN
-#define PC_SPLIT_NT4_MIN 8193   // ... and 64-candidate tiles (> 256 tiles of 32)
-#endif
-static int pc_pick_nt(int rows, bool split) {
-    // exact fp32 (scripts/kbench.py): 16 candidates x 8 waves per workgroup beats 32 x 4 at every
-    // size (R=25,600: 125 vs 153 us/step): 112 VGPRs leave room for two workgroups per CU, while
-    // the 32-wide tile needs 373 registers (one wave per SIMD).
-    // split-f16: each workgroup streams the 1 MB of GEMM weights once per step whatever its width,
-    // so 32-candidate tiles halve the weight stream per candidate once there are enough tiles.
-    // One workgroup per CU either way (the LDS of a 32- or 64-candidate tile), so the tile width is
-    // the smallest that keeps the launch within one pass of the 256 CUs, or the widest above that.
-    if (!split) return 1;
-    return rows >= PC_SPLIT_NT4_MIN ? 4 : (rows >= PC_SPLIT_NT2_MIN ? 2 : 1);
-}
+static int pc_pick_nt(int rows, bool split) { return head_pick_nt(rows, split); }
 
 // Candidates per PC-step workgroup that gp_pc_sample picks for `rows` (split: head weights with
 // the f16 planes) -- lets callers size their accounting from the kernel's real tiling.
