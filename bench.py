@@ -234,6 +234,11 @@ def main():
                     help="ode: the shipped evaluation's sampler (scripts/eval_single.sh: --sampler_mode ode "
                          "--T0 0.55, sampling_steps unset); reports B*K*nfev/s")
     ap.add_argument("--t0", type=float, default=0.55)
+    ap.add_argument("--energy-overlap", type=int, default=0,
+                    help="0 (default): the EnergyNet encoder runs after the score sampler on the same stream; "
+                         "1: on a side stream beside it (runner.EvaluationPipeline). Config 4: 23.12 vs 22.83 "
+                         "ms/step, but beside the sampler its workgroups hold CUs at ~45 of the 501 PC-step "
+                         "launches per step (up to 1.1 ms each; profiles/r2/energy_overlap_ab.json)")
     ap.add_argument("--dino", choices=["none", "pointwise"], default="none",
                     help="pointwise: the DINO-pointwise fused encoder (Pointnet2ClsMSGFus) for the score and energy "
                          "models, fed synthetic per-point image features (B, N, 384) resident in HBM")
@@ -305,7 +310,7 @@ def main():
                 side.wait_stream(stream)
                 with torch.cuda.stream(side):
                     energy.encode_func(edata)
-            score.after_encode = start_energy_encoder
+            score.after_encode = start_energy_encoder if args.energy_overlap else None
         if record and not ode:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -336,6 +341,8 @@ def main():
             score.heads.pc_sample = orig
             samp_ev.append((e0, e1))
         if energy is not None:
+            if not args.energy_overlap:
+                energy.encode_func(edata)
             stream.wait_stream(side)
             edata["pts_feat"].record_stream(stream)
             e = energy.get_energy(edata, pose, T=1e-5, extract_feature=False)
@@ -407,7 +414,8 @@ def main():
                                    f"{' + ScaleNet' if cfgd['scale'] else ''} (encoder + sampler per step)"
                                    f"{', DINO-pointwise fused encoders' if args.dino == 'pointwise' else ''}",
                        "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)",
-                       "encoder_pipelined": bool(args.pipeline)},
+                       "encoder_pipelined": bool(args.pipeline),
+                       "energy_encoder_overlapped": bool(args.energy_overlap) and cfgd["energy"]},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": load_traffic(B * K, split),
                          "kernel": "pc_step_kernel", "arith": score.heads.arith, "flop_per_launch": flop_launch,
