@@ -57,6 +57,13 @@ _SIGS: Dict[str, tuple] = {
     "gp_fusion_attend": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p]),
     "gp_fusion_mix": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "gp_weights_pack": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_void_p)]),
+    "gp_weights_free": (None, [c_void_p]),
+    "gp_weights_heads": (ctypes.POINTER(HeadWeights), [c_void_p]),
+    "gp_weights_scale": (ctypes.POINTER(ScaleWeights), [c_void_p]),
+    "gp_weights_encoder": (c_void_p, [c_void_p, ctypes.POINTER(c_int64_p)]),
+    "gp_weights_pack_host": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                     ctypes.POINTER(c_size_t), c_int64_p, c_int64_p]),
     "gp_head_object_proj": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_int, c_void_p, c_void_p]),
     "gp_head_time_proj": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_int, c_void_p, c_void_p]),
     "gp_score_eval": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_float, c_void_p, c_int, c_int,

@@ -303,6 +303,32 @@ int gp_points_mean(const float *pts, int b, int n, int c, float *out, hipStream_
 int gp_bbox_length(const float *pcl, int b, int n, int c, const float *pose, float *length,
                    hipStream_t stream);
 
+/* ===================================================================== weight packing
+ * The load path of PoseNet.load_ckpt -> load_state_dict (posenet_agent.py:171-203) for the --dino none
+ * models, without Python: a model's state-dict tensors (HOST float32 arrays named by the reference's
+ * model_state_dict keys; a "module." prefix is stripped; num_batches_tracked and unknown keys are ignored)
+ * -> every packed layout the kernels read (BN folded in float64, MFMA fragment order, split-f16 planes and
+ * bounds), byte-identical to genpose2_amd/pack.py.
+ * gp_weights_pack uploads them into ONE device allocation (the only allocating call of the library; not a
+ * hot call) and returns an opaque handle; gp_weights_heads / gp_weights_scale / gp_weights_encoder give
+ * the structs and pointers the other entry points take (valid until gp_weights_free).
+ * gp_weights_pack_host writes the same packed buffer to host memory instead (out == NULL: size query):
+ * fields[GP_PACK_NFIELDS] = float offsets of the encoder buffer (GP_PACK_ENC), the 16 gp_head_weights
+ * fields in struct order (GP_PACK_HEADS + i) or the 8 gp_scale_weights fields (GP_PACK_SCALE + i), -1 if
+ * absent; enc_table (120 int64) = gp_encoder_forward's layer_off relative to the encoder buffer. */
+enum { GP_MODEL_SCORE = 0, GP_MODEL_ENERGY = 1, GP_MODEL_SCALE = 2 };
+enum { GP_PACK_ENC = 0, GP_PACK_HEADS = 1, GP_PACK_SCALE = 17, GP_PACK_NFIELDS = 25 };
+typedef struct gp_weights gp_weights;
+int gp_weights_pack(int kind, int n, const char *const *names, const float *const *data,
+                    const int64_t *numel, gp_weights **out);
+void gp_weights_free(gp_weights *w);
+const gp_head_weights *gp_weights_heads(const gp_weights *w);
+const gp_scale_weights *gp_weights_scale(const gp_weights *w);
+const float *gp_weights_encoder(const gp_weights *w, const int64_t **layer_off);
+int gp_weights_pack_host(int kind, int n, const char *const *names, const float *const *data,
+                         const int64_t *numel, float *out, size_t out_floats, size_t *need_floats,
+                         int64_t *fields, int64_t *enc_table);
+
 #ifdef __cplusplus
 }
 #endif

@@ -332,3 +332,61 @@ def test_fus_manifest_matches_reference_layout():
         lay = json.load(f)
     mine = {k[len("pts_encoder."):]: list(s) for k, s, _ in weights.fus_encoder_manifest()}
     assert mine == lay
+
+
+def _pack_host(kind_id, sd):
+    """gp_weights_pack_host over a state dict (host arrays); returns (buffer, fields, enc_table)."""
+    import ctypes
+    from genpose2_amd import _lib
+    lib = _lib.load()
+    keys = [k for k, v in sd.items() if v.dtype == np.float32]
+    arrs = [np.ascontiguousarray(sd[k], np.float32) for k in keys]
+    names = (ctypes.c_char_p * len(keys))(*[k.encode() for k in keys])
+    data = (ctypes.c_void_p * len(keys))(*[a.ctypes.data for a in arrs])
+    numel = np.array([a.size for a in arrs], np.int64)
+    fields = np.zeros(25, np.int64)
+    table = np.zeros(120, np.int64)
+    need = ctypes.c_size_t(0)
+    args = (kind_id, len(keys), ctypes.cast(names, ctypes.c_void_p), ctypes.cast(data, ctypes.c_void_p),
+            numel.ctypes.data)
+    _lib.check(lib.gp_weights_pack_host(*args, None, 0, ctypes.byref(need), fields.ctypes.data_as(_lib.c_int64_p),
+                                        table.ctypes.data_as(_lib.c_int64_p)), "pack_host size")
+    buf = np.zeros(need.value, np.float32)
+    _lib.check(lib.gp_weights_pack_host(*args, buf.ctypes.data, buf.size, ctypes.byref(need),
+                                        fields.ctypes.data_as(_lib.c_int64_p), table.ctypes.data_as(_lib.c_int64_p)),
+               "pack_host")
+    return buf, fields, table
+
+
+@pytest.mark.parametrize("kind,kind_id", [("score", 0), ("energy", 1), ("scale", 2)])
+def test_weights_pack_host_matches_pack_py(kind, kind_id):
+    """The C++ packer behind gp_weights_pack (the non-Python load path) writes byte-identical layouts to
+    genpose2_amd/pack.py: folded + fragment-packed encoder and its table, every head field (split-f16
+    planes and activation bounds included), ScaleNet copies; a "module." prefix is accepted."""
+    from genpose2_amd import pack, weights
+    sd = weights.synthetic_state_dict(kind)
+    sd_mod = {("module." + k if i % 2 else k): v for i, (k, v) in enumerate(sd.items())}
+    buf, fields, table = _pack_host(kind_id, sd_mod)
+    if kind == "scale":
+        ref = pack.pack_scale(sd)
+        for i, k in enumerate(pack.SCALE_FIELDS):
+            v = ref[k].reshape(-1)
+            np.testing.assert_array_equal(buf[fields[17 + i]:fields[17 + i] + v.size], v)
+        assert fields[0] == -1
+        return
+    ebuf, etab = pack.pack_encoder(sd)
+    np.testing.assert_array_equal(table.reshape(5, 2, 3, 4), etab)
+    assert fields[0] == 0
+    np.testing.assert_array_equal(buf[:ebuf.size].view(np.uint32), ebuf.view(np.uint32))
+    ref = pack.pack_heads(sd)
+    for i, k in enumerate(pack.HEAD_FIELDS):
+        v = ref[k].reshape(-1).view(np.uint32)
+        np.testing.assert_array_equal(buf[fields[1 + i]:fields[1 + i] + v.size].view(np.uint32), v, err_msg=k)
+
+
+def test_weights_pack_host_reports_missing_key():
+    from genpose2_amd import _lib, weights
+    sd = weights.synthetic_state_dict("score")
+    del sd["pose_score_net.pose_encoder.2.bias"]
+    with pytest.raises(_lib.GenPoseHipError, match="pose_encoder.2.bias"):
+        _pack_host(0, sd)
