@@ -146,10 +146,10 @@ def cpu_baseline(cfg, config_id, threads, sample_objects, reps=3):
     return out
 
 
-def load_traffic(rows, split):
-    """HBM(+Infinity Cache) bytes per pc_step launch from the newest committed PMC pass for the
-    same row count and arithmetic (profiles/**/pmc_pc_step*.json, scripts/pmc_passes.sh), or None.
-    Split-f16 instantiations carry a `true` template argument in the recorded kernel name."""
+def load_traffic(rows, split, tile):
+    """HBM(+Infinity Cache) bytes per pc_step launch from the newest committed PMC pass of the same
+    kernel instantiation (tile width, arithmetic) and row count (profiles/**/pmc_pc_step*.json,
+    scripts/pmc_passes.sh), or None."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "**", "pmc_pc_step*.json"), recursive=True))
     for fn in reversed(files):
         try:
@@ -157,7 +157,8 @@ def load_traffic(rows, split):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("rows") == rows and (", true>" in d.get("kernel", "")) == bool(split):
+        k = d.get("kernel", "")
+        if d.get("rows") == rows and (", true>" in k) == bool(split) and k.startswith(f"void pc_step_kernel<{tile // 16},"):
             return d.get("hbm_bytes_per_launch")
     return None
 
@@ -417,7 +418,7 @@ def main():
                        "encoder_pipelined": bool(args.pipeline),
                        "energy_encoder_overlapped": bool(args.energy_overlap) and cfgd["energy"]},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": load_traffic(B * K, split),
+                         "frac": achieved / peak, "traffic": load_traffic(B * K, split, tile),
                          "kernel": "pc_step_kernel", "arith": score.heads.arith, "flop_per_launch": flop_launch,
                          "avg_launch_us": per_launch_s * 1e6, "sampler_ms_per_step": samp_ms,
                          "fp32_mfma_equiv_frac": achieved / FP32_PEAK_TFLOPS,
