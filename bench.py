@@ -235,9 +235,11 @@ def main():
                     help="ode: the shipped evaluation's sampler (scripts/eval_single.sh: --sampler_mode ode "
                          "--T0 0.55, sampling_steps unset); reports B*K*nfev/s")
     ap.add_argument("--t0", type=float, default=0.55)
-    ap.add_argument("--energy-overlap", type=int, default=0,
-                    help="0 (default): the EnergyNet encoder runs after the score sampler on the same stream; "
-                         "1: on a side stream beside it (runner.EvaluationPipeline). Config 4: 23.12 vs 22.83 "
+    ap.add_argument("--energy-overlap", type=int, default=2, choices=[0, 1, 2],
+                    help="2 (default): the EnergyNet encoder runs on a side stream beside the score encoder, "
+                         "both ahead of the sampler, which waits for both (config 4: 22.21 ms/step); 0: after "
+                         "the sampler on the same stream (22.75); 1: beside the sampler (runner."
+                         "EvaluationPipeline). Config 4: 23.12 vs 22.83 "
                          "ms/step, but beside the sampler its workgroups hold CUs at ~45 of the 501 PC-step "
                          "launches per step (up to 1.1 ms each; profiles/r2/energy_overlap_ab.json)")
     ap.add_argument("--dino", choices=["none", "pointwise"], default="none",
@@ -311,7 +313,12 @@ def main():
                 side.wait_stream(stream)
                 with torch.cuda.stream(side):
                     energy.encode_func(edata)
-            score.after_encode = start_energy_encoder if args.energy_overlap else None
+            score.after_encode = start_energy_encoder if args.energy_overlap == 1 else None
+            if args.energy_overlap == 2:
+                # both encoders together ahead of the sampler (their latency-bound launches interleave);
+                # the sampler then waits for both, so nothing shares CUs with it
+                start_energy_encoder()
+                score.after_encode = lambda: stream.wait_stream(side)
         if record and not ode:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -416,7 +423,8 @@ def main():
                                    f"{', DINO-pointwise fused encoders' if args.dino == 'pointwise' else ''}",
                        "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)",
                        "encoder_pipelined": bool(args.pipeline),
-                       "energy_encoder_overlapped": bool(args.energy_overlap) and cfgd["energy"]},
+                       "energy_encoder": (["after the sampler", "beside the sampler", "beside the score encoder"]
+                                          [args.energy_overlap] if cfgd["energy"] else None)},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": load_traffic(B * K, split, tile),
                          "kernel": "pc_step_kernel", "arith": score.heads.arith, "flop_per_launch": flop_launch,

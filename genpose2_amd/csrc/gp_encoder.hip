@@ -635,6 +635,9 @@ struct NarrowArgs {
     int m, ns, nobj;
     float* out;            // (B, m, c_out_total)
     int c_out_total, out_off;
+    const float* w1h;      // split-f16 planes of layers 1 / 2 (sa_narrow_split_kernel) and their exponents
+    const float* w2h;
+    int ew1, ew2;
 };
 
 template <int KG1, int NT1, int NT2, int SPAN>
@@ -736,6 +739,129 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
     }
 }
 
+// Narrow level with layers 1-2 as split-f16 MFMA (v_mfma_f32_16x16x32_f16, three products of hi/lo
+// planes, fp32 accumulation, as sa_split_kernel) and per-column power-of-two activation scaling. A
+// column's values sit in the four lanes (q, n) of its column index n, so the column maximum is a 4-lane
+// max of registers: layer 0's from the gathered projection, layer 1's from its accumulators. The
+// accumulator tiles 2c, 2c+1 of one layer are chunk c of the next layer's B operand as is, so the
+// activations never leave registers. KC0 = 32-deep chunks of layer 0's output (its width / 32).
+template <int KC0, int NT1, int NT2, int SPAN>
+__device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* lds) {
+    constexpr int KG1 = 2 * KC0, KC1 = NT1 / 2;
+    static_assert(NT1 % 2 == 0, "layer-1 tiles pair into 32-deep chunks");
+    constexpr int NA1 = NT1 * KC0 * 2 * 64, NA2 = NT2 * KC1 * 2 * 64;   // f16x8 fragments
+    f16x8* sA1 = reinterpret_cast<f16x8*>(lds);
+    f16x8* sA2 = sA1 + NA1;
+    f32x4* sW0x = reinterpret_cast<f32x4*>(sA2 + NA2);
+    float* sB1 = reinterpret_cast<float*>(sW0x + KG1 * 16);
+    float* sB2 = sB1 + NT1 * 16;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < NA1; i += SA_THREADS) sA1[i] = __builtin_bit_cast(f16x8, ld4(a.w1h + (size_t)i * 4));
+    for (int i = tid; i < NA2; i += SA_THREADS) sA2[i] = __builtin_bit_cast(f16x8, ld4(a.w2h + (size_t)i * 4));
+    for (int ch = tid; ch < KG1 * 16; ch += SA_THREADS)
+        sW0x[ch] = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
+    for (int i = tid; i < NT1 * 16; i += SA_THREADS) sB1[i] = a.b1[i];
+    for (int i = tid; i < NT2 * 16; i += SA_THREADS) sB2[i] = a.b2[i];
+    __syncthreads();
+    const int lane = tid & 63, q = lane >> 4, nn = lane & 15;
+    const int nw = gridDim.x * (SA_THREADS / 64);
+    const int total = a.nobj * a.m;
+    for (int task = blockIdx.x * (SA_THREADS / 64) + (tid >> 6); task < total; task += nw) {
+        const int b = task / a.m;
+        const float* cc = a.cent + (size_t)task * 3;
+        const float cx = cc[0], cy = cc[1], cz = cc[2];
+        f32x4 rmax[NT2];
+#pragma unroll
+        for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ct = 0; ct < SPAN; ++ct) {
+            const int p = a.nbr[(size_t)task * a.ns + ct * 16 + nn];
+            const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
+            f32x4 bf[KG1];
+#pragma unroll
+            for (int g = 0; g < KG1; ++g) bf[g] = ld4(qrow + 16 * g);
+            float mx = 0.f;
+#pragma unroll
+            for (int g = 0; g < KG1; ++g) {
+#pragma clang fp contract(off)
+                float r[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 wx = sW0x[16 * g + 4 * q + j];
+                    r[j] = fmaxf(bf[g][j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
+                    mx = fmaxf(mx, r[j]);
+                }
+                bf[g] = f32x4{r[0], r[1], r[2], r[3]};
+            }
+            // layer 0 -> chunk planes at the column's scale
+            const int E0 = col_exponent(rows_max(mx));
+            f16x8 h0[KC0], l0[KC0];
+#pragma unroll
+            for (int c = 0; c < KC0; ++c) split_pair(bf[2 * c], bf[2 * c + 1], exp2i(14 - E0), h0[c], l0[c]);
+            f32x4 acc1[NT1];
+#pragma unroll
+            for (int t = 0; t < NT1; ++t) acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < KC0; ++c) {
+#pragma unroll
+                for (int t = 0; t < NT1; ++t) {
+                    const f16x8 ah = sA1[((t * KC0 + c) * 2 + 0) * 64 + lane];
+                    const f16x8 al = sA1[((t * KC0 + c) * 2 + 1) * 64 + lane];
+                    acc1[t] = mfma_h(al, h0[c], acc1[t]);
+                    acc1[t] = mfma_h(ah, l0[c], acc1[t]);
+                    acc1[t] = mfma_h(ah, h0[c], acc1[t]);
+                }
+            }
+            const float u0 = exp2i(E0 - 14 - a.ew1);
+            float m1 = 0.f;
+#pragma unroll
+            for (int t = 0; t < NT1; ++t) {
+                acc1[t] = relu4(acc1[t] * u0 + ld4(&sB1[16 * t + 4 * q]));
+                m1 = fmaxf(m1, fmaxf(fmaxf(acc1[t].x, acc1[t].y), fmaxf(acc1[t].z, acc1[t].w)));
+            }
+            const int E1 = col_exponent(rows_max(m1));
+            f16x8 h1[KC1], l1[KC1];
+#pragma unroll
+            for (int c = 0; c < KC1; ++c) split_pair(acc1[2 * c], acc1[2 * c + 1], exp2i(14 - E1), h1[c], l1[c]);
+            f32x4 acc2[NT2];
+#pragma unroll
+            for (int t = 0; t < NT2; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < KC1; ++c) {
+#pragma unroll
+                for (int t = 0; t < NT2; ++t) {
+                    const f16x8 ah = sA2[((t * KC1 + c) * 2 + 0) * 64 + lane];
+                    const f16x8 al = sA2[((t * KC1 + c) * 2 + 1) * 64 + lane];
+                    acc2[t] = mfma_h(al, h1[c], acc2[t]);
+                    acc2[t] = mfma_h(ah, l1[c], acc2[t]);
+                    acc2[t] = mfma_h(ah, h1[c], acc2[t]);
+                }
+            }
+            const float u1 = exp2i(E1 - 14 - a.ew2);
+#pragma unroll
+            for (int t = 0; t < NT2; ++t) {
+                const f32x4 v = relu4(acc2[t] * u1 + ld4(&sB2[16 * t + 4 * q]));
+                rmax[t] = f32x4{fmaxf(rmax[t].x, v.x), fmaxf(rmax[t].y, v.y), fmaxf(rmax[t].z, v.z),
+                                fmaxf(rmax[t].w, v.w)};
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        float* o = a.out + (size_t)task * a.c_out_total + a.out_off + 4 * q;
+#pragma unroll
+        for (int t = 0; t < NT2; ++t) {
+            f32x4 v = rmax[t];
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) {
+                v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
+                v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
+                v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
+                v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
+            }
+            if (nn == 0) st4(o + 16 * t, v);
+        }
+    }
+}
+
 // FPS levels run beside a narrow level's MLP as extra workgroups (blockIdx.y == 0, one per
 // object): the chain's later levels depend only on the previous level's centroids, so they need
 // not sit on the critical path. Level l+1 reads level l's sampled coordinates.
@@ -793,6 +919,23 @@ __global__ __launch_bounds__(SA_THREADS) void sa_narrow_kernel(NarrowArgs a0, Na
         narrow_branch<KG1a, NT1a, NT2a, SPANa>(a0, lds);
     else
         narrow_branch<KG1b, NT1b, NT2b, SPANb>(a1, lds);
+}
+
+// Level 1 with split-f16 layers 1-2 (both branches), FPS levels 2-3 beside it.
+template <int KC0a, int NT1a, int NT2a, int SPANa, int KC0b, int NT1b, int NT2b, int SPANb>
+__global__ __launch_bounds__(SA_THREADS) void sa_narrow_split_kernel(NarrowArgs a0, NarrowArgs a1, FpsSide f) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+    if (blockIdx.y == 0)
+        fps_side(f, reinterpret_cast<char*>(lds));
+    else if (blockIdx.y == 1)
+        narrow_branch_split<KC0a, NT1a, NT2a, SPANa>(a0, lds);
+    else
+        narrow_branch_split<KC0b, NT1b, NT2b, SPANb>(a1, lds);
+}
+
+static size_t narrow_split_lds(int kc0, int nt1, int nt2) {
+    return 16 * ((size_t)nt1 * kc0 * 2 * 64 + (size_t)nt2 * (nt1 / 2) * 2 * 64 + (size_t)2 * kc0 * 16) +
+           sizeof(float) * 16 * (nt1 + nt2);
 }
 
 static size_t narrow_lds(int kg1, int nt1, int nt2) {
@@ -1020,6 +1163,10 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             n.out = out;
             n.out_off = out_off;
             out_off += kWidths[l][br][3];
+            n.w1h = o1[2] >= 0 ? wbuf + o1[2] : nullptr;
+            n.w2h = o2[2] >= 0 ? wbuf + o2[2] : nullptr;
+            n.ew1 = (int)o1[3];
+            n.ew2 = (int)o2[3];
         }
         FpsSide fs = {};   // nobj = 0: the FPS row of workgroups returns at once
         if (side) {
@@ -1042,6 +1189,10 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             const size_t lds = std::max({narrow_lds(1, 1, 2), narrow_lds(2, 2, 4), fps_side_lds(fs)});
             hipLaunchKernelGGL((sa_narrow_kernel<1, 1, 2, 1, 2, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
                                na[1], fs);
+        } else if (na[0].w1h && na[0].w2h && na[1].w1h && na[1].w2h) {
+            const size_t lds = std::max({narrow_split_lds(2, 4, 8), narrow_split_lds(2, 6, 8), fps_side_lds(fs)});
+            hipLaunchKernelGGL((sa_narrow_split_kernel<2, 4, 8, 1, 2, 6, 8, 2>), grid, dim3(SA_THREADS), lds, st,
+                               na[0], na[1], fs);
         } else {
             const size_t lds = std::max({narrow_lds(4, 4, 8), narrow_lds(4, 6, 8), fps_side_lds(fs)});
             hipLaunchKernelGGL((sa_narrow_kernel<4, 4, 8, 1, 4, 6, 8, 2>), grid, dim3(SA_THREADS), lds, st, na[0],

@@ -46,7 +46,8 @@ def pad_vec(b: np.ndarray, n: int) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- encoder
-ENC_SPLIT_LEVELS = (2, 3)   # levels whose layers 1-2 also get split-f16 planes (sa_split_kernel)
+ENC_SPLIT_LEVELS = (1, 2, 3)   # levels whose layers 1-2 also get split-f16 planes (level 1: sa_narrow_split_kernel,
+                               # levels 2-3: sa_split_kernel)
 
 
 def pad32(v: int) -> int:
