@@ -351,11 +351,23 @@ __device__ __forceinline__ void stream_h_step(__amdgpu_buffer_rsrc_t W, const in
     stream_hk_step<KC_HID, G, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc);
 }
 
+// The split trunk's activation bounds and weight exponents (gp_head_weights.hsc). Loaded at kernel entry by
+// the callers: read where they are used, their round trip (a cold L2 line after the kernel boundary) sat
+// on the critical path between the PC update and pose_encoder.0.
+struct SplitScalars {
+    float A0, B0, A2, B2;
+    int ew2, ewh;
+};
+__device__ __forceinline__ SplitScalars load_split_scalars(const gp_head_weights& w) {
+    const f32x4 a = ld4(w.hsc), b = ld4(w.hsc + 4);
+    return SplitScalars{a.x, a.y, a.z, a.w, (int)b.x, (int)b.y};
+}
+
 // head_trunk with the split-f16 GEMMs (same contract and phases; pose_encoder.0 and layer 2 stay fp32).
 template <int NT, int WV>
 __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const float* __restrict__ pobj,
                                                  const float* __restrict__ tproj, const int* obj_of_col,
-                                                 HeadSmem<NT, WV>& sm, int trace_slot = 0) {
+                                                 HeadSmem<NT, WV>& sm, int trace_slot, const SplitScalars hs) {
     constexpr int TPW = 16 / WV;   // output tiles per wave; tiles (2c, 2c+1) form 32-deep chunk c
     static_assert(TPW % 2 == 0, "split trunk pairs a wave's output tiles into 32-deep chunks");
     constexpr int CPW = TPW / 2;
@@ -385,8 +397,8 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     __syncthreads();
     PC_MARK(1);
     // ---- per-candidate exponents: bound1 >= |pose_encoder.0 out|, bound2 >= |pose_encoder.2 out|
-    const float A0 = w.hsc[0], B0 = w.hsc[1], A2 = w.hsc[2], B2 = w.hsc[3];
-    const int ew2 = (int)w.hsc[4], ewh = (int)w.hsc[5];
+    const float A0 = hs.A0, B0 = hs.B0, A2 = hs.A2, B2 = hs.B2;
+    const int ew2 = hs.ew2, ewh = hs.ewh;
     f32x4 bf[NT];
     float s1[NT], s2[NT], u2[NT], uh[NT], sh[NT];
 #pragma unroll

@@ -69,6 +69,8 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
     __shared__ double y0s[ROWS * 9], y1s[ROWS * 9], esq[NTH];
     const int tid = threadIdx.x;
     const int r0 = blockIdx.x * ROWS;
+    SplitScalars hs = {};
+    if constexpr (SPLIT) hs = load_split_scalars(a.w);
     const double* y = a.y;
     const double* kin[ODE_NK];
 #pragma unroll
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
     }
     if constexpr (SPLIT)
-        head_trunk_split<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
+        head_trunk_split<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm, 0, hs);
     else
         head_trunk<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
     double sq = 0.0;   // this thread's (err/scale)^2 terms, its elements in increasing order

@@ -86,6 +86,8 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
     __shared__ HeadSmem<1, EVAL_WV> sm;
     __shared__ int obj[16];
     const int r0 = blockIdx.x * 16;
+    SplitScalars hs = {};
+    if constexpr (SPLIT) hs = load_split_scalars(w);
     stage_small_weights<1, EVAL_WV>(w, sm);
     for (int i = threadIdx.x; i < 256; i += EVAL_WV * 64) {
         const int c = i >> 4, j = i & 15;
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
         obj[threadIdx.x] = (r < rows ? r : rows - 1) / kper;
     }
     if constexpr (SPLIT)
-        head_trunk_split<1, EVAL_WV>(w, pobj, tproj, obj, sm);
+        head_trunk_split<1, EVAL_WV>(w, pobj, tproj, obj, sm, 0, hs);
     else
         head_trunk<1, EVAL_WV>(w, pobj, tproj, obj, sm);
     if (MODE == 0) {
@@ -185,6 +187,8 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r0 = blockIdx.x * ROWS;
     const int trace_slot = i & 1;
+    SplitScalars hs = {};
+    if constexpr (SPLIT) hs = load_split_scalars(a.w);   // in flight across the update
     PC_MARK(0);
     if (wid < NT) {
         // ---- every load first and unconditional (rows clamped: a guarded load becomes a branch,
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     }
     stage_small_weights<NT, WV, 64 * NT>(a.w, sm);
     if constexpr (SPLIT)
-        head_trunk_split<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
+        head_trunk_split<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
     else
         head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
     PC_MARK(7);
