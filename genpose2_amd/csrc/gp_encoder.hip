@@ -65,8 +65,26 @@ extern "C" int gp_debug_sa_trace(int sel, unsigned long long* host) {
         return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_sa_trace_sel), &sel, sizeof(int)) == hipSuccess ? 0 : -1;
 }
+// split-f16 levels (8 waves per workgroup): marks 0 start, 1 staged + barrier, 2 layer-0 gather + barrier,
+// 3 layer-1 stream done, 4 column-max barrier, 5 layer-1 planes written, 6 layer-2 barrier, 7 end
+__device__ unsigned long long g_split_trace[8192 * 8 * 8];
+__device__ int g_split_trace_sel = -1;
+#define SPLIT_MARK(a, k)                                                                                   \
+    do {                                                                                                   \
+        const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                               \
+        if ((a).tag == g_split_trace_sel && (threadIdx.x & 63) == 0 && wg_ < 8192)                         \
+            g_split_trace[(wg_ * 8 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime();       \
+    } while (0)
+extern "C" int gp_debug_split_trace(int sel, unsigned long long* host) {
+    if (host) return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_split_trace), sizeof(g_split_trace)) == hipSuccess ? 0 : -1;
+    void* ptr = nullptr;
+    if (hipGetSymbolAddress(&ptr, HIP_SYMBOL(g_split_trace)) != hipSuccess || hipMemset(ptr, 0, sizeof(g_split_trace)) != hipSuccess)
+        return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_split_trace_sel), &sel, sizeof(int)) == hipSuccess ? 0 : -1;
+}
 #else
 #define SA_MARK(k) ((void)0)
+#define SPLIT_MARK(a, k) ((void)0)
 #endif
 
 constexpr int SA_THREADS = 256;
@@ -389,6 +407,7 @@ struct SplitArgs {
     int ew[2];                        // weight exponents
     float* out;                       // (B, m, c_out_total)
     int c_out_total, out_off;
+    int tag;                          // level * 2 + branch (tuning traces)
 };
 
 __device__ __forceinline__ float max4(f32x4 v) { return fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)); }
@@ -484,7 +503,9 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
         stream_hk_step<KC0, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
         if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, col0, wid, lane);
         __syncthreads();
+        SPLIT_MARK(a, 2);
         stream_hk_step<KC0, D, KC0 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
+        SPLIT_MARK(a, 3);
         // unscale (exact powers of two), bias, ReLU, partial column maxima
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
@@ -501,6 +522,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
             if (q == 0) pm[wid * C + ct * 16 + n] = M;
         }
         __syncthreads();   // every read of layer 0's planes is done; the partial maxima are visible
+        SPLIT_MARK(a, 4);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             float M = 0.f;
@@ -517,6 +539,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
                 X[((oc * CT + ct) * 2 + 1) * 64 + lane] = lo;
             }
         }
+        SPLIT_MARK(a, 5);
     }
 }
 
@@ -543,6 +566,7 @@ __device__ __forceinline__ void split_layer2(const SplitArgs& a, const f16x8* X,
         for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
     stream_hk_step<KC1, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
     __syncthreads();   // layer 1's planes are complete
+    SPLIT_MARK(a, 6);
     stream_hk_step<KC1, D, KC1 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
     const int span = a.ns >> 4;   // column tiles per centroid (1 or 2)
 #pragma unroll
@@ -584,9 +608,11 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.y, col0 = blockIdx.x * C;
+    SPLIT_MARK(a, 0);
     for (int ch = tid; ch < KC0 * 32; ch += SPLIT_WV * 64)   // packed layer-0 fragment of channel ch, q = 0
         w0x[ch] = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
     __syncthreads();
+    SPLIT_MARK(a, 1);
     int e1[CT];
     // layer-1 output chunks of this wave: wid, wid + 8, ... below OC1
     constexpr int NC1_HI = (OC1 + SPLIT_WV - 1) / SPLIT_WV;
@@ -597,6 +623,7 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
         split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1);
     static_assert(OC2 % SPLIT_WV == 0, "layer-2 chunks spread evenly over the waves");
     split_layer2<CT, OC1, OC2 / SPLIT_WV, D>(a, X, e1, b, col0, wid, lane, OC2);
+    SPLIT_MARK(a, 7);
 }
 
 // Both branches of a level per launch (blockIdx.z = branch).
@@ -1231,6 +1258,7 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             a.out = out;
             a.c_out_total = kCout[l];
             a.out_off = off_out;
+            a.tag = l * 2 + br;
             off_out += kWidths[l][br][3];
             GP_REQUIRE(a.cols % (16 * CT) == 0 && (16 * CT) % a.ns == 0,
                        "encoder: level %d columns %d do not tile by %d", l, a.cols, 16 * CT);

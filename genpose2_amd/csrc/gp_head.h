@@ -471,30 +471,38 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     // ---- head layer 1 (pose block 256 -> 3x256)
     stream_h_step<DH, KC_HID + DH, 3 * TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc);
     PC_MARK(5);
-    // ---- ReLU -> head layer 2 partial dot products (fp32, as head_trunk)
+    // ---- ReLU -> head layer 2 partial dot products (fp32 VALU, one FMA chain per output: at 64
+    //      candidates this is the PC step's longest serial phase, ~1000 instructions per wave with
+    //      separately rounded products and sums; fp32 MFMAs for it measured slower, 10.1k vs 8.1k cycles)
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
+        float p[NT][3];
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) p[ct][0] = p[ct][1] = p[ct][2] = 0.f;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {   // each weight fragment read once for all column tiles
+            const int ch = 16 * (wid * TPW + t) + 4 * q;
+            const f32x4 w0 = ld4(&sm.h2w[(h * 3 + 0) * HID + ch]);
+            const f32x4 w1 = ld4(&sm.h2w[(h * 3 + 1) * HID + ch]);
+            const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) {
+                const f32x4 u = relu4(acc[h * TPW + t][ct] * uh[ct]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    p[ct][0] = __builtin_fmaf(u[j], w0[j], p[ct][0]);
+                    p[ct][1] = __builtin_fmaf(u[j], w1[j], p[ct][1]);
+                    p[ct][2] = __builtin_fmaf(u[j], w2[j], p[ct][2]);
+                }
+            }
+        }
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-            float p0 = 0.f, p1 = 0.f, p2 = 0.f;
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) {
-                const f32x4 u = relu4(acc[h * TPW + t][ct] * uh[ct]);
-                const int ch = 16 * (wid * TPW + t) + 4 * q;
-                const f32x4 w0 = ld4(&sm.h2w[(h * 3 + 0) * HID + ch]);
-                const f32x4 w1 = ld4(&sm.h2w[(h * 3 + 1) * HID + ch]);
-                const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
-                p0 += u.x * w0.x + u.y * w0.y + u.z * w0.z + u.w * w0.w;
-                p1 += u.x * w1.x + u.y * w1.y + u.z * w1.z + u.w * w1.w;
-                p2 += u.x * w2.x + u.y * w2.y + u.z * w2.z + u.w * w2.w;
-            }
-            p0 = rows_sum(p0);
-            p1 = rows_sum(p1);
-            p2 = rows_sum(p2);
+            const float s0 = rows_sum(p[ct][0]), s1 = rows_sum(p[ct][1]), s2 = rows_sum(p[ct][2]);
             if (q == 0) {
-                sm.red[ct * 16 + n][h * 3 + 0][wid] = p0;
-                sm.red[ct * 16 + n][h * 3 + 1][wid] = p1;
-                sm.red[ct * 16 + n][h * 3 + 2][wid] = p2;
+                sm.red[ct * 16 + n][h * 3 + 0][wid] = s0;
+                sm.red[ct * 16 + n][h * 3 + 1][wid] = s1;
+                sm.red[ct * 16 + n][h * 3 + 2][wid] = s2;
             }
         }
     }
