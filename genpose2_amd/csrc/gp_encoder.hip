@@ -417,16 +417,27 @@ __device__ __forceinline__ int col_exponent(float m) { return m > 1e-30f ? ilog2
 
 // Layer-0 planes of column tile ct: lane (q, n) gathers column n's channels 32c + 4q + j and
 // 32c + 16 + 4q + j (j < 4) of every chunk c -- exactly its B fragments.
+// Neighbour index and centroid of lane column n of column tile ct: loaded at kernel entry, one round trip
+// ahead of the layer-0 gather that depends on them.
+struct Gather0Pre {
+    int p;
+    float cx, cy, cz;
+};
+__device__ __forceinline__ Gather0Pre split_gather0_pre(const SplitArgs& a, int b, int col0, int ct, int lane) {
+    const int g = col0 + ct * 16 + (lane & 15);
+    const int m = g / a.ns, s = g - (g / a.ns) * a.ns;
+    const float* cc = a.cent + ((size_t)b * a.m + m) * 3;
+    return Gather0Pre{a.nbr[((size_t)b * a.m + m) * a.ns + s], cc[0], cc[1], cc[2]};
+}
+
 template <int CT, int KC0>
 __device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, const f32x4* w0x, int b,
-                                              int col0, int ct, int lane) {
+                                              int ct, int lane, const Gather0Pre pre) {
 #pragma clang fp contract(off)
     const int q = lane >> 4, n = lane & 15;
-    const int col = ct * 16 + n, g = col0 + col;
-    const int m = g / a.ns, s = g - (g / a.ns) * a.ns;
-    const int p = a.nbr[((size_t)b * a.m + m) * a.ns + s];
-    const float* cc = a.cent + ((size_t)b * a.m + m) * 3;
-    const float cx = cc[0], cy = cc[1], cz = cc[2];
+    const int col = ct * 16 + n;
+    const int p = pre.p;
+    const float cx = pre.cx, cy = pre.cy, cz = pre.cz;
     const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
     f32x4 v[KC0][2];
 #pragma unroll
@@ -465,14 +476,15 @@ __device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int*
 // column's exponent in e1[ct] (for lane column n). Executes the same two barriers in every wave.
 template <int CT, int KC0, int NC, int D>
 __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* w0x,
-                                             int b, int col0, int wid, int lane, int oc1, int (&e1)[CT]) {
+                                             int b, int col0, int wid, int lane, int oc1, int (&e1)[CT],
+                                             const Gather0Pre pre) {
     constexpr int C = 16 * CT;
     const int q = lane >> 4, n = lane & 15;
     float pmax[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) pmax[ct] = 0.f;
     if constexpr (NC == 0) {
-        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, col0, wid, lane);
+        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, wid, lane, pre);
         __syncthreads();
         if (q == 0)
 #pragma unroll
@@ -501,7 +513,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
         stream_hk_step<KC0, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
-        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, col0, wid, lane);
+        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, wid, lane, pre);
         __syncthreads();
         SPLIT_MARK(a, 2);
         stream_hk_step<KC0, D, KC0 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
@@ -598,9 +610,12 @@ __device__ __forceinline__ void split_layer2(const SplitArgs& a, const f16x8* X,
     }
 }
 
+#ifndef SPLIT_D
+#define SPLIT_D 2   // 32-deep weight chunks in flight per layer
+#endif
 template <int CT, int KC0, int OC1, int OC2>
 __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
-    constexpr int C = 16 * CT, KX = KC0 > OC1 ? KC0 : OC1, D = 2;
+    constexpr int C = 16 * CT, KX = KC0 > OC1 ? KC0 : OC1, D = SPLIT_D;
     f16x8* X = reinterpret_cast<f16x8*>(smem);                       // [chunk][ct][plane][lane]
     f32x4* w0x = reinterpret_cast<f32x4*>(smem + (size_t)KX * CT * 2048);   // (wx, wy, wz, 0) per channel
     float* pm = reinterpret_cast<float*>(w0x + KC0 * 32);           // [wave][column] partial maxima
@@ -609,6 +624,7 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.y, col0 = blockIdx.x * C;
     SPLIT_MARK(a, 0);
+    const Gather0Pre pre = wid < CT ? split_gather0_pre(a, b, col0, wid, lane) : Gather0Pre{0, 0.f, 0.f, 0.f};
     for (int ch = tid; ch < KC0 * 32; ch += SPLIT_WV * 64)   // packed layer-0 fragment of channel ch, q = 0
         w0x[ch] = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
     __syncthreads();
@@ -618,9 +634,9 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     constexpr int NC1_HI = (OC1 + SPLIT_WV - 1) / SPLIT_WV;
     const int nc1 = wid < OC1 % SPLIT_WV || OC1 % SPLIT_WV == 0 ? NC1_HI : NC1_HI - 1;
     if (nc1 == NC1_HI)
-        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1);
+        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
     else
-        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1);
+        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
     static_assert(OC2 % SPLIT_WV == 0, "layer-2 chunks spread evenly over the waves");
     split_layer2<CT, OC1, OC2 / SPLIT_WV, D>(a, X, e1, b, col0, wid, lane, OC2);
     SPLIT_MARK(a, 7);
