@@ -83,6 +83,112 @@ __global__ __launch_bounds__(FUS_THREADS) void linear_kernel(const float* __rest
     }
 }
 
+// LDS-tiled form for large token counts: a workgroup owns 128 tokens x (32 * WN) outputs, 4 waves as 2 x 2
+// of 64 tokens x (16 * WN) outputs, so every fragment read from LDS feeds 4 (or WN) MFMAs and every
+// operand element is fetched from L2 once per workgroup. K advances 32 per stage through two LDS buffers
+// (one barrier per stage; the next stage's global loads are in flight while this stage computes). Both
+// operands are stored in LDS in fragment order [k-group][q][row] x float4: a lane's ds_read_b128 of row r,
+// k-slice q lands in a distinct bank group (conflict-free).
+constexpr int LK_BM = 128, LK_KC = 32;
+template <int WN, int ACT>
+__global__ __launch_bounds__(FUS_THREADS, 2) void linear_lds_kernel(const float* __restrict__ x, int ldx, int m, int k,
+                                                                    const float* __restrict__ w,
+                                                                    const float* __restrict__ bias, int n,
+                                                                    float* __restrict__ y, int ldy) {
+    constexpr int BN = 32 * WN;                        // outputs per workgroup
+    constexpr int XF4 = LK_BM * LK_KC / 4, WF4 = BN * LK_KC / 4;   // float4s per stage
+    __shared__ f32x4 sx[2][XF4];
+    __shared__ f32x4 sw[2][WF4];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int q = lane >> 4, r = lane & 15;
+    const int tok0 = blockIdx.x * LK_BM, out0 = blockIdx.y * BN;
+    const int ntile = n >> 4;
+    // staging: float4 e of a stage = (row, k-group g, slice qq); loads are row-major coalesced
+    constexpr int XPT = XF4 / FUS_THREADS, WPT = (WF4 + FUS_THREADS - 1) / FUS_THREADS;
+    const float* xs[XPT];
+    int xdst[XPT];
+#pragma unroll
+    for (int u = 0; u < XPT; ++u) {
+        const int e = tid + u * FUS_THREADS, row = e >> 3, g = (e >> 2) & 1, qq = e & 3;
+        xs[u] = x + (size_t)min(tok0 + row, m - 1) * ldx + 16 * g + 4 * qq;
+        xdst[u] = (g * 4 + qq) * LK_BM + row;
+    }
+    const float* ws[WPT];
+    int wdst[WPT];
+#pragma unroll
+    for (int u = 0; u < WPT; ++u) {
+        const int e = min(tid + u * FUS_THREADS, WF4 - 1), row = e >> 3, g = (e >> 2) & 1, qq = e & 3;
+        ws[u] = w + (size_t)min(out0 + row, n - 1) * k + 16 * g + 4 * qq;
+        wdst[u] = (g * 4 + qq) * BN + row;
+    }
+    f32x4 px[XPT], pw[WPT];
+    auto fetch = [&](int kk) {
+#pragma unroll
+        for (int u = 0; u < XPT; ++u) px[u] = ld4(xs[u] + kk);
+#pragma unroll
+        for (int u = 0; u < WPT; ++u) pw[u] = ld4(ws[u] + kk);
+    };
+    auto stash = [&](int b) {
+#pragma unroll
+        for (int u = 0; u < XPT; ++u) sx[b][xdst[u]] = px[u];
+#pragma unroll
+        for (int u = 0; u < WPT; ++u)
+            if (WF4 % FUS_THREADS == 0 || tid + u * FUS_THREADS < WF4) sw[b][wdst[u]] = pw[u];
+    };
+    const int wm = wid & 1, wn = wid >> 1;
+    f32x4 acc[WN][4];
+#pragma unroll
+    for (int a = 0; a < WN; ++a)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int stages = k / LK_KC;
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    for (int s = 0; s < stages; ++s) {
+        const int b = s & 1;
+        if (s + 1 < stages) fetch((s + 1) * LK_KC);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            f32x4 af[WN], bf[4];
+#pragma unroll
+            for (int a = 0; a < WN; ++a) af[a] = sw[b][(g * 4 + q) * BN + wn * 16 * WN + 16 * a + r];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) bf[t] = sx[b][(g * 4 + q) * LK_BM + wm * 64 + 16 * t + r];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int a = 0; a < WN; ++a)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) acc[a][t] = mfma4(af[a][j], bf[t][j], acc[a][t]);
+        }
+        if (s + 1 < stages) stash(b ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < WN; ++a) {
+        const int T = (out0 >> 4) + wn * WN + a;
+        if (T >= ntile) continue;
+        const f32x4 bv = bias ? ld4(bias + 16 * T + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int tok = tok0 + wm * 64 + 16 * t + r;
+            if (tok >= m) continue;
+            f32x4 v = acc[a][t] + bv;
+            if (ACT == 1) v = relu4(v);
+            if (ACT == 2) v = f32x4{sigmoidf(v.x), sigmoidf(v.y), sigmoidf(v.z), sigmoidf(v.w)};
+            st4(y + (size_t)tok * ldy + 16 * T + 4 * q, v);
+        }
+    }
+}
+
+template <int WN, int ACT>
+static void launch_linear_lds(const float* x, int ldx, int m, int k, const float* w, const float* bias, int n, float* y,
+                              int ldy, hipStream_t st) {
+    const dim3 grid((m + LK_BM - 1) / LK_BM, (n + 32 * WN - 1) / (32 * WN));
+    hipLaunchKernelGGL((linear_lds_kernel<WN, ACT>), grid, dim3(FUS_THREADS), 0, st, x, ldx, m, k, w, bias, n, y, ldy);
+}
+
 template <int TN, int ACT>
 static void launch_linear(const float* x, int ldx, int m, int k, const float* w, const float* bias, int n, float* y,
                           int ldy, hipStream_t st) {
@@ -108,6 +214,16 @@ extern "C" int gp_linear(const float* x, int ldx, int m, int k, const float* w, 
                "linear: pointers must be 16-byte aligned");
     GP_REQUIRE(act >= 0 && act <= 2, "linear: act %d", act);
     if (!m) return GP_OK;
+    if (m >= 1024 && k % LK_KC == 0 && n >= 64) {   // LDS-tiled: 128 tokens x 128 (or 64) outputs per workgroup
+        const bool wide = n % 128 == 0;   // else 64-output columns (n = 96, 192, 288: less padding)
+#define GP_LIN_LDS(WN)                                                                                     \
+        if (act == 0) launch_linear_lds<WN, 0>(x, ldx, m, k, w, bias, n, y, ldy, st);                      \
+        else if (act == 1) launch_linear_lds<WN, 1>(x, ldx, m, k, w, bias, n, y, ldy, st);                 \
+        else launch_linear_lds<WN, 2>(x, ldx, m, k, w, bias, n, y, ldy, st);
+        if (wide) { GP_LIN_LDS(4) } else { GP_LIN_LDS(2) }
+#undef GP_LIN_LDS
+        return gp_check_launch("linear_lds_kernel");
+    }
     // output tiles per wave: the widest that divides n into whole workgroup columns
     if (n % 128 == 0) launch_linear_act<4>(act, x, ldx, m, k, w, bias, n, y, ldy, st);
     else if (n % 96 == 0) launch_linear_act<3>(act, x, ldx, m, k, w, bias, n, y, ldy, st);

@@ -53,7 +53,9 @@ def fus_model(fus_sd):
 
 # ---------------------------------------------------------------- blocks
 @pytest.mark.parametrize("m,k,n,act,pad", [(100, 96, 288, 0, 0), (4096, 256, 1024, 1, 0), (37, 384, 96, 2, 0),
-                                           (513, 1024, 192, 1, 32), (64, 2048, 1024, 0, 16), (1, 1024, 3072, 0, 0)])
+                                           (513, 1024, 192, 1, 32), (64, 2048, 1024, 0, 16), (1, 1024, 3072, 0, 0),
+                                           (1500, 96, 288, 1, 0), (2000, 384, 96, 2, 16), (1031, 4096, 1024, 0, 0),
+                                           (4096, 1024, 4096, 1, 0)])
 def test_linear_vs_torch(lib, m, k, n, act, pad):
     from genpose2_amd._lib import check
     g = torch.Generator().manual_seed(m + k + n)
