@@ -134,6 +134,14 @@ def cpu_baseline(cfg, config_id, threads, sample_objects, reps=3):
            "cpu_model": model, "physical_cores": phys, "cpus_available": avail,
            "torch_threads": torch.get_num_threads(),
            "float32_matmul_precision": torch.get_float32_matmul_precision()}
+    # the bounded sample against the whole batch, measured once on the GPU host (scripts/cpu_full_vs_sample.py)
+    chk = os.path.join(REPO, "profiles", "r2", "cpu_full_vs_sample.json")
+    if os.path.exists(chk) and config_id == 4:
+        with open(chk) as f:
+            c = json.load(f)
+        out["full_batch_check"] = {"full_256_objects_value": c["full_256_objects"]["value"],
+                                   "sample_16_objects_value": c["sample_16_objects"]["value"],
+                                   "threads": c["threads"], "source": os.path.relpath(chk, REPO)}
     # the oracle/reference time ratio measured in the build container on identical
     # inputs (oracle/calibrate_cpu.py); converts the port figure to reference terms
     for cal in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "cpu_calibration.json")), reverse=True):
