@@ -425,6 +425,7 @@ struct Gather0Pre {
 };
 __device__ __forceinline__ Gather0Pre split_gather0_pre(const SplitArgs& a, int b, int col0, int ct, int lane) {
     const int g = col0 + ct * 16 + (lane & 15);
+    if (g >= a.cols) return Gather0Pre{0, 0.f, 0.f, 0.f};   // past the last centroid (ragged last workgroup)
     const int m = g / a.ns, s = g - (g / a.ns) * a.ns;
     const float* cc = a.cent + ((size_t)b * a.m + m) * 3;
     return Gather0Pre{a.nbr[((size_t)b * a.m + m) * a.ns + s], cc[0], cc[1], cc[2]};
@@ -602,20 +603,17 @@ __device__ __forceinline__ void split_layer2(const SplitArgs& a, const f16x8* X,
                 r.z = fmaxf(r.z, __shfl_xor(r.z, off, 64));
                 r.w = fmaxf(r.w, __shfl_xor(r.w, off, 64));
             }
-            if (n == 0) {
-                const int mi = (col0 + ct * 16) / a.ns;
+            const int mi = (col0 + ct * 16) / a.ns;
+            if (n == 0 && mi < a.m) {
                 st4(a.out + ((size_t)b * a.m + mi) * a.c_out_total + a.out_off + 16 * T[t] + 4 * q, r);
             }
         }
     }
 }
 
-#ifndef SPLIT_D
-#define SPLIT_D 2   // 32-deep weight chunks in flight per layer
-#endif
-template <int CT, int KC0, int OC1, int OC2>
+template <int CT, int D, int KC0, int OC1, int OC2>
 __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
-    constexpr int C = 16 * CT, KX = KC0 > OC1 ? KC0 : OC1, D = SPLIT_D;
+    constexpr int C = 16 * CT, KX = KC0 > OC1 ? KC0 : OC1;
     f16x8* X = reinterpret_cast<f16x8*>(smem);                       // [chunk][ct][plane][lane]
     f32x4* w0x = reinterpret_cast<f32x4*>(smem + (size_t)KX * CT * 2048);   // (wx, wy, wz, 0) per channel
     float* pm = reinterpret_cast<float*>(w0x + KC0 * 32);           // [wave][column] partial maxima
@@ -643,15 +641,35 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
 }
 
 // Both branches of a level per launch (blockIdx.z = branch).
-template <int CT, int KC0, int OC1A, int OC2A, int OC1B, int OC2B>
+// CT column tiles per workgroup (whole centroids; the last workgroup of a branch may be ragged), D
+// 32-deep weight chunks in flight per layer.
+template <int CT, int D, int KC0, int OC1A, int OC2A, int OC1B, int OC2B>
 __global__ __launch_bounds__(SPLIT_WV * 64) void sa_split_kernel(SplitArgs a0, SplitArgs a1) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.z == 0) {
-        if ((int)blockIdx.x * 16 * CT < a0.cols) sa_split_body<CT, KC0, OC1A, OC2A>(a0, smem);
+        if ((int)blockIdx.x * 16 * CT < a0.cols) sa_split_body<CT, D, KC0, OC1A, OC2A>(a0, smem);
     } else {
-        if ((int)blockIdx.x * 16 * CT < a1.cols) sa_split_body<CT, KC0, OC1B, OC2B>(a1, smem);
+        if ((int)blockIdx.x * 16 * CT < a1.cols) sa_split_body<CT, D, KC0, OC1B, OC2B>(a1, smem);
     }
 }
+
+// Column tiles per workgroup at levels 2 / 3 and the weight ring depth. Level 3 (101 KB of LDS at 4
+// tiles: one workgroup per CU either way) takes 6 tiles, the most LDS holds: every weight fragment
+// streamed from L2 then feeds 6 column tiles (1.69 -> 1.31 ms at B=256). Level 2 keeps 4 tiles, two
+// workgroups per CU whose gather and barrier phases overlap each other's streams (8 tiles: 0.87 ->
+// 1.40 ms).
+#ifndef SPLIT_CT2
+#define SPLIT_CT2 4
+#endif
+#ifndef SPLIT_CT3
+#define SPLIT_CT3 6
+#endif
+#ifndef SPLIT_D2
+#define SPLIT_D2 2
+#endif
+#ifndef SPLIT_D3
+#define SPLIT_D3 2
+#endif
 
 template <int CT, int KC0, int OC1>
 static size_t sa_split_lds() {
@@ -683,6 +701,38 @@ struct NarrowArgs {
     int ew1, ew2;
 };
 
+// A centroid's gathered layer-0 projections (SPAN column tiles x KG k-groups) and its coordinates.
+// The task loops run a two-stage software pipeline over a wave's centroids: the neighbour indices
+// of centroid i+2 and the projection rows of centroid i+1 are in flight while centroid i computes,
+// so the dependent index -> row round trips leave the critical path.
+template <int SPAN, int KG>
+struct NarrowGather {
+    f32x4 q[SPAN][KG];
+    float cx, cy, cz;
+};
+
+template <int SPAN>
+__device__ __forceinline__ void narrow_nbr(const NarrowArgs& a, int task, int nn, int (&p)[SPAN]) {
+#pragma unroll
+    for (int ct = 0; ct < SPAN; ++ct) p[ct] = a.nbr[(size_t)task * a.ns + ct * 16 + nn];
+}
+
+template <int SPAN, int KG>
+__device__ __forceinline__ void narrow_fetch(const NarrowArgs& a, int task, const int (&p)[SPAN], int q,
+                                             NarrowGather<SPAN, KG>& g) {
+    const int b = task / a.m;
+    const float* cc = a.cent + (size_t)task * 3;
+    g.cx = cc[0];
+    g.cy = cc[1];
+    g.cz = cc[2];
+#pragma unroll
+    for (int ct = 0; ct < SPAN; ++ct) {
+        const float* qrow = a.qin + ((size_t)b * a.n_prev + p[ct]) * a.q_stride + a.q_off + 4 * q;
+#pragma unroll
+        for (int g2 = 0; g2 < KG; ++g2) g.q[ct][g2] = ld4(qrow + 16 * g2);
+    }
+}
+
 template <int KG1, int NT1, int NT2, int SPAN>
 __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
     constexpr int KG2 = NT1;
@@ -703,20 +753,25 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
     const int lane = tid & 63, q = lane >> 4, nn = lane & 15;
     const int nw = gridDim.x * (SA_THREADS / 64);
     const int total = a.nobj * a.m;
-    for (int task = blockIdx.x * (SA_THREADS / 64) + (tid >> 6); task < total; task += nw) {
-        const int b = task / a.m;
-        const float* cc = a.cent + (size_t)task * 3;
-        const float cx = cc[0], cy = cc[1], cz = cc[2];
+    int task = blockIdx.x * (SA_THREADS / 64) + (tid >> 6);
+    if (task >= total) return;
+    int pn[SPAN];
+    NarrowGather<SPAN, KG1> cur, nxt;
+    narrow_nbr<SPAN>(a, task, nn, pn);
+    narrow_fetch<SPAN, KG1>(a, task, pn, q, cur);
+    if (task + nw < total) narrow_nbr<SPAN>(a, task + nw, nn, pn);
+    for (; task < total; task += nw) {
+        if (task + nw < total) {
+            narrow_fetch<SPAN, KG1>(a, task + nw, pn, q, nxt);
+            if (task + 2 * nw < total) narrow_nbr<SPAN>(a, task + 2 * nw, nn, pn);
+        }
+        const float cx = cur.cx, cy = cur.cy, cz = cur.cz;
         f32x4 rmax[NT2];
 #pragma unroll
         for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{0.f, 0.f, 0.f, 0.f};   // max of ReLU outputs
 #pragma unroll
         for (int ct = 0; ct < SPAN; ++ct) {
-            const int p = a.nbr[(size_t)task * a.ns + ct * 16 + nn];
-            const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
             f32x4 bf[KG1];
-#pragma unroll
-            for (int g = 0; g < KG1; ++g) bf[g] = ld4(qrow + 16 * g);
 #pragma unroll
             for (int g = 0; g < KG1; ++g) {
 #pragma clang fp contract(off)
@@ -724,7 +779,7 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const f32x4 wx = sW0x[16 * g + 4 * q + j];
-                    r[j] = fmaxf(bf[g][j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
+                    r[j] = fmaxf(cur.q[ct][g][j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
                 }
                 bf[g] = f32x4{r[0], r[1], r[2], r[3]};
             }
@@ -779,6 +834,7 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
             }
             if (nn == 0) st4(o + 16 * t, v);
         }
+        cur = nxt;
     }
 }
 
@@ -809,20 +865,25 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
     const int lane = tid & 63, q = lane >> 4, nn = lane & 15;
     const int nw = gridDim.x * (SA_THREADS / 64);
     const int total = a.nobj * a.m;
-    for (int task = blockIdx.x * (SA_THREADS / 64) + (tid >> 6); task < total; task += nw) {
-        const int b = task / a.m;
-        const float* cc = a.cent + (size_t)task * 3;
-        const float cx = cc[0], cy = cc[1], cz = cc[2];
+    int task = blockIdx.x * (SA_THREADS / 64) + (tid >> 6);
+    if (task >= total) return;
+    int pn[SPAN];
+    NarrowGather<SPAN, KG1> cur, nxt;
+    narrow_nbr<SPAN>(a, task, nn, pn);
+    narrow_fetch<SPAN, KG1>(a, task, pn, q, cur);
+    if (task + nw < total) narrow_nbr<SPAN>(a, task + nw, nn, pn);
+    for (; task < total; task += nw) {
+        if (task + nw < total) {
+            narrow_fetch<SPAN, KG1>(a, task + nw, pn, q, nxt);
+            if (task + 2 * nw < total) narrow_nbr<SPAN>(a, task + 2 * nw, nn, pn);
+        }
+        const float cx = cur.cx, cy = cur.cy, cz = cur.cz;
         f32x4 rmax[NT2];
 #pragma unroll
         for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ct = 0; ct < SPAN; ++ct) {
-            const int p = a.nbr[(size_t)task * a.ns + ct * 16 + nn];
-            const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
             f32x4 bf[KG1];
-#pragma unroll
-            for (int g = 0; g < KG1; ++g) bf[g] = ld4(qrow + 16 * g);
             float mx = 0.f;
 #pragma unroll
             for (int g = 0; g < KG1; ++g) {
@@ -831,7 +892,7 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const f32x4 wx = sW0x[16 * g + 4 * q + j];
-                    r[j] = fmaxf(bf[g][j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
+                    r[j] = fmaxf(cur.q[ct][g][j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
                     mx = fmaxf(mx, r[j]);
                 }
                 bf[g] = f32x4{r[0], r[1], r[2], r[3]};
@@ -902,6 +963,7 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
             }
             if (nn == 0) st4(o + 16 * t, v);
         }
+        cur = nxt;
     }
 }
 
@@ -976,6 +1038,22 @@ __global__ __launch_bounds__(SA_THREADS) void sa_narrow_split_kernel(NarrowArgs 
         narrow_branch_split<KC0b, NT1b, NT2b, SPANb>(a1, lds);
 }
 
+// Level 0: the 16-wide branch in exact fp32 (its layer 0 does not fill a 32-deep chunk), the 32-wide
+// branch with split-f16 layers 1-2 (5x fewer MFMA cycles than fp32 16x16x4), FPS level 1 beside them.
+template <int KG1a, int NT1a, int NT2a, int SPANa, int KC0b, int NT1b, int NT2b, int SPANb>
+__global__ __launch_bounds__(SA_THREADS) void sa_narrow_mixed_kernel(NarrowArgs a0, NarrowArgs a1, FpsSide f) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 lds[];
+#ifdef NARROW_PROBE   // timing probes only (results are wrong): 1 = FPS only, 2 = branch a only, 3 = branch b only
+    if (blockIdx.y != (NARROW_PROBE - 1)) return;
+#endif
+    if (blockIdx.y == 0)
+        fps_side(f, reinterpret_cast<char*>(lds));
+    else if (blockIdx.y == 1)
+        narrow_branch<KG1a, NT1a, NT2a, SPANa>(a0, lds);
+    else
+        narrow_branch_split<KC0b, NT1b, NT2b, SPANb>(a1, lds);
+}
+
 static size_t narrow_split_lds(int kc0, int nt1, int nt2) {
     return 16 * ((size_t)nt1 * kc0 * 2 * 64 + (size_t)nt2 * (nt1 / 2) * 2 * 64 + (size_t)2 * kc0 * 16) +
            sizeof(float) * 16 * (nt1 + nt2);
@@ -983,6 +1061,207 @@ static size_t narrow_split_lds(int kc0, int nt1, int nt2) {
 
 static size_t narrow_lds(int kg1, int nt1, int nt2) {
     return sizeof(f32x4) * ((size_t)nt1 * kg1 * 64 + (size_t)nt2 * nt1 * 64 + kg1 * 16) + sizeof(float) * 16 * (nt1 + nt2);
+}
+
+// ============================================================================ split-f16 token GEMMs
+// Per-point GEMMs of the encoder as token GEMMs: points are MFMA columns, outputs MFMA rows, both
+// operands staged through LDS per 32-deep chunk (weights: pack_h16_fragments planes; points: fp32 rows
+// split into hi/lo f16 on the way in at a per-point power-of-two scale from the point's max |x|), three
+// products per chunk with fp32 accumulation as the other split levels. Workgroup tile: 64*WO outputs x
+// 64*(8/WO) points, 8 waves as WO (outputs) x 8/WO (points) of 64 x 64; two LDS stages, one barrier per
+// chunk.
+//   MODE 0 (GroupAll layer 0, both branches in one launch): y = relu(W0 [f | xyz] + b) point-major, and
+//          per point and branch the max of y (atomicMax on the bits of a float >= 0) for layer 1's scale;
+//   MODE 1 (GroupAll layer 1): relu(W1 y + b), max over each object's 64 points (one wave's block), out;
+//   MODE 2 (levels 1-3, per-point layer-0 projection Q = W0 [f | xyz] + b, no activation): y.
+struct TokArgs {
+    const float* x0[2];    // per branch: first input block, row-major (M, ld0), k0 columns
+    int ld0, k0;
+    const float* x1;       // second input block (M, ld1), k1 columns (null when k1 = 0)
+    int ld1, k1;
+    int M, KC;             // points; 32-deep chunks of the padded input
+    const float* rmax[2];  // per branch: per-point max |x| over its input row
+    const float* w[2];     // per branch: split planes, bias (padded to 32), weight exponent
+    const float* bias[2];
+    int ew[2];
+    int nbpb;              // output blocks (64 * WO wide) per branch
+    float* y;              // MODE 0/2: (M, ldy), branch br's outputs from column ycol[br]
+    int ldy, ycol[2];
+    unsigned* ymax;        // MODE 0: [2][M] max of y per point and branch
+    float* out;            // MODE 1: (M / 64, ldo), branch br's outputs from column out_off[br]
+    int ldo, out_off[2];
+};
+constexpr int TG_THREADS = 512;
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+template <int WO>
+constexpr size_t tg_lds_bytes() {   // two stages of (4*WO weight + 4*(8/WO) point) tiles of 2 KiB + exponents
+    return 2 * (size_t)(4 * WO + 4 * (8 / WO)) * 2048 + sizeof(int) * 64 * (8 / WO);
+}
+
+// max |x| over each point's input row [x0 | x1] (a wave per point)
+__global__ __launch_bounds__(256) void tok_rowmax_kernel(const float* __restrict__ x0, int ld0, int k0,
+                                                         const float* __restrict__ x1, int ld1, int k1, int M,
+                                                         float* __restrict__ rmax) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= M) return;
+    float m = 0.f;
+    for (int k = lane; k < k0; k += 64) m = fmaxf(m, fabsf(x0[(size_t)r * ld0 + k]));
+    for (int k = lane; k < k1; k += 64) m = fmaxf(m, fabsf(x1[(size_t)r * ld1 + k]));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if (lane == 0) rmax[r] = m;
+}
+
+template <int MODE, int WO>
+__global__ __launch_bounds__(TG_THREADS) void tok_split_gemm_kernel(TokArgs a) {
+    constexpr int WT = 8 / WO, BM = 64 * WT;
+    constexpr int NA = 4 * WO * 128, NB = 4 * WT * 128;   // f16x8 fragments per stage
+    extern __shared__ __attribute__((aligned(16))) f16x8 tg_lds[];
+    auto sA = [&](int st) { return tg_lds + st * (NA + NB); };
+    auto sB = [&](int st) { return tg_lds + st * (NA + NB) + NA; };
+    int* eT = reinterpret_cast<int*>(tg_lds + 2 * (NA + NB));
+    const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, n = lane & 15;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int br = blockIdx.x / a.nbpb, nblk = blockIdx.x - br * a.nbpb;
+    const int m0 = blockIdx.y * BM, T0 = nblk * 4 * WO;
+    const f16x8* W = reinterpret_cast<const f16x8*>(a.w[br]);
+    const float* X0 = a.x0[br];
+    // staging roles: weight fragments tid + 512u (u < WO); point rows (tid + 512u) / 8 (u < WT), k-group g
+    const int g = tid & 7;
+    int row[WT];
+    float sc[WT];
+#pragma unroll
+    for (int u = 0; u < WT; ++u) {
+        const int r = (tid + 512 * u) >> 3;
+        row[u] = m0 + r;
+        const int E = col_exponent(row[u] < a.M ? a.rmax[br][row[u]] : 0.f);
+        sc[u] = exp2i(14 - E);
+        if (g == 0) eT[r] = E;
+    }
+    auto fetch_x = [&](int r, int col) -> f32x4 {
+        if (r >= a.M) return f32x4{0.f, 0.f, 0.f, 0.f};
+        if (col + 4 <= a.k0) return ld4(X0 + (size_t)r * a.ld0 + col);
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = col + j;
+            v[j] = k < a.k0 ? X0[(size_t)r * a.ld0 + k] : (k - a.k0 < a.k1 ? a.x1[(size_t)r * a.ld1 + k - a.k0] : 0.f);
+        }
+        return f32x4{v[0], v[1], v[2], v[3]};
+    };
+    auto load = [&](int c, f32x4 (&ra)[WO], f32x4 (&rb)[WT]) {
+#pragma unroll
+        for (int u = 0; u < WO; ++u) {
+            const int idx = tid + 512 * u;
+            ra[u] = ld4(reinterpret_cast<const float*>(W + ((size_t)(T0 + (idx >> 7)) * a.KC + c) * 128 + (idx & 127)));
+        }
+#pragma unroll
+        for (int u = 0; u < WT; ++u) rb[u] = fetch_x(row[u], 32 * c + 4 * g);
+    };
+    auto store = [&](int s, const f32x4 (&ra)[WO], const f32x4 (&rb)[WT]) {
+#pragma unroll
+        for (int u = 0; u < WO; ++u) sA(s)[tid + 512 * u] = __builtin_bit_cast(f16x8, ra[u]);
+#pragma unroll
+        for (int u = 0; u < WT; ++u) {
+#pragma clang fp contract(off)
+            const int r = (tid + 512 * u) >> 3, ln = 16 * (g & 3) + (r & 15), half = g >> 2;
+            f16x4 hi, lo;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float x = rb[u][j] * sc[u];
+                const _Float16 h = (_Float16)x;
+                hi[j] = h;
+                lo[j] = (_Float16)(x - (float)h);
+            }
+            reinterpret_cast<f16x4*>(&sB(s)[((r >> 4) * 2 + 0) * 64 + ln])[half] = hi;
+            reinterpret_cast<f16x4*>(&sB(s)[((r >> 4) * 2 + 1) * 64 + ln])[half] = lo;
+        }
+    };
+    const int wo = wid % WO, wt = wid / WO;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 ra[WO], rb[WT];
+    load(0, ra, rb);
+    store(0, ra, rb);
+    __syncthreads();
+    for (int c = 0; c < a.KC; ++c) {
+        const int s = c & 1;
+        if (c + 1 < a.KC) load(c + 1, ra, rb);
+        f16x8 bh[4], bl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bh[j] = sB(s)[((4 * wt + j) * 2 + 0) * 64 + lane];
+            bl[j] = sB(s)[((4 * wt + j) * 2 + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x8 ah = sA(s)[((4 * wo + i) * 2 + 0) * 64 + lane];
+            const f16x8 al = sA(s)[((4 * wo + i) * 2 + 1) * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(al, bh[j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(ah, bl[j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(ah, bh[j], acc[i][j]);
+        }
+        if (c + 1 < a.KC) store(s ^ 1, ra, rb);
+        __syncthreads();
+    }
+    // epilogue: unscale (exact powers of two), bias, ReLU (MODE 0/1)
+    const float* bias = a.bias[br];
+    if constexpr (MODE == 0 || MODE == 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int pc = (4 * wt + j) * 16 + n, r = m0 + pc;
+            const float u = exp2i(eT[pc] - 14 - a.ew[br]);
+            float cm = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int o = (T0 + 4 * wo + i) * 16 + 4 * q;
+                f32x4 v = acc[i][j] * u + ld4(bias + o);
+                if constexpr (MODE == 0) {
+                    v = relu4(v);
+                    cm = fmaxf(cm, max4(v));
+                }
+                if (r < a.M) st4(a.y + (size_t)r * a.ldy + a.ycol[br] + o, v);
+            }
+            if constexpr (MODE == 0) {
+                cm = rows_max(cm);
+                if (q == 0 && r < a.M) atomicMax(a.ymax + (size_t)br * a.M + r, __float_as_uint(cm));
+            }
+        }
+    } else {
+        f32x4 pm[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pm[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int pc = (4 * wt + j) * 16 + n;
+            const float u = exp2i(eT[pc] - 14 - a.ew[br]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const f32x4 v = relu4(acc[i][j] * u + ld4(bias + (T0 + 4 * wo + i) * 16 + 4 * q));
+                pm[i] = f32x4{fmaxf(pm[i].x, v.x), fmaxf(pm[i].y, v.y), fmaxf(pm[i].z, v.z), fmaxf(pm[i].w, v.w)};
+            }
+        }
+        const int obj = (m0 + 64 * wt) >> 6;   // the wave's 64 points are one object
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f32x4 v = pm[i];
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) {
+                v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
+                v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
+                v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
+                v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
+            }
+            if (n == 0 && obj * 64 < a.M)
+                st4(a.out + (size_t)obj * a.ldo + a.out_off[br] + (T0 + 4 * wo + i) * 16 + 4 * q, v);
+        }
+    }
 }
 
 // ============================================================================ host side
@@ -1119,6 +1398,111 @@ static EncCtx enc_ctx(const float* wbuf, const int64_t* layer_off, const float* 
     return c;
 }
 
+// Per-point layer-0 projection of level l (1-3) as a split-f16 token GEMM (MODE 2): Q = W0 [f | xyz] + b
+// for both branches into qbuf (B, n_prev, proj_stride). The per-point maxima go to level l-1's
+// projection buffer, free once level l-1 has run.
+static int run_proj_split(const EncCtx& c, int l, int c_prev, const float* feat_prev, const float* xyz_prev,
+                          int n_prev, float* qbuf, hipStream_t st) {
+    const int B = c.B, M = B * n_prev, w = kWidths[l][0][1];
+    GP_REQUIRE(w == kWidths[l][1][1] && (w == 64 || w == 128 || w == 256) && feat_prev && c_prev % 4 == 0,
+               "encoder: level %d projection of width %d has no split tile", l, w);
+    float* rmax = reinterpret_cast<float*>(c.ws + c.L.proj[l - 1]);
+    hipLaunchKernelGGL(tok_rowmax_kernel, dim3((M + 3) / 4), dim3(256), 0, st, feat_prev, c_prev, c_prev, xyz_prev, 3,
+                       3, M, rmax);
+    TokArgs a = {};
+    a.M = M;
+    a.nbpb = 1;
+    for (int br = 0; br < 2; ++br) {
+        const int64_t* o = enc_layer(c.tab, l, br, 0);
+        a.x0[br] = feat_prev;
+        a.rmax[br] = rmax;
+        a.w[br] = c.wbuf + o[2];
+        a.bias[br] = c.wbuf + o[1];
+        a.ew[br] = (int)o[3];
+        a.ycol[br] = br == 0 ? 0 : pad16(w);
+    }
+    a.ld0 = c_prev;
+    a.k0 = c_prev;
+    a.x1 = xyz_prev;
+    a.ld1 = 3;
+    a.k1 = 3;
+    a.KC = (c_prev + 3 + 31) / 32;
+    a.y = qbuf;
+    a.ldy = proj_stride(l);
+#define GP_PROJ(WO)                                                                                          \
+    hipLaunchKernelGGL((tok_split_gemm_kernel<2, WO>), dim3(2, (M + 64 * (8 / WO) - 1) / (64 * (8 / WO))), \
+                       dim3(TG_THREADS), tg_lds_bytes<WO>(), st, a)
+    if (w == 256) GP_PROJ(4);
+    else if (w == 128) GP_PROJ(2);
+    else GP_PROJ(1);
+#undef GP_PROJ
+    return gp_check_launch("tok_split_gemm_kernel (projection)");
+}
+
+// GroupAll as two split-f16 token GEMMs (tok_split_gemm_kernel) when the table carries both layers' planes.
+// Scratch: layer 0's output (B*64 x 1024) in level 3's projection buffer, the per-point maxima in level
+// 2's, both free once level 3 has run.
+static int run_groupall_split(const EncCtx& c, const float* feat_prev, float* out, hipStream_t st) {
+    const int B = c.B, P = kNpoint[3], M = B * P;
+    const int k_in = kCout[3];
+    GP_REQUIRE(P == 64 && kWidths[4][0][1] == 512 && kWidths[4][1][1] == 512 && kWidths[4][0][2] == 512 &&
+                   kWidths[4][1][2] == 512 && kWidths[4][0][0] == k_in + 3,
+               "encoder: GroupAll split path expects 64 points of %d + 3 channels", k_in);
+    float* y0 = reinterpret_cast<float*>(c.ws + c.L.proj[3]);
+    float* rmax0 = reinterpret_cast<float*>(c.ws + c.L.proj[2]);
+    unsigned* ymax = reinterpret_cast<unsigned*>(rmax0 + M);
+    GP_REQUIRE((size_t)kNpoint[2] * proj_stride(3) >= (size_t)P * 1024 && (size_t)kNpoint[1] * proj_stride(2) >= 3u * P,
+               "encoder: GroupAll scratch does not fit the projection buffers");
+    const float* xyz = c.nxyz[3];
+    hipLaunchKernelGGL(tok_rowmax_kernel, dim3((M + 3) / 4), dim3(256), 0, st, feat_prev, k_in, k_in, xyz, 3, 3, M,
+                       rmax0);
+    if (hipMemsetAsync(ymax, 0, sizeof(unsigned) * 2 * (size_t)M, st) != hipSuccess)
+        return gp_check_launch("groupall memset");
+    TokArgs a = {};
+    a.M = M;
+    a.nbpb = 2;
+    for (int br = 0; br < 2; ++br) {
+        const int64_t* o = enc_layer(c.tab, 4, br, 0);
+        a.x0[br] = feat_prev;
+        a.rmax[br] = rmax0;
+        a.w[br] = c.wbuf + o[2];
+        a.bias[br] = c.wbuf + o[1];
+        a.ew[br] = (int)o[3];
+    }
+    a.ld0 = k_in;
+    a.k0 = k_in;
+    a.x1 = xyz;
+    a.ld1 = 3;
+    a.k1 = 3;
+    a.KC = (k_in + 3 + 31) / 32;
+    a.y = y0;
+    a.ldy = 1024;
+    a.ycol[0] = 0;
+    a.ycol[1] = 512;
+    a.ymax = ymax;
+    const dim3 grid(4, (M + 127) / 128);
+    hipLaunchKernelGGL((tok_split_gemm_kernel<0, 4>), grid, dim3(TG_THREADS), tg_lds_bytes<4>(), st, a);
+    TokArgs b = {};
+    b.M = M;
+    b.nbpb = 2;
+    for (int br = 0; br < 2; ++br) {
+        const int64_t* o = enc_layer(c.tab, 4, br, 1);
+        b.x0[br] = y0 + 512 * br;
+        b.rmax[br] = reinterpret_cast<const float*>(ymax) + (size_t)br * M;
+        b.w[br] = c.wbuf + o[2];
+        b.bias[br] = c.wbuf + o[1];
+        b.ew[br] = (int)o[3];
+        b.out_off[br] = 512 * br;
+    }
+    b.ld0 = 1024;
+    b.k0 = 512;
+    b.KC = 16;
+    b.out = out;
+    b.ldo = kCout[4];
+    hipLaunchKernelGGL((tok_split_gemm_kernel<1, 4>), grid, dim3(TG_THREADS), tg_lds_bytes<4>(), st, b);
+    return gp_check_launch("tok_split_gemm_kernel");
+}
+
 // One SA level l (ball query, per-point layer 0, layers 1-2 + max-pool) over the FPS results already
 // in the workspace. feat_prev (B, n_prev, c_prev) point-major or null (c_prev = 0); out (B, M_l, C_l).
 // side: FPS levels that ride along as extra workgroups of the narrow launches (gp_encoder_forward),
@@ -1168,9 +1552,14 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             pa.tag = 16 + l * 2 + br;
             q_off += pad16(kWidths[l][br][1]);
         }
-        rc = launch_pair<4>(pp[0], pp[1], B, st);
+        const bool split0 = l >= 1 && enc_layer(layer_off, l, 0, 0)[2] >= 0 && enc_layer(layer_off, l, 1, 0)[2] >= 0;
+        rc = split0 ? run_proj_split(c, l, c_prev, feat_prev, xyz_prev, n_prev, qbuf, st)
+                    : launch_pair<4>(pp[0], pp[1], B, st);
         if (rc) return rc;
     }
+    if (l == 4 && enc_layer(layer_off, 4, 0, 0)[2] >= 0 && enc_layer(layer_off, 4, 0, 1)[2] >= 0 &&
+        enc_layer(layer_off, 4, 1, 0)[2] >= 0 && enc_layer(layer_off, 4, 1, 1)[2] >= 0)
+        return run_groupall_split(c, feat_prev, out, st);
     if (l == 4) {  // group-all pools with atomicMax when a centroid spans workgroups
         if (hipMemsetAsync(out, 0, sizeof(float) * B * kCout[4], st) != hipSuccess)
             return gp_check_launch("encoder memset");
@@ -1228,7 +1617,11 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             }
         }
         const dim3 grid(std::max(512, B), 3);
-        if (l == 0) {
+        if (l == 0 && na[1].w1h && na[1].w2h) {
+            const size_t lds = std::max({narrow_lds(1, 1, 2), narrow_split_lds(1, 2, 4), fps_side_lds(fs)});
+            hipLaunchKernelGGL((sa_narrow_mixed_kernel<1, 1, 2, 1, 1, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st,
+                               na[0], na[1], fs);
+        } else if (l == 0) {
             const size_t lds = std::max({narrow_lds(1, 1, 2), narrow_lds(2, 2, 4), fps_side_lds(fs)});
             hipLaunchKernelGGL((sa_narrow_kernel<1, 1, 2, 1, 2, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st, na[0],
                                na[1], fs);
@@ -1246,7 +1639,7 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
     // levels 2-3: split-f16 kernel when the table carries the planes (pack.pack_encoder)
     if ((l == 2 || l == 3) && enc_layer(layer_off, l, 0, 1)[2] >= 0 && enc_layer(layer_off, l, 0, 2)[2] >= 0 &&
         enc_layer(layer_off, l, 1, 1)[2] >= 0 && enc_layer(layer_off, l, 1, 2)[2] >= 0) {
-        constexpr int CT = 4;
+        const int CT = l == 2 ? SPLIT_CT2 : SPLIT_CT3;
         SplitArgs sp[2];
         int off_out = 0;
         for (int br = 0; br < 2; ++br) {
@@ -1276,16 +1669,18 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             a.out_off = off_out;
             a.tag = l * 2 + br;
             off_out += kWidths[l][br][3];
-            GP_REQUIRE(a.cols % (16 * CT) == 0 && (16 * CT) % a.ns == 0,
-                       "encoder: level %d columns %d do not tile by %d", l, a.cols, 16 * CT);
+            GP_REQUIRE((16 * CT) % a.ns == 0, "encoder: level %d centroids of %d columns straddle %d-column tiles",
+                       l, a.ns, 16 * CT);
         }
-        const dim3 grid(std::max(sp[0].cols, sp[1].cols) / (16 * CT), B, 2), blk(SPLIT_WV * 64);
+        const int cmax = std::max(sp[0].cols, sp[1].cols);
+        const dim3 grid((cmax + 16 * CT - 1) / (16 * CT), B, 2), blk(SPLIT_WV * 64);
         if (l == 2) {
-            const size_t lds = sa_split_lds<CT, 4, 7>();
-            hipLaunchKernelGGL((sa_split_kernel<CT, 4, 7, 8, 7, 8>), grid, blk, lds, st, sp[0], sp[1]);
+            const size_t lds = sa_split_lds<SPLIT_CT2, 4, 7>();
+            hipLaunchKernelGGL((sa_split_kernel<SPLIT_CT2, SPLIT_D2, 4, 7, 8, 7, 8>), grid, blk, lds, st, sp[0], sp[1]);
         } else {
-            const size_t lds = std::max(sa_split_lds<CT, 8, 8>(), sa_split_lds<CT, 8, 12>());
-            hipLaunchKernelGGL((sa_split_kernel<CT, 8, 8, 16, 12, 16>), grid, blk, lds, st, sp[0], sp[1]);
+            const size_t lds = std::max(sa_split_lds<SPLIT_CT3, 8, 8>(), sa_split_lds<SPLIT_CT3, 8, 12>());
+            hipLaunchKernelGGL((sa_split_kernel<SPLIT_CT3, SPLIT_D3, 8, 8, 16, 12, 16>), grid, blk, lds, st, sp[0],
+                               sp[1]);
         }
         return gp_check_launch("sa_split_kernel");
     }

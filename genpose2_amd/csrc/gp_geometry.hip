@@ -159,65 +159,87 @@ int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const i
 }
 
 // ============================================================================ ball query
-// One wave per centroid, NR radii (1 or 2) answered by the same scan.
-template <int NR>
+// One wave per centroid, NR radii (1 or 2) answered by the same scan, 4 * BQ_CPW centroids of one
+// object per workgroup. LDSP: the object's points are staged in LDS once per workgroup as (x, y, z, 0)
+// (one ds_read_b128 per lane per 64-point ballot instead of three strided global loads); used while
+// they fit (n <= BQ_LDS_MAX).
+constexpr int BQ_CPW = 8;
+constexpr int BQ_LDS_MAX = 4096;
+template <int NR, bool LDSP>
 __global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const float* __restrict__ new_xyz,
                                                          const float* __restrict__ xyz, float r2a,
                                                          float r2b, int nsa, int nsb,
                                                          int* __restrict__ idxa,
                                                          int* __restrict__ idxb) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 sp[];
     const int lane = threadIdx.x & 63;
-    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int b = blockIdx.y;
-    if (p >= m) return;  // wave-uniform
-    const float* c = new_xyz + ((size_t)b * m + p) * 3;
-    const float cx = c[0], cy = c[1], cz = c[2];
     const float* pts = xyz + (size_t)b * n * 3;
-    int* oa = idxa + ((size_t)b * m + p) * nsa;
-    int* ob = NR > 1 ? idxb + ((size_t)b * m + p) * nsb : nullptr;
-    int cnta = 0, cntb = 0, firsta = -1, firstb = -1;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    for (int base = 0; base < n; base += 64) {
-        const int k = base + lane;
-        float d2 = 3.0e38f;
-        if (k < n) d2 = dist2_ref(cx, cy, cz, pts[3 * k + 0], pts[3 * k + 1], pts[3 * k + 2]);
-        const bool ha = (k < n) && d2 < r2a;
-        const unsigned long long ma = __ballot(ha);
-        if (cnta < nsa && ma) {
-            const int rank = cnta + __popcll(ma & lt);
-            if (ha && rank < nsa) oa[rank] = k;
-            if (firsta < 0) firsta = base + __ffsll((long long)ma) - 1;
-            cnta += __popcll(ma);
-        }
-        if (NR > 1) {
-            const bool hb = (k < n) && d2 < r2b;
-            const unsigned long long mb = __ballot(hb);
-            if (cntb < nsb && mb) {
-                const int rank = cntb + __popcll(mb & lt);
-                if (hb && rank < nsb) ob[rank] = k;
-                if (firstb < 0) firstb = base + __ffsll((long long)mb) - 1;
-                cntb += __popcll(mb);
-            }
-        }
-        if (cnta >= nsa && (NR == 1 || cntb >= nsb)) break;
+    if constexpr (LDSP) {
+        for (int i = threadIdx.x; i < n; i += 256) sp[i] = f32x4{pts[3 * i + 0], pts[3 * i + 1], pts[3 * i + 2], 0.f};
+        __syncthreads();
     }
-    // pad with the first hit (ball_query_gpu.cu:35-40); no hit -> 0 (zero-initialised output)
-    for (int s = (cnta < nsa ? cnta : nsa) + lane; s < nsa; s += 64) oa[s] = firsta < 0 ? 0 : firsta;
-    if (NR > 1)
-        for (int s = (cntb < nsb ? cntb : nsb) + lane; s < nsb; s += 64) ob[s] = firstb < 0 ? 0 : firstb;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int pend = min(m, (int)(blockIdx.x + 1) * 4 * BQ_CPW);
+    for (int p = blockIdx.x * 4 * BQ_CPW + (threadIdx.x >> 6); p < pend; p += 4) {   // wave-uniform
+        const float* c = new_xyz + ((size_t)b * m + p) * 3;
+        const float cx = c[0], cy = c[1], cz = c[2];
+        int* oa = idxa + ((size_t)b * m + p) * nsa;
+        int* ob = NR > 1 ? idxb + ((size_t)b * m + p) * nsb : nullptr;
+        int cnta = 0, cntb = 0, firsta = -1, firstb = -1;
+        for (int base = 0; base < n; base += 64) {
+            const int k = base + lane;
+            float d2 = 3.0e38f;
+            if (k < n) {
+                if constexpr (LDSP) {
+                    const f32x4 v = sp[k];
+                    d2 = dist2_ref(cx, cy, cz, v.x, v.y, v.z);
+                } else {
+                    d2 = dist2_ref(cx, cy, cz, pts[3 * k + 0], pts[3 * k + 1], pts[3 * k + 2]);
+                }
+            }
+            const bool ha = (k < n) && d2 < r2a;
+            const unsigned long long ma = __ballot(ha);
+            if (cnta < nsa && ma) {
+                const int rank = cnta + __popcll(ma & lt);
+                if (ha && rank < nsa) oa[rank] = k;
+                if (firsta < 0) firsta = base + __ffsll((long long)ma) - 1;
+                cnta += __popcll(ma);
+            }
+            if (NR > 1) {
+                const bool hb = (k < n) && d2 < r2b;
+                const unsigned long long mb = __ballot(hb);
+                if (cntb < nsb && mb) {
+                    const int rank = cntb + __popcll(mb & lt);
+                    if (hb && rank < nsb) ob[rank] = k;
+                    if (firstb < 0) firstb = base + __ffsll((long long)mb) - 1;
+                    cntb += __popcll(mb);
+                }
+            }
+            if (cnta >= nsa && (NR == 1 || cntb >= nsb)) break;
+        }
+        // pad with the first hit (ball_query_gpu.cu:35-40); no hit -> 0 (zero-initialised output)
+        for (int s = (cnta < nsa ? cnta : nsa) + lane; s < nsa; s += 64) oa[s] = firsta < 0 ? 0 : firsta;
+        if (NR > 1)
+            for (int s = (cntb < nsb ? cntb : nsb) + lane; s < nsb; s += 64) ob[s] = firstb < 0 ? 0 : firstb;
+    }
 }
 
 int gp_launch_ball_query2(int b, int n, int m, float ra, float rb, int nsa, int nsb,
                           const float* new_xyz, const float* xyz, int* idxa, int* idxb,
                           hipStream_t st) {
     const float r2a = ra * ra, r2b = rb * rb;  // radius2 = radius * radius in fp32
-    dim3 grid((m + 3) / 4, b);
-    if (idxb)
-        hipLaunchKernelGGL(ball_query_kernel<2>, grid, dim3(256), 0, st, n, m, new_xyz, xyz, r2a, r2b,
-                           nsa, nsb, idxa, idxb);
-    else
-        hipLaunchKernelGGL(ball_query_kernel<1>, grid, dim3(256), 0, st, n, m, new_xyz, xyz, r2a, 0.f,
-                           nsa, 0, idxa, nullptr);
+    dim3 grid((m + 4 * BQ_CPW - 1) / (4 * BQ_CPW), b);
+    const bool lds = n <= BQ_LDS_MAX;
+    const size_t bytes = lds ? sizeof(f32x4) * (size_t)n : 0;
+#define GP_BQ(NR, L) hipLaunchKernelGGL((ball_query_kernel<NR, L>), grid, dim3(256), bytes, st, n, m, new_xyz, xyz, \
+                                        r2a, NR > 1 ? r2b : 0.f, nsa, NR > 1 ? nsb : 0, idxa, NR > 1 ? idxb : nullptr)
+    if (idxb) {
+        if (lds) GP_BQ(2, true); else GP_BQ(2, false);
+    } else {
+        if (lds) GP_BQ(1, true); else GP_BQ(1, false);
+    }
+#undef GP_BQ
     return gp_check_launch("ball_query_kernel");
 }
 

@@ -319,7 +319,21 @@ __device__ __forceinline__ void stream_hk_step(__amdgpu_buffer_rsrc_t W, const i
                         __builtin_bit_cast(f16x8, ldbuf4(W, voff, ((T[t] * KC + G) * 2 + p) * 1024));
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (G >= D) {
+        if constexpr (G >= D && NT > 4) {
+            // wide column blocks (encoder levels 2-3): one column tile's planes live at a time
+            constexpr int GG = G - D, S = GG % (D + 1);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) {
+                const f16x8 bh = B[((GG * NT + ct) * 2 + 0) * 64 + lane];
+                const f16x8 bl = B[((GG * NT + ct) * 2 + 1) * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t][ct] = mfma_h(ring[S][t][1], bh, acc[t][ct]);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t][ct] = mfma_h(ring[S][t][0], bl, acc[t][ct]);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t][ct] = mfma_h(ring[S][t][0], bh, acc[t][ct]);
+            }
+        } else if constexpr (G >= D) {
             constexpr int GG = G - D, S = GG % (D + 1);
             f16x8 bh[NT], bl[NT];
 #pragma unroll

@@ -8,7 +8,8 @@
 // model_state_dict keys.
 //   * SA layers: Conv2d 1x1 + BatchNorm2d(eval) folded in float64, rounded once (pytorch_utils.py:58-106);
 //     MFMA A-fragment order; layer 0's input channels permuted to [feats | xyz | pad] (pack.pack_encoder);
-//     split-f16 hi/lo planes for levels 1-3 layers 1-2 (pack.pack_h16_fragments, per-layer exponent).
+//     split-f16 hi/lo planes for every layer of levels 1-4 and layers 1-2 of level 0 (pack.pack_h16_fragments,
+//     per-layer exponent).
 //   * heads: first head layer split into its [pts 1024 | t 128 | pose 256] column blocks (scorenet.py:249),
 //     fragments / transposes / split planes / activation bounds as pack.pack_heads.
 //   * ScaleNet: plain copies.
@@ -197,11 +198,17 @@ bool pack_encoder(StateDict& sd, Packer& P, int64_t* table) {
                 std::vector<float> bp(pad_to(n_out, 32), 0.f);
                 std::copy(b.begin(), b.end(), bp.begin());
                 row[1] = (int64_t)(P.add(bp) - base);
-                if (lv >= 1 && lv <= 3 && i >= 1) {   // pack.ENC_SPLIT_LEVELS
+                if (lv >= 1 || i >= 1) {   // pack.enc_split_layer
                     const int np = pad_to(n_out, 32), kp = pad_to(k_in, 32);
                     std::vector<float> wq((size_t)np * kp, 0.f);
-                    for (int o = 0; o < n_out; ++o)
-                        for (int c = 0; c < k_in; ++c) wq[(size_t)o * kp + c] = W[(size_t)o * k_in + c];
+                    for (int o = 0; o < n_out; ++o) {
+                        if (i == 0) {   // layer 0: [feats | xyz | 0]
+                            for (int c = 0; c < c_prev; ++c) wq[(size_t)o * kp + c] = W[(size_t)o * k_in + 3 + c];
+                            for (int c = 0; c < 3; ++c) wq[(size_t)o * kp + c_prev + c] = W[(size_t)o * k_in + c];
+                        } else {
+                            for (int c = 0; c < k_in; ++c) wq[(size_t)o * kp + c] = W[(size_t)o * k_in + c];
+                        }
+                    }
                     const int e = split_exponent(W);
                     row[2] = (int64_t)(P.add_bits(pack_h16(wq, np, kp, e)) - base);
                     row[3] = e;

@@ -53,8 +53,9 @@ class EncoderModel:
         self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
 
     def set_arith(self, arith: str) -> None:
-        """GEMM arithmetic of SA levels 2-3: "split_f16" (f16 hi/lo MFMA products with per-column
-        activation scaling, sa_split_kernel) or "f32" (exact fp32 MFMA)."""
+        """GEMM arithmetic of SA levels 1-3 and GroupAll: "split_f16" (f16 hi/lo MFMA products with
+        per-column activation scaling: sa_narrow_split_kernel, sa_split_kernel, tok_split_gemm_kernel)
+        or "f32" (exact fp32 MFMA)."""
         if arith not in ("split_f16", "f32"):
             raise ValueError(f"unknown encoder arithmetic {arith!r} (split_f16 | f32)")
         t = self._table.copy()

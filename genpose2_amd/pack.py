@@ -46,8 +46,15 @@ def pad_vec(b: np.ndarray, n: int) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- encoder
-ENC_SPLIT_LEVELS = (1, 2, 3)   # levels whose layers 1-2 also get split-f16 planes (level 1: sa_narrow_split_kernel,
-                               # levels 2-3: sa_split_kernel)
+ENC_SPLIT_LEVELS = (1, 2, 3, 4)   # levels whose every layer also gets split-f16 planes: layer 0 of levels 1-3 and
+                                  # both GroupAll layers run as token GEMMs (tok_split_gemm_kernel), layers 1-2 of
+                                  # level 1 in sa_narrow_split_kernel, of levels 2-3 in sa_split_kernel; level 0
+                                  # has planes for layers 1-2 (its 32-wide branch in sa_narrow_mixed_kernel)
+
+
+def enc_split_layer(lv: int, i: int) -> bool:
+    """Whether layer i of level lv carries split-f16 planes."""
+    return lv in ENC_SPLIT_LEVELS or i >= 1
 
 
 def pad32(v: int) -> int:
@@ -57,7 +64,9 @@ def pad32(v: int) -> int:
 def pack_encoder(sd: weights.StateDict, levels=None) -> Tuple[np.ndarray, np.ndarray]:
     """All SA layers, BN folded, into one flat float32 buffer + int64 table [5][2][3][4]:
     [0] offset of the fp32 A fragments, [1] offset of the bias (padded to 32), [2] offset of the
-    split-f16 planes (levels 2-3, layers 1-2; -1 elsewhere), [3] their power-of-two exponent.
+    split-f16 planes (enc_split_layer: every layer of levels 1-4 and layers 1-2 of level 0; -1 for
+    level 0's layer 0),
+    [3] their power-of-two exponent.
 
     Layer 0 of each branch has its input channels permuted from the reference's
     [xyz(3) | feats(C)] (pointnet2_utils.py:287-289) to [feats(C) | xyz(3) | 0...] with
@@ -98,9 +107,14 @@ def pack_encoder(sd: weights.StateDict, levels=None) -> Tuple[np.ndarray, np.nda
                     packed = pack_a_fragments(W)
                 offsets[lv, br.branch, i, 0] = add(packed)
                 offsets[lv, br.branch, i, 1] = add(pad_vec(b, pad32(W.shape[0])))
-                if lv in ENC_SPLIT_LEVELS and i >= 1:
-                    wq = np.zeros((pad32(W.shape[0]), pad32(W.shape[1])), np.float32)
-                    wq[:W.shape[0], :W.shape[1]] = W
+                if enc_split_layer(lv, i):
+                    if i == 0:   # layer 0: the [feats | xyz | 0...] order of the fp32 fragments
+                        wq = np.zeros((pad32(W.shape[0]), pad32(c_prev + 3)), np.float32)
+                        wq[:W.shape[0], :c_prev] = W[:, 3:]
+                        wq[:W.shape[0], c_prev:c_prev + 3] = W[:, :3]
+                    else:
+                        wq = np.zeros((pad32(W.shape[0]), pad32(W.shape[1])), np.float32)
+                        wq[:W.shape[0], :W.shape[1]] = W
                     e = split_exponent(W)
                     offsets[lv, br.branch, i, 2] = add(pack_h16_fragments(wq, e))
                     offsets[lv, br.branch, i, 3] = e

@@ -87,12 +87,14 @@ def test_encoder_packing_covers_every_layer(score_sd):
             n = len(br.widths) - 1
             assert (off[lv, br.branch, :n, :2] >= 0).all() and (off[lv, br.branch, n:] == -1).all()
             assert (off[lv, br.branch, :n, :2] % 4 == 0).all()    # 16-byte aligned
-            for i in range(n):   # split-f16 planes: levels 2-3, layers 1-2
-                has = lv in pack.ENC_SPLIT_LEVELS and i >= 1
-                assert (off[lv, br.branch, i, 2] >= 0) == has
+            for i in range(n):   # split-f16 planes: every layer of levels 1-4, layers 1-2 of level 0
+                has = lv >= 1 or i >= 1
+                assert (off[lv, br.branch, i, 2] >= 0) == has == pack.enc_split_layer(lv, i)
                 if has:
                     assert off[lv, br.branch, i, 2] % 4 == 0
                     W, _ = weights.encoder_layers(score_sd)[lv][br.branch][i]
+                    if i == 0:   # layer-0 inputs permuted to [feats | xyz]
+                        W = np.concatenate([W[:, 3:], W[:, :3]], 1)
                     e = int(off[lv, br.branch, i, 3])
                     n_pad, k_pad = pack.pad32(W.shape[0]), pack.pad32(W.shape[1])
                     words = buf[off[lv, br.branch, i, 2]:][: n_pad * k_pad].view(np.int32)
