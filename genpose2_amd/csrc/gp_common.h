@@ -115,6 +115,20 @@ __device__ __forceinline__ float row16_sum(float v) {
     return dpp_add<0x140>(v);   // row_mirror
 }
 __device__ __forceinline__ float wave_sum(float v) { return rows_sum(row16_sum(v)); }
+// max over the 16 lanes of each row, DPP only (no ds_bpermute round trip through LDS)
+template <int CTRL>
+__device__ __forceinline__ float dpp_max(float v) {
+    return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false)));
+}
+__device__ __forceinline__ float row16_max(float v) {
+    v = dpp_max<0xB1>(v);
+    v = dpp_max<0x4E>(v);
+    v = dpp_max<0x141>(v);
+    return dpp_max<0x140>(v);
+}
+__device__ __forceinline__ f32x4 row16_max4(f32x4 v) {
+    return f32x4{row16_max(v.x), row16_max(v.y), row16_max(v.z), row16_max(v.w)};
+}
 // value of lane 4*(l/4) (first lane of the quad)
 __device__ __forceinline__ float quad_bcast0(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x00, 0xF, 0xF, false));

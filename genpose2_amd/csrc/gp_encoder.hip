@@ -219,13 +219,7 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
                         const f32x4 w2 = relu4(acc[t][cb + u] + bias);
                         v = f32x4{fmaxf(v.x, w2.x), fmaxf(v.y, w2.y), fmaxf(v.z, w2.z), fmaxf(v.w, w2.w)};
                     }
-#pragma unroll
-                    for (int off = 8; off >= 1; off >>= 1) {
-                        v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
-                        v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
-                        v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
-                        v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
-                    }
+                    v = row16_max4(v);
                     const int colc = col0 + (cbase + cb) * 16;
                     if (nn == 0 && colc < a.cols) {
                         const int m = colc / a.ns;
@@ -596,13 +590,7 @@ __device__ __forceinline__ void split_layer2(const SplitArgs& a, const f16x8* X,
                               fmaxf(v[ct].w, v[ct + 1].w)};
             }
             f32x4 r = v[ct];
-#pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) {
-                r.x = fmaxf(r.x, __shfl_xor(r.x, off, 64));
-                r.y = fmaxf(r.y, __shfl_xor(r.y, off, 64));
-                r.z = fmaxf(r.z, __shfl_xor(r.z, off, 64));
-                r.w = fmaxf(r.w, __shfl_xor(r.w, off, 64));
-            }
+            r = row16_max4(r);
             const int mi = (col0 + ct * 16) / a.ns;
             if (n == 0 && mi < a.m) {
                 st4(a.out + ((size_t)b * a.m + mi) * a.c_out_total + a.out_off + 16 * T[t] + 4 * q, r);
@@ -717,6 +705,24 @@ __device__ __forceinline__ void narrow_nbr(const NarrowArgs& a, int task, int nn
     for (int ct = 0; ct < SPAN; ++ct) p[ct] = a.nbr[(size_t)task * a.ns + ct * 16 + nn];
 }
 
+// W0_xyz . x_c for the lane's layer-0 channels 16g + 4q + j: the same for every column of a centroid
+template <int KG>
+__device__ __forceinline__ const f32x4* narrow_centroid_term(const f32x4* sW0x, int q, float cx, float cy, float cz,
+                                                             f32x4 (&cw)[KG]) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+        float r[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f32x4 wx = sW0x[16 * g + 4 * q + j];
+            r[j] = (wx.x * cx + wx.y * cy) + wx.z * cz;
+        }
+        cw[g] = f32x4{r[0], r[1], r[2], r[3]};
+    }
+    return cw;
+}
+
 template <int SPAN, int KG>
 __device__ __forceinline__ void narrow_fetch(const NarrowArgs& a, int task, const int (&p)[SPAN], int q,
                                              NarrowGather<SPAN, KG>& g) {
@@ -757,6 +763,7 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
     if (task >= total) return;
     int pn[SPAN];
     NarrowGather<SPAN, KG1> cur, nxt;
+    f32x4 cwv[KG1];
     narrow_nbr<SPAN>(a, task, nn, pn);
     narrow_fetch<SPAN, KG1>(a, task, pn, q, cur);
     if (task + nw < total) narrow_nbr<SPAN>(a, task + nw, nn, pn);
@@ -769,18 +776,15 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
         f32x4 rmax[NT2];
 #pragma unroll
         for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{0.f, 0.f, 0.f, 0.f};   // max of ReLU outputs
+        const f32x4* cw = narrow_centroid_term<KG1>(sW0x, q, cx, cy, cz, cwv);
 #pragma unroll
         for (int ct = 0; ct < SPAN; ++ct) {
             f32x4 bf[KG1];
 #pragma unroll
             for (int g = 0; g < KG1; ++g) {
-#pragma clang fp contract(off)
                 float r[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const f32x4 wx = sW0x[16 * g + 4 * q + j];
-                    r[j] = fmaxf(cur.q[ct][g][j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
-                }
+                for (int j = 0; j < 4; ++j) r[j] = fmaxf(fsub(cur.q[ct][g][j], cw[g][j]), 0.f);
                 bf[g] = f32x4{r[0], r[1], r[2], r[3]};
             }
             f32x4 acc1[NT1];
@@ -825,13 +829,7 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
 #pragma unroll
         for (int t = 0; t < NT2; ++t) {
             f32x4 v = rmax[t];
-#pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) {
-                v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
-                v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
-                v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
-                v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
-            }
+            v = row16_max4(v);
             if (nn == 0) st4(o + 16 * t, v);
         }
         cur = nxt;
@@ -869,6 +867,7 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
     if (task >= total) return;
     int pn[SPAN];
     NarrowGather<SPAN, KG1> cur, nxt;
+    f32x4 cwv[KG1];
     narrow_nbr<SPAN>(a, task, nn, pn);
     narrow_fetch<SPAN, KG1>(a, task, pn, q, cur);
     if (task + nw < total) narrow_nbr<SPAN>(a, task + nw, nn, pn);
@@ -881,18 +880,17 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
         f32x4 rmax[NT2];
 #pragma unroll
         for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4* cw = narrow_centroid_term<KG1>(sW0x, q, cx, cy, cz, cwv);
 #pragma unroll
         for (int ct = 0; ct < SPAN; ++ct) {
             f32x4 bf[KG1];
             float mx = 0.f;
 #pragma unroll
             for (int g = 0; g < KG1; ++g) {
-#pragma clang fp contract(off)
                 float r[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const f32x4 wx = sW0x[16 * g + 4 * q + j];
-                    r[j] = fmaxf(cur.q[ct][g][j] - ((wx.x * cx + wx.y * cy) + wx.z * cz), 0.f);
+                    r[j] = fmaxf(fsub(cur.q[ct][g][j], cw[g][j]), 0.f);
                     mx = fmaxf(mx, r[j]);
                 }
                 bf[g] = f32x4{r[0], r[1], r[2], r[3]};
@@ -954,13 +952,7 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
 #pragma unroll
         for (int t = 0; t < NT2; ++t) {
             f32x4 v = rmax[t];
-#pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) {
-                v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
-                v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
-                v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
-                v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
-            }
+            v = row16_max4(v);
             if (nn == 0) st4(o + 16 * t, v);
         }
         cur = nxt;
@@ -1251,13 +1243,7 @@ __global__ __launch_bounds__(TG_THREADS) void tok_split_gemm_kernel(TokArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             f32x4 v = pm[i];
-#pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) {
-                v.x = fmaxf(v.x, __shfl_xor(v.x, off, 64));
-                v.y = fmaxf(v.y, __shfl_xor(v.y, off, 64));
-                v.z = fmaxf(v.z, __shfl_xor(v.z, off, 64));
-                v.w = fmaxf(v.w, __shfl_xor(v.w, off, 64));
-            }
+            v = row16_max4(v);
             if (n == 0 && obj * 64 < a.M)
                 st4(a.out + (size_t)obj * a.ldo + a.out_off[br] + (T0 + 4 * wo + i) * 16 + 4 * q, v);
         }
