@@ -118,7 +118,8 @@ __device__ __forceinline__ float wave_sum(float v) { return rows_sum(row16_sum(v
 // max over the 16 lanes of each row, DPP only (no ds_bpermute round trip through LDS)
 template <int CTRL>
 __device__ __forceinline__ float dpp_max(float v) {
-    return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false)));
+    // every source lane of these patterns exists, so bound_ctrl never applies; it lets the DPP fold into v_max
+    return fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true)));
 }
 __device__ __forceinline__ float row16_max(float v) {
     v = dpp_max<0xB1>(v);

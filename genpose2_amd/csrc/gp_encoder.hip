@@ -405,6 +405,13 @@ struct SplitArgs {
 };
 
 __device__ __forceinline__ float max4(f32x4 v) { return fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)); }
+__device__ __forceinline__ f32x4 vmax4(f32x4 a, f32x4 b) {
+    return f32x4{fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)};
+}
+// Max-pooling before the bias and ReLU: x -> relu(x + b) is monotonic and rounding is monotonic, so
+// relu(max_n x_n + b) equals max_n relu(x_n + b) bit for bit -- the pools take the max of the unscaled
+// accumulators (scales are exact powers of two) and add the bias once per pooled output.
+constexpr float NEG_BIG = -3.0e38f;
 
 // Column exponent: E with the column maximum in [2^E, 2^(E+1)); all-zero columns get E = -100.
 __device__ __forceinline__ int col_exponent(float m) { return m > 1e-30f ? ilog2f(m) : -100; }
@@ -586,11 +593,9 @@ __device__ __forceinline__ void split_layer2(const SplitArgs& a, const f16x8* X,
         for (int ct = 0; ct < CT; ++ct) {
             if (span == 2) {
                 if (ct & 1) continue;
-                v[ct] = f32x4{fmaxf(v[ct].x, v[ct + 1].x), fmaxf(v[ct].y, v[ct + 1].y), fmaxf(v[ct].z, v[ct + 1].z),
-                              fmaxf(v[ct].w, v[ct + 1].w)};
+                v[ct] = vmax4(v[ct], v[ct + 1]);
             }
-            f32x4 r = v[ct];
-            r = row16_max4(r);
+            const f32x4 r = row16_max4(v[ct]);
             const int mi = (col0 + ct * 16) / a.ns;
             if (n == 0 && mi < a.m) {
                 st4(a.out + ((size_t)b * a.m + mi) * a.c_out_total + a.out_off + 16 * T[t] + 4 * q, r);
@@ -775,7 +780,7 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
         const float cx = cur.cx, cy = cur.cy, cz = cur.cz;
         f32x4 rmax[NT2];
 #pragma unroll
-        for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{0.f, 0.f, 0.f, 0.f};   // max of ReLU outputs
+        for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};   // pre-bias maxima
         const f32x4* cw = narrow_centroid_term<KG1>(sW0x, q, cx, cy, cz, cwv);
 #pragma unroll
         for (int ct = 0; ct < SPAN; ++ct) {
@@ -818,18 +823,13 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
-            for (int t = 0; t < NT2; ++t) {
-                const f32x4 v = relu4(acc2[t] + ld4(&sB2[16 * t + 4 * q]));
-                rmax[t] = f32x4{fmaxf(rmax[t].x, v.x), fmaxf(rmax[t].y, v.y), fmaxf(rmax[t].z, v.z),
-                                fmaxf(rmax[t].w, v.w)};
-            }
+            for (int t = 0; t < NT2; ++t) rmax[t] = vmax4(rmax[t], acc2[t]);
             __builtin_amdgcn_sched_barrier(0);
         }
         float* o = a.out + (size_t)task * a.c_out_total + a.out_off + 4 * q;
 #pragma unroll
         for (int t = 0; t < NT2; ++t) {
-            f32x4 v = rmax[t];
-            v = row16_max4(v);
+            const f32x4 v = relu4(row16_max4(rmax[t]) + ld4(&sB2[16 * t + 4 * q]));
             if (nn == 0) st4(o + 16 * t, v);
         }
         cur = nxt;
@@ -879,7 +879,7 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
         const float cx = cur.cx, cy = cur.cy, cz = cur.cz;
         f32x4 rmax[NT2];
 #pragma unroll
-        for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < NT2; ++t) rmax[t] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};   // pre-bias maxima
         const f32x4* cw = narrow_centroid_term<KG1>(sW0x, q, cx, cy, cz, cwv);
 #pragma unroll
         for (int ct = 0; ct < SPAN; ++ct) {
@@ -941,18 +941,13 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
             }
             const float u1 = exp2i(E1 - 14 - a.ew2);
 #pragma unroll
-            for (int t = 0; t < NT2; ++t) {
-                const f32x4 v = relu4(acc2[t] * u1 + ld4(&sB2[16 * t + 4 * q]));
-                rmax[t] = f32x4{fmaxf(rmax[t].x, v.x), fmaxf(rmax[t].y, v.y), fmaxf(rmax[t].z, v.z),
-                                fmaxf(rmax[t].w, v.w)};
-            }
+            for (int t = 0; t < NT2; ++t) rmax[t] = vmax4(rmax[t], acc2[t] * u1);
             __builtin_amdgcn_sched_barrier(0);
         }
         float* o = a.out + (size_t)task * a.c_out_total + a.out_off + 4 * q;
 #pragma unroll
         for (int t = 0; t < NT2; ++t) {
-            f32x4 v = rmax[t];
-            v = row16_max4(v);
+            const f32x4 v = relu4(row16_max4(rmax[t]) + ld4(&sB2[16 * t + 4 * q]));
             if (nn == 0) st4(o + 16 * t, v);
         }
         cur = nxt;
@@ -1228,22 +1223,18 @@ __global__ __launch_bounds__(TG_THREADS) void tok_split_gemm_kernel(TokArgs a) {
     } else {
         f32x4 pm[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pm[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 4; ++i) pm[i] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};   // pre-bias maxima
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int pc = (4 * wt + j) * 16 + n;
             const float u = exp2i(eT[pc] - 14 - a.ew[br]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const f32x4 v = relu4(acc[i][j] * u + ld4(bias + (T0 + 4 * wo + i) * 16 + 4 * q));
-                pm[i] = f32x4{fmaxf(pm[i].x, v.x), fmaxf(pm[i].y, v.y), fmaxf(pm[i].z, v.z), fmaxf(pm[i].w, v.w)};
-            }
+            for (int i = 0; i < 4; ++i) pm[i] = vmax4(pm[i], acc[i][j] * u);
         }
         const int obj = (m0 + 64 * wt) >> 6;   // the wave's 64 points are one object
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            f32x4 v = pm[i];
-            v = row16_max4(v);
+            const f32x4 v = relu4(row16_max4(pm[i]) + ld4(bias + (T0 + 4 * wo + i) * 16 + 4 * q));
             if (n == 0 && obj * 64 < a.M)
                 st4(a.out + (size_t)obj * a.ldo + a.out_off[br] + (T0 + 4 * wo + i) * 16 + 4 * q, v);
         }
