@@ -1241,6 +1241,39 @@ __global__ __launch_bounds__(TG_THREADS) void tok_split_gemm_kernel(TokArgs a) {
     }
 }
 
+// Level-0 projection without point features (Light encoder, c_prev = 0): Q[p] = W0_xyz . x_p + b for
+// both branches, a thread per (point, 4 channels), from the packed layer-0 fragments' xyz k-group (lane
+// ch % 16 of tile ch / 16 holds (wx, wy, wz, 0)). The fma chain in k order is what the fp32 MFMA path
+// (sa_pair_kernel) computes.
+struct ProjXyzArgs {
+    const float* xyz;       // (B * n, 3)
+    int npts;               // B * n
+    const float* w0[2];     // packed layer-0 fragments (k-groups kg0 = 1, xyz group 0)
+    const float* b0[2];
+    int ch[2];              // padded channel counts (16 | 32)
+    float* q;               // (B * n, q_stride)
+    int q_stride;
+};
+__global__ __launch_bounds__(256) void proj_xyz_kernel(ProjXyzArgs a) {
+    const int g4 = (a.ch[0] + a.ch[1]) / 4;
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (size_t)a.npts * g4) return;
+    const int p = (int)(t / g4), g = (int)(t - (size_t)p * g4);
+    const int br = 4 * g < a.ch[0] ? 0 : 1, c0 = 4 * g - (br ? a.ch[0] : 0);
+    const float x = a.xyz[(size_t)p * 3 + 0], y = a.xyz[(size_t)p * 3 + 1], z = a.xyz[(size_t)p * 3 + 2];
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ch = c0 + j;
+        const f32x4 w = ld4(a.w0[br] + ((size_t)(ch >> 4) * 64 + (ch & 15)) * 4);
+        float acc = __builtin_fmaf(w.x, x, 0.f);
+        acc = __builtin_fmaf(w.y, y, acc);
+        acc = __builtin_fmaf(w.z, z, acc);
+        v[j] = acc + a.b0[br][ch];
+    }
+    st4(a.q + (size_t)p * a.q_stride + 4 * g, f32x4{v[0], v[1], v[2], v[3]});
+}
+
 // ============================================================================ host side
 static const int kNpoint[4] = {512, 256, 128, 64};
 static const int kNs[2] = {16, 32};
@@ -1530,8 +1563,25 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             q_off += pad16(kWidths[l][br][1]);
         }
         const bool split0 = l >= 1 && enc_layer(layer_off, l, 0, 0)[2] >= 0 && enc_layer(layer_off, l, 1, 0)[2] >= 0;
-        rc = split0 ? run_proj_split(c, l, c_prev, feat_prev, xyz_prev, n_prev, qbuf, st)
-                    : launch_pair<4>(pp[0], pp[1], B, st);
+        if (l == 0 && c_prev == 0) {   // xyz only: 3 multiply-adds per channel
+            ProjXyzArgs pa = {};
+            pa.xyz = xyz_prev;
+            pa.npts = B * n_prev;
+            for (int br = 0; br < 2; ++br) {
+                pa.w0[br] = pp[br].w[0];
+                pa.b0[br] = pp[br].bias[0];
+                pa.ch[br] = pad16(kWidths[0][br][1]);
+            }
+            GP_REQUIRE(pa.ch[0] + pa.ch[1] == proj_stride(0), "encoder: level-0 projection layout");
+            pa.q = qbuf;
+            pa.q_stride = proj_stride(0);
+            const size_t threads = (size_t)pa.npts * (pa.ch[0] + pa.ch[1]) / 4;
+            hipLaunchKernelGGL(proj_xyz_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, pa);
+            rc = gp_check_launch("proj_xyz_kernel");
+        } else {
+            rc = split0 ? run_proj_split(c, l, c_prev, feat_prev, xyz_prev, n_prev, qbuf, st)
+                        : launch_pair<4>(pp[0], pp[1], B, st);
+        }
         if (rc) return rc;
     }
     if (l == 4 && enc_layer(layer_off, 4, 0, 0)[2] >= 0 && enc_layer(layer_off, 4, 0, 1)[2] >= 0 &&

@@ -159,12 +159,50 @@ int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const i
 }
 
 // ============================================================================ ball query
-// One wave per centroid, NR radii (1 or 2) answered by the same scan, 4 * BQ_CPW centroids of one
-// object per workgroup. LDSP: the object's points are staged in LDS once per workgroup as (x, y, z, 0)
-// (one ds_read_b128 per lane per 64-point ballot instead of three strided global loads); used while
-// they fit (n <= BQ_LDS_MAX).
+// NR radii (1 or 2) answered by the same scan.
 constexpr int BQ_CPW = 8;
 constexpr int BQ_LDS_MAX = 4096;
+// Scan state of one centroid: hits so far and the first hit, per radius.
+struct BqState {
+    int cnta, cntb, firsta, firstb;
+};
+
+template <int NR>
+__device__ __forceinline__ void bq_take(float d2, int k, int n, int base, float r2a, float r2b, int nsa, int nsb,
+                                        unsigned long long lt, int* oa, int* ob, BqState& st) {
+    const bool ha = (k < n) && d2 < r2a;
+    const unsigned long long ma = __ballot(ha);
+    if (st.cnta < nsa && ma) {
+        const int rank = st.cnta + __popcll(ma & lt);
+        if (ha && rank < nsa) oa[rank] = k;
+        if (st.firsta < 0) st.firsta = base + __ffsll((long long)ma) - 1;
+        st.cnta += __popcll(ma);
+    }
+    if (NR > 1) {
+        const bool hb = (k < n) && d2 < r2b;
+        const unsigned long long mb = __ballot(hb);
+        if (st.cntb < nsb && mb) {
+            const int rank = st.cntb + __popcll(mb & lt);
+            if (hb && rank < nsb) ob[rank] = k;
+            if (st.firstb < 0) st.firstb = base + __ffsll((long long)mb) - 1;
+            st.cntb += __popcll(mb);
+        }
+    }
+}
+
+template <int NR>
+__device__ __forceinline__ void bq_pad(int lane, int nsa, int nsb, int* oa, int* ob, const BqState& st) {
+    // pad with the first hit (ball_query_gpu.cu:35-40); no hit -> 0 (zero-initialised output)
+    for (int s = (st.cnta < nsa ? st.cnta : nsa) + lane; s < nsa; s += 64) oa[s] = st.firsta < 0 ? 0 : st.firsta;
+    if (NR > 1)
+        for (int s = (st.cntb < nsb ? st.cntb : nsb) + lane; s < nsb; s += 64) ob[s] = st.firstb < 0 ? 0 : st.firstb;
+}
+
+// One wave scans two centroids at once (p and p + 4): the distances of a point to both are packed fp32
+// operations (v_pk_add_f32 / v_pk_mul_f32), each rounded exactly as dist2_ref. 4 * BQ_CPW centroids of one
+// object per workgroup. LDSP: the object's points are staged in LDS once per workgroup as (x, y, z, 0);
+// used while they fit (n <= BQ_LDS_MAX).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int NR, bool LDSP>
 __global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const float* __restrict__ new_xyz,
                                                          const float* __restrict__ xyz, float r2a,
@@ -181,47 +219,40 @@ __global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const flo
     }
     const unsigned long long lt = (1ull << lane) - 1ull;
     const int pend = min(m, (int)(blockIdx.x + 1) * 4 * BQ_CPW);
-    for (int p = blockIdx.x * 4 * BQ_CPW + (threadIdx.x >> 6); p < pend; p += 4) {   // wave-uniform
-        const float* c = new_xyz + ((size_t)b * m + p) * 3;
-        const float cx = c[0], cy = c[1], cz = c[2];
-        int* oa = idxa + ((size_t)b * m + p) * nsa;
-        int* ob = NR > 1 ? idxb + ((size_t)b * m + p) * nsb : nullptr;
-        int cnta = 0, cntb = 0, firsta = -1, firstb = -1;
+    for (int p = blockIdx.x * 4 * BQ_CPW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); p < pend; p += 8) {
+        const int q = p + 4 < pend ? p + 4 : p;   // second centroid (a repeat of the first when absent)
+        const float* c0 = new_xyz + ((size_t)b * m + p) * 3;
+        const float* c1 = new_xyz + ((size_t)b * m + q) * 3;
+        const f32x2 cx = {c0[0], c1[0]}, cy = {c0[1], c1[1]}, cz = {c0[2], c1[2]};
+        int* oa0 = idxa + ((size_t)b * m + p) * nsa;
+        int* oa1 = idxa + ((size_t)b * m + q) * nsa;
+        int* ob0 = NR > 1 ? idxb + ((size_t)b * m + p) * nsb : nullptr;
+        int* ob1 = NR > 1 ? idxb + ((size_t)b * m + q) * nsb : nullptr;
+        BqState s0 = {0, 0, -1, -1}, s1 = {0, 0, -1, -1};
+        const bool two = q != p;
         for (int base = 0; base < n; base += 64) {
             const int k = base + lane;
-            float d2 = 3.0e38f;
+            f32x2 d2 = {3.0e38f, 3.0e38f};
             if (k < n) {
+#pragma clang fp contract(off)
+                float px, py, pz;
                 if constexpr (LDSP) {
                     const f32x4 v = sp[k];
-                    d2 = dist2_ref(cx, cy, cz, v.x, v.y, v.z);
+                    px = v.x; py = v.y; pz = v.z;
                 } else {
-                    d2 = dist2_ref(cx, cy, cz, pts[3 * k + 0], pts[3 * k + 1], pts[3 * k + 2]);
+                    px = pts[3 * k + 0]; py = pts[3 * k + 1]; pz = pts[3 * k + 2];
                 }
+                const f32x2 dx = cx - f32x2{px, px}, dy = cy - f32x2{py, py}, dz = cz - f32x2{pz, pz};
+                d2 = (dx * dx + dy * dy) + dz * dz;
             }
-            const bool ha = (k < n) && d2 < r2a;
-            const unsigned long long ma = __ballot(ha);
-            if (cnta < nsa && ma) {
-                const int rank = cnta + __popcll(ma & lt);
-                if (ha && rank < nsa) oa[rank] = k;
-                if (firsta < 0) firsta = base + __ffsll((long long)ma) - 1;
-                cnta += __popcll(ma);
-            }
-            if (NR > 1) {
-                const bool hb = (k < n) && d2 < r2b;
-                const unsigned long long mb = __ballot(hb);
-                if (cntb < nsb && mb) {
-                    const int rank = cntb + __popcll(mb & lt);
-                    if (hb && rank < nsb) ob[rank] = k;
-                    if (firstb < 0) firstb = base + __ffsll((long long)mb) - 1;
-                    cntb += __popcll(mb);
-                }
-            }
-            if (cnta >= nsa && (NR == 1 || cntb >= nsb)) break;
+            bq_take<NR>(d2.x, k, n, base, r2a, r2b, nsa, nsb, lt, oa0, ob0, s0);
+            if (two) bq_take<NR>(d2.y, k, n, base, r2a, r2b, nsa, nsb, lt, oa1, ob1, s1);
+            const bool done0 = s0.cnta >= nsa && (NR == 1 || s0.cntb >= nsb);
+            const bool done1 = !two || (s1.cnta >= nsa && (NR == 1 || s1.cntb >= nsb));
+            if (done0 && done1) break;
         }
-        // pad with the first hit (ball_query_gpu.cu:35-40); no hit -> 0 (zero-initialised output)
-        for (int s = (cnta < nsa ? cnta : nsa) + lane; s < nsa; s += 64) oa[s] = firsta < 0 ? 0 : firsta;
-        if (NR > 1)
-            for (int s = (cntb < nsb ? cntb : nsb) + lane; s < nsb; s += 64) ob[s] = firstb < 0 ? 0 : firstb;
+        bq_pad<NR>(lane, nsa, nsb, oa0, ob0, s0);
+        if (two) bq_pad<NR>(lane, nsa, nsb, oa1, ob1, s1);
     }
 }
 
