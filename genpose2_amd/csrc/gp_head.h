@@ -51,14 +51,17 @@ struct HeadSmem {
 };
 
 // Threads [FIRST, WV*64) copy the small weights into LDS.
-template <int NT, int WV, int FIRST = 0>
+// PE0 = false: pose_encoder.0's fragments and bias are not staged (the split trunk holds them in
+// registers from kernel entry, SplitScalars).
+template <int NT, int WV, int FIRST = 0, bool PE0 = true>
 __device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, HeadSmem<NT, WV>& sm) {
     constexpr int NTH = WV * 64 - FIRST;
     const int t0 = (int)threadIdx.x - FIRST;
     if (t0 < 0) return;
-    for (int i = t0; i < 16 * 64; i += NTH) sm.pe0w[i] = ld4(w.pe0_w + (size_t)i * 4);
+    if constexpr (PE0)
+        for (int i = t0; i < 16 * 64; i += NTH) sm.pe0w[i] = ld4(w.pe0_w + (size_t)i * 4);
     for (int i = t0; i < HID; i += NTH) {
-        sm.pe0b[i] = w.pe0_b[i];
+        if constexpr (PE0) sm.pe0b[i] = w.pe0_b[i];
         sm.pe2b[i] = w.pe2_b[i];
     }
     for (int i = t0; i < 9 * HID / 4; i += NTH) st4(&sm.h2w[i * 4], ld4(w.h2_w + (size_t)i * 4));
@@ -368,13 +371,26 @@ __device__ __forceinline__ void stream_h_step(__amdgpu_buffer_rsrc_t W, const in
 // The split trunk's activation bounds and weight exponents (gp_head_weights.hsc). Loaded at kernel entry by
 // the callers: read where they are used, their round trip (a cold L2 line after the kernel boundary) sat
 // on the critical path between the PC update and pose_encoder.0.
+// Also this wave's pose_encoder.0 A fragments and bias (output tiles 2 wid, 2 wid + 1 of an 8-wave
+// workgroup): loaded at kernel entry instead of being staged through LDS for every launch.
+constexpr int HSPLIT_WV = 8;   // waves per workgroup of every split-trunk kernel
 struct SplitScalars {
     float A0, B0, A2, B2;
     int ew2, ewh;
+    f32x4 pe0a[16 / HSPLIT_WV], pe0b[16 / HSPLIT_WV];
 };
 __device__ __forceinline__ SplitScalars load_split_scalars(const gp_head_weights& w) {
     const f32x4 a = ld4(w.hsc), b = ld4(w.hsc + 4);
-    return SplitScalars{a.x, a.y, a.z, a.w, (int)b.x, (int)b.y};
+    SplitScalars r{a.x, a.y, a.z, a.w, (int)b.x, (int)b.y, {}, {}};
+    const int lane = threadIdx.x & 63, q = lane >> 4;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int t = 0; t < 16 / HSPLIT_WV; ++t) {
+        const int T = wid * (16 / HSPLIT_WV) + t;
+        r.pe0a[t] = ld4(w.pe0_w + ((size_t)T * 64 + lane) * 4);
+        r.pe0b[t] = ld4(w.pe0_b + 16 * T + 4 * q);
+    }
+    return r;
 }
 
 // head_trunk with the split-f16 GEMMs (same contract and phases; pose_encoder.0 and layer 2 stay fp32).
@@ -384,6 +400,7 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
                                                  HeadSmem<NT, WV>& sm, int trace_slot, const SplitScalars hs) {
     constexpr int TPW = 16 / WV;   // output tiles per wave; tiles (2c, 2c+1) form 32-deep chunk c
     static_assert(TPW % 2 == 0, "split trunk pairs a wave's output tiles into 32-deep chunks");
+    static_assert(WV == HSPLIT_WV, "SplitScalars carries the pose_encoder.0 fragments of HSPLIT_WV waves");
     constexpr int CPW = TPW / 2;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -442,8 +459,8 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
         const int Ta = wid * TPW + 2 * c;
-        const f32x4 a0 = sm.pe0w[Ta * 64 + lane], a1 = sm.pe0w[(Ta + 1) * 64 + lane];
-        const f32x4 bias0 = ld4(&sm.pe0b[16 * Ta + 4 * q]), bias1 = ld4(&sm.pe0b[16 * (Ta + 1) + 4 * q]);
+        const f32x4 a0 = hs.pe0a[2 * c], a1 = hs.pe0a[2 * c + 1];
+        const f32x4 bias0 = hs.pe0b[2 * c], bias1 = hs.pe0b[2 * c + 1];
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
             const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -501,7 +518,7 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
             const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
 #pragma unroll
             for (int ct = 0; ct < NT; ++ct) {
-                const f32x4 u = relu4(acc[h * TPW + t][ct] * uh[ct]);
+                const f32x4 u = relu4(acc[h * TPW + t][ct]);   // still in the scaled domain
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     p[ct][0] = __builtin_fmaf(u[j], w0[j], p[ct][0]);
@@ -510,9 +527,13 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
                 }
             }
         }
+        // uh[ct] is a power of two: relu, every product and every partial sum scale by it exactly,
+        // so undoing it once per row sum equals undoing it per accumulator element (12 multiplies
+        // per column tile instead of 16 per output tile)
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-            const float s0 = rows_sum(p[ct][0]), s1 = rows_sum(p[ct][1]), s2 = rows_sum(p[ct][2]);
+            const float s0 = rows_sum(p[ct][0]) * uh[ct], s1 = rows_sum(p[ct][1]) * uh[ct],
+                        s2 = rows_sum(p[ct][2]) * uh[ct];
             if (q == 0) {
                 sm.red[ct * 16 + n][h * 3 + 0][wid] = s0;
                 sm.red[ct * 16 + n][h * 3 + 1][wid] = s1;

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         kout = a.kbuf[c->kidx[a.stage]];
         ynew = a.ybuf[c->yi ^ 1];
     }
-    stage_small_weights<NT, EVAL_WV>(a.w, sm);
+    stage_small_weights<NT, EVAL_WV, 0, !SPLIT>(a.w, sm);
     for (int i = tid; i < ROWS * 16; i += NTH) {
         const int c = i >> 4, j = i & 15;
         const int r = r0 + c;

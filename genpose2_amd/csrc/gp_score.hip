@@ -88,7 +88,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
     const int r0 = blockIdx.x * 16;
     SplitScalars hs = {};
     if constexpr (SPLIT) hs = load_split_scalars(w);
-    stage_small_weights<1, EVAL_WV>(w, sm);
+    stage_small_weights<1, EVAL_WV, 0, !SPLIT>(w, sm);
     for (int i = threadIdx.x; i < 256; i += EVAL_WV * 64) {
         const int c = i >> 4, j = i & 15;
         const int r = r0 + c;
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             }
         }
     }
-    stage_small_weights<NT, WV, 64 * NT>(a.w, sm);
+    stage_small_weights<NT, WV, 64 * NT, !SPLIT>(a.w, sm);
     if constexpr (SPLIT)
         head_trunk_split<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
     else
