@@ -43,11 +43,45 @@ def dist_env():
     return ws, rank, local
 
 
+def launch_command(argv, gpus, env, device_count, probe=False):
+    """How `bench.py --gpus N` runs: None = in this process (N == 1, or already a rank of a launcher
+    whose WORLD_SIZE equals N); otherwise the torchrun command that starts N ranks (one per GPU) as a
+    CHILD process -- never an exec, and decided before anything touches the GPU. Raises when N GPUs
+    are not there or a launcher's WORLD_SIZE disagrees with --gpus, so a 1-GPU box never reports a
+    1-rank run as N GPUs."""
+    if "WORLD_SIZE" in env:
+        ws = int(env["WORLD_SIZE"])
+        if ws != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {gpus}")
+        return None
+    if gpus == 1:
+        return None
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus}")
+    if not probe and device_count < gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but only {device_count} HIP device(s) are visible")
+    port = 29000 + os.getpid() % 2000
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_probe(ws, rank):
+    """--launch-probe: the launcher's rank plumbing without the GPU (gloo on CPU): every rank joins the
+    group, the ranks' ids are summed, rank 0 prints one JSON line."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([rank], dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_probe": True, "n_gpus": ws, "rank_sum": int(t.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def broadcast_weights(agent, ws):
-    """RCCL broadcast of the packed weight buffers from rank 0."""
+    """RCCL broadcast of the packed weights (device buffers + host layer tables) from rank 0."""
     if ws > 1:
         from genpose2_amd import shard
-        shard.broadcast_tensors(shard.model_tensors(agent), src=0)
+        shard.broadcast_agent(agent, src=0)
 
 
 def cpu_info():
@@ -257,9 +291,18 @@ def main():
                     help="1: encode batch k+1 on a side stream while batch k samples (every timed step "
                          "still encodes and samples one batch; the first encode is not overlapped). "
                          "Off by default: no gain measured (profiles/r1/ab_encoder_pipeline.txt)")
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    # device_count() does not initialise the GPU on this image, so starting a launcher after it is safe
+    ndev = 0 if args.launch_probe else torch.cuda.device_count()
+    cmd = launch_command(sys.argv[1:], args.gpus, os.environ, ndev, probe=args.launch_probe)
+    if cmd is not None:
+        import subprocess
+        sys.exit(subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")))
     cfgd = CONFIGS[args.config]
     ws, rank, local = dist_env()
+    if args.launch_probe:
+        return launch_probe(ws, rank)
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if ws > 1:

@@ -234,11 +234,11 @@ extern "C" int gp_linear(const float* x, int ldx, int m, int k, const float* w, 
 
 // ============================================================================ residual + LayerNorm
 // One wave per row (d <= 1024: up to 16 values per lane in registers), torch's biased variance.
-__global__ __launch_bounds__(FUS_THREADS) void add_layernorm_kernel(const float* __restrict__ x,
+__global__ __launch_bounds__(FUS_THREADS) void add_layernorm_kernel(const float* x,
                                                                     const float* __restrict__ r, int m, int d,
                                                                     const float* __restrict__ gamma,
                                                                     const float* __restrict__ beta, float eps,
-                                                                    float* __restrict__ y) {
+                                                                    float* y) {   // y may alias x
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * (FUS_THREADS / 64) + (threadIdx.x >> 6);

@@ -52,6 +52,17 @@ class EncoderModel:
         self._ws: Optional[torch.Tensor] = None
         self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
 
+    @property
+    def table(self) -> np.ndarray:
+        """The host layer table [5][2][3][4] (offsets and split-f16 exponents derived from the weight
+        values): part of the model's state beside ``wbuf``, so a weight broadcast carries it too."""
+        return self._table
+
+    def set_table(self, table: np.ndarray) -> None:
+        table = np.ascontiguousarray(table, np.int64).reshape(self._table.shape)
+        self._table = table
+        self.set_arith(self.arith)
+
     def set_arith(self, arith: str) -> None:
         """GEMM arithmetic of SA levels 1-3 and GroupAll: "split_f16" (f16 hi/lo MFMA products with
         per-column activation scaling: sa_narrow_split_kernel, sa_split_kernel, tok_split_gemm_kernel)

@@ -83,10 +83,20 @@ class FusEncoderModel:
         self.device = device
         buf, offs = pack.pack_encoder(sd, arch.fus_sa_branches())
         self.wbuf = torch.from_numpy(buf).to(device)
-        self.offsets = np.ascontiguousarray(offs.reshape(-1), np.int64)
+        self._table = np.ascontiguousarray(offs, np.int64)
+        self.offsets = self._table.reshape(-1)
         self.t = {k: torch.from_numpy(v).to(device) for k, v in pack_fus_blocks(sd).items()}
         self._ws: Optional[torch.Tensor] = None
         self._bias: Optional[torch.Tensor] = None
+
+    @property
+    def table(self) -> np.ndarray:
+        """Host SA layer table (offsets + split-f16 exponents), broadcast with the device buffers."""
+        return self._table
+
+    def set_table(self, table: np.ndarray) -> None:
+        self._table = np.ascontiguousarray(table, np.int64).reshape(self._table.shape)
+        self.offsets = self._table.reshape(-1)
 
     def _s(self):
         return ctypes.c_void_p(stream_handle(self.device))

@@ -94,20 +94,38 @@ class EvaluationPipeline:
 class ShardedEvaluationPipeline:
     """EvaluationPipeline over one process group (config 4: B=2048 objects over 8 GPUs).
 
-    Every rank holds the same agents; their packed weights are broadcast from ``src`` once (RCCL over
-    xGMI), so weights loaded on ``src`` alone (load_ckpt) reach every GPU. ``run`` takes the WHOLE
+    Every rank holds the same agents; their packed weights (device buffers and the host layer tables)
+    are broadcast from ``src`` (RCCL over xGMI) at construction and by ``sync_weights``, so weights
+    loaded on ``src`` alone (``load_ckpt`` then ``sync_weights``) reach every GPU. ``run`` takes the WHOLE
     batch on every rank, processes the rank's contiguous object block (shard.shard_range) with no
     collective on the sampling path -- each shard is a reference call on its sub-batch -- and gathers
     pred_pose, pts_feat, energy, aggregated and length back in object order on every rank (dst=None)
     or on ``dst`` only."""
 
     def __init__(self, cfg: GenPoseConfig, with_energy: bool = True, with_scale: bool = False, src: int = 0):
-        from . import shard
         self.local = EvaluationPipeline(cfg, with_energy, with_scale)
         self.src = src
-        for a in (self.local.score_agent, self.local.energy_agent, self.local.scale_agent):
-            if a is not None:
-                shard.broadcast_tensors(shard.model_tensors(a), src=src)
+        self.sync_weights()
+
+    def agents(self):
+        return [a for a in (self.local.score_agent, self.local.energy_agent, self.local.scale_agent) if a is not None]
+
+    def load_ckpt(self, score: Optional[str] = None, energy: Optional[str] = None, scale: Optional[str] = None) -> None:
+        """Load reference checkpoints on ``src`` only (paths may not exist on the other ranks), then
+        broadcast them to every rank."""
+        import torch.distributed as dist
+        if dist.get_rank() == self.src:
+            for a, p in ((self.local.score_agent, score), (self.local.energy_agent, energy),
+                         (self.local.scale_agent, scale)):
+                if a is not None and p:
+                    a.load_ckpt(model_dir=p, model_path=True, load_model_only=True)
+        self.sync_weights()
+
+    def sync_weights(self) -> None:
+        """Every agent's weights from ``src`` to all ranks (buffers + host tables; shard.broadcast_agent)."""
+        from . import shard
+        for a in self.agents():
+            shard.broadcast_agent(a, src=self.src)
 
     def run(self, batch: Dict[str, torch.Tensor], dst: Optional[int] = None) -> Optional[StageOutputs]:
         import torch.distributed as dist

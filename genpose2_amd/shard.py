@@ -32,6 +32,54 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0) -> None:
         dist.broadcast(t, src=src)
 
 
+def broadcast_packed(tensors: Iterable[torch.Tensor], tables: Iterable[np.ndarray], src: int = 0,
+                     device: Optional[torch.device] = None) -> List[np.ndarray]:
+    """Broadcast an agent's packed buffers AND its host layer tables from ``src``; returns the tables
+    as received. The tables hold the split-f16 exponents the encoder kernels read from the host
+    (pack.split_exponent of the weight values), so a rank that broadcast only the buffers would keep
+    exponents of its own initial weights and scale its levels wrongly. ``device``: where the table
+    travels (the buffers' device under RCCL; CPU under gloo)."""
+    import torch.distributed as dist
+    broadcast_tensors(tensors, src)
+    out = []
+    for tab in tables:
+        t = torch.from_numpy(np.ascontiguousarray(tab, np.int64).copy())
+        if device is not None:
+            t = t.to(device)
+        dist.broadcast(t, src=src)
+        out.append(t.cpu().numpy().reshape(np.shape(tab)))
+    return out
+
+
+def model_tables(agent) -> List[np.ndarray]:
+    """Host-side weight-derived state of an agent (the encoder's layer table), in a fixed order --
+    the same order as ``packed_host_tables``."""
+    enc = getattr(agent, "encoder", None)
+    return [enc.table] if enc is not None else []
+
+
+def broadcast_agent(agent, src: int = 0) -> None:
+    """Make every rank's agent hold ``src``'s weights: the device buffers (``model_tensors``) and the
+    host layer tables (``model_tables``), then drop caches derived from the old weights. Call it
+    after construction and again after ``load_ckpt`` on ``src``."""
+    dev_ = agent.device if agent.device.type == "cuda" else None
+    tabs = broadcast_packed(model_tensors(agent), model_tables(agent), src, dev_)
+    if tabs:
+        agent.encoder.set_table(tabs[0])
+    agent._pc_cache = {}
+
+
+def packed_host_tables(kind: str, sd) -> List[np.ndarray]:
+    """Host tables ``model_tables`` holds for an agent of ``kind`` built from ``sd``."""
+    from . import pack
+    if kind == "scale":
+        return []
+    if kind.endswith("_pointwise"):
+        from . import arch
+        return [pack.pack_encoder(sd, arch.fus_sa_branches())[1]]
+    return [pack.pack_encoder(sd)[1]]
+
+
 def model_tensors(agent) -> List[torch.Tensor]:
     """Device tensors holding an agent's packed weights, in a fixed order: the encoder buffer, then
     the head (or ScaleNet) buffers by name -- the same order as ``packed_host_tensors``."""

@@ -64,7 +64,9 @@ int gp_group_points(int b, int c, int n, int npoints, int nsample, const float *
  * layer i of branch b of level l, {float offset of the fp32 A fragments, float offset of the bias
  * (padded to 32), float offset of the split-f16 hi/lo planes or -1, their power-of-two exponent}
  * (-1 = absent). Levels 2-3 run as split-f16 MFMA (per-column activation scaling) when all four of
- * their layer-1/2 plane offsets are given, exact fp32 MFMA otherwise. ABI 4. */
+ * their layer-1/2 plane offsets are given, exact fp32 MFMA otherwise. ABI 5: the [..][4] table;
+ * a [5][2][3][2] table of ABI <= 3 is no longer accepted. The exponents are weight-derived state: a
+ * host that receives the weights from another rank must receive this table too. */
 size_t gp_encoder_workspace_size(int b, int n);
 /* HOST out: byte offsets in the workspace of, per level l<4: fps idx (b,M_l) int32,
  * new_xyz (b,M_l,3) fp32, ball idx branch0/1 (b,M_l,ns) int32; and per level l<5 the level

@@ -219,10 +219,18 @@ def _gloo_worker(rank, world, port, out_dir, total):
     # weights, the others start from different ones and receive rank 0's by broadcast (the RCCL step)
     ok = True
     for kind in ("score", "energy", "scale"):
-        mine = shard.packed_host_tensors(kind, weights.synthetic_state_dict(kind, seed=0 if rank == 0 else 99))
-        shard.broadcast_tensors(mine, src=0)
-        ref = shard.packed_host_tensors(kind, weights.synthetic_state_dict(kind, seed=0))
+        sd_mine = weights.synthetic_state_dict(kind, seed=0 if rank == 0 else 99)
+        mine = shard.packed_host_tensors(kind, sd_mine)
+        # the host layer tables (split-f16 exponents of the weight VALUES) travel with the buffers
+        tabs = shard.broadcast_packed(mine, shard.packed_host_tables(kind, sd_mine), src=0)
+        sd_ref = weights.synthetic_state_dict(kind, seed=0)
+        ref = shard.packed_host_tensors(kind, sd_ref)
+        ref_tabs = shard.packed_host_tables(kind, sd_ref)
         ok &= len(mine) == len(ref) and all(torch.equal(a, b) for a, b in zip(mine, ref))
+        ok &= len(tabs) == len(ref_tabs) and all(np.array_equal(a, b) for a, b in zip(tabs, ref_tabs))
+        if rank != 0 and kind != "scale":
+            # the seeds differ in at least one exponent, or this check would prove nothing
+            ok &= not all(np.array_equal(a, b) for a, b in zip(shard.packed_host_tables(kind, sd_mine), ref_tabs))
     lo, hi = shard.shard_range(total, world, rank)
     K, T = 4, 5
     if hi > lo:
@@ -392,3 +400,46 @@ def test_weights_pack_host_reports_missing_key():
     del sd["pose_score_net.pose_encoder.2.bias"]
     with pytest.raises(_lib.GenPoseHipError, match="pose_encoder.2.bias"):
         _pack_host(0, sd)
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("genpose_bench", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_bench_launcher_plan():
+    """bench.py --gpus N: in-process for N=1 or inside a launcher whose WORLD_SIZE is N; a torchrun CHILD
+    with N ranks otherwise; a loud failure when N GPUs are missing or WORLD_SIZE disagrees."""
+    b = _bench_module()
+    assert b.launch_command(["--gpus", "1"], 1, {}, 0) is None
+    assert b.launch_command(["--gpus", "8"], 8, {"WORLD_SIZE": "8"}, 8) is None
+    cmd = b.launch_command(["--gpus", "4", "--steps", "3"], 4, {}, 8)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    with pytest.raises(SystemExit, match="only 1 HIP device"):
+        b.launch_command(["--gpus", "2"], 2, {}, 1)
+    with pytest.raises(SystemExit, match="WORLD_SIZE=1"):
+        b.launch_command(["--gpus", "2"], 2, {"WORLD_SIZE": "1"}, 8)
+
+
+def test_bench_gpus2_without_gpus_fails_loudly():
+    """On a host with fewer GPUs than --gpus the bench exits non-zero instead of printing n_gpus: 1."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--no-cpu-baseline"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode != 0 and "HIP device" in p.stderr and '"n_gpus"' not in p.stdout
+
+
+def test_bench_launcher_starts_world2_gloo():
+    """The launcher path end to end on CPU: bench.py --gpus 2 --launch-probe starts 2 ranks under torchrun
+    (gloo), which all-reduce their ranks; rank 0 prints n_gpus 2."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--launch-probe"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line == {"launch_probe": True, "n_gpus": 2, "rank_sum": 1}

@@ -1,0 +1,66 @@
+"""Multi-rank product path on one MI355X: two ranks share cuda:0 over gloo (RCCL needs one GPU per
+rank; the driver's 8-GPU run covers RCCL itself). Each rank builds its agents from DIFFERENT synthetic
+weights; after ShardedEvaluationPipeline's broadcast every rank must compute with rank 0's weights,
+including the encoder's host layer table (split-f16 exponents), so the gathered outputs equal
+per-shard EvaluationPipeline runs with rank 0's weights (each shard is a reference call
+on its sub-batch)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _cfg(seed):
+    from genpose2_amd.config import GenPoseConfig
+    return GenPoseConfig(device=DEV, sampling_steps=20, eval_repeat_num=20, noise_seed=4, seed=seed)
+
+
+def _batch(total):
+    from genpose2_amd import synthetic
+    pts, center = synthetic.make_batch(12, total, 1024)
+    return {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
+
+
+def _worker(rank, world, port, out_dir, total, ckpt):
+    import torch.distributed as dist
+    from genpose2_amd.runner import ShardedEvaluationPipeline
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        pipe = ShardedEvaluationPipeline(_cfg(seed=0 if rank == 0 else 99), with_scale=True)
+        if ckpt:   # rank 0 alone reads a checkpoint (seed 7 weights), then broadcasts it
+            pipe.load_ckpt(score=ckpt if rank == 0 else "/nonexistent/on/this/rank.pth")
+        got = pipe.run(_batch(total))
+        if rank == 0:
+            for k in ("pred_pose", "pts_feat", "energy", "aggregated", "length"):
+                np.save(os.path.join(out_dir, f"{k}.npy"), getattr(got, k).cpu().numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("with_ckpt", [False, True])
+def test_two_ranks_mismatched_seeds_equal_rank0_weights(tmp_path, with_ckpt):
+    import torch.multiprocessing as mp
+    from conftest import write_reference_checkpoint
+    from genpose2_amd import shard
+    from genpose2_amd.runner import EvaluationPipeline
+    total, world = 5, 2
+    ckpt = write_reference_checkpoint(str(tmp_path / "score.pth"), "score", seed=7) if with_ckpt else ""
+    port = 29300 + (os.getpid() + int(with_ckpt)) % 600
+    mp.spawn(_worker, args=(world, port, str(tmp_path), total, ckpt), nprocs=world, join=True)
+    batch = _batch(total)
+    parts = []
+    for r in range(world):
+        lo, hi = shard.shard_range(total, world, r)
+        ref = EvaluationPipeline(_cfg(seed=0), with_scale=True)
+        if with_ckpt:
+            ref.score_agent.load_ckpt(model_dir=ckpt, model_path=True, load_model_only=True)
+        parts.append(ref.run({k: v[lo:hi] for k, v in batch.items()}))
+    for k in ("pred_pose", "pts_feat", "energy", "aggregated", "length"):
+        want = torch.cat([getattr(p, k) for p in parts]).cpu().numpy()
+        np.testing.assert_array_equal(np.load(tmp_path / f"{k}.npy"), want, err_msg=k)
