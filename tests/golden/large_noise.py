@@ -21,14 +21,20 @@ CASES = {
     "pc_r12800_t500": ("pc", 63, 256, 50, 500, None, 6300),   # the north-star shape itself
     "ode_r4800": ("ode", 64, 96, 50, None, 0.55, 6400),
     "ode_r12800": ("ode", 65, 256, 50, None, 0.55, 6500),
+    "pc_cfg5_t100": ("pc", 66, 256, 100, 100, None, 6600),    # config-5 shape (N=2048, K=100) at T=100
 }
+# points per object where it is not 1024
+N_POINTS = {"pc_cfg5_t100": 2048}
+# steps j of pc_r12800_t500 whose reference state x_j (the score net's input at step j) and x_{j+1} are
+# recorded in golden_large_steps_r12800.npz: single-step pins of the 64-candidate PC tile
+STEP_PINS = (1, 400)
 
 
 def inputs(name: str):
     """(pts (B,N,3), pts_center (B,3), prior (R,9), z1 (T,R,9) | None, z2 (T,R,9) | None)."""
     from genpose2_amd import synthetic
     sampler, cid, B, K, T, _, seed = CASES[name]
-    pts, center = synthetic.make_batch(cid, B, 1024)
+    pts, center = synthetic.make_batch(cid, B, N_POINTS.get(name, 1024))
     R = B * K
     rng = np.random.Generator(np.random.PCG64(seed))
     prior = rng.standard_normal((R, 9), dtype=np.float32)

@@ -1,0 +1,191 @@
+"""The north-star configurations at full size on a real MI355X, against the reference where a reference
+run fits this container (tests/golden/make_golden_large.py) and through size-independent properties
+where it does not.
+
+* EnergyNet + ranking + aggregation at config 4's shape (R = 12,800) on the reference's own poses:
+  energies within 1e-5 of max|ref| per object, the sort order identical, the aggregated 4x4 within
+  1e-5 (rotation absolute, translation relative) -- with and without DBSCAN, and on a clustered
+  candidate set where DBSCAN re-averages every object.
+* Config 5's shape (B=256, N=2048, K=100: R = 25,600 rows, two passes of 64-candidate PC tiles) at
+  T=100: the N=2048 encoder output at 1e-5, the PC poses at the calibrated bar
+  (large_noise.check_calibrated), ScaleNet lengths at 1e-5.
+* Single-step pins at R = 12,800: from the reference's own state x_j, one PC step (Langevin corrector
+  with the batch's grad_norm, predictor, Gram-Schmidt) against the reference's x_{j+1} -- 1e-5 on
+  rotation (absolute) and translation (relative), for both arithmetic paths. This holds the
+  64-candidate tile itself to the north-star bar, independent of trajectory chaos.
+* Config 5 at its full T=1000 with device noise: determinism, Philox == the same draws injected,
+  orthonormal rotations, unit quaternions, finite ScaleNet lengths.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _agent(**kw):
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    return PoseNet(GenPoseConfig(device=DEV, **kw)).eval()
+
+
+def _rot_abs(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())
+
+
+def _rel(a, b):
+    b = np.asarray(b, np.float64)
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _check_agg(got, want):
+    assert _rot_abs(got[:, :3, :3], want[:, :3, :3]) < 1e-5
+    assert _rel(got[:, :3, 3], want[:, :3, 3]) < 1e-5
+    assert np.array_equal(got[:, 3], want[:, 3])
+
+
+@pytest.mark.parametrize("arith", ["split_f16", "f32"])
+def test_energy_rank_aggregate_r12800_vs_reference(arith):
+    import large_noise
+    from genpose2_amd import aggregate, synthetic
+    g = golden("large_energy_r12800")
+    src = str(g["src"])
+    _, cid, B, K, _, _, _ = large_noise.CASES[src]
+    pts, center = synthetic.make_batch(cid, B, 1024)
+    agent = _agent(agent_type="energy")
+    agent.heads.set_arith(arith)
+    agent.encoder.set_arith(arith)
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
+    cases = [(golden(f"large_{src}")["pred_pose"], g["energy"], g["sort_idx"], {0: g["aggregated_c0"],
+                                                                              1: g["aggregated_c1"]}),
+             (g["cl_pose"], g["cl_energy"], g["cl_sort_idx"], {1: g["cl_aggregated_c1"]})]
+    keep = int(K * 0.4)
+    for pose_np, e_ref, idx_ref, aggs in cases:
+        pose = torch.from_numpy(pose_np).to(DEV)
+        e = agent.get_energy(dict(data), pose, T=1e-5, mode="test", extract_feature=True)
+        assert e.shape == (B, K, 2) and e.dtype == torch.float32
+        e_np = e.cpu().numpy()
+        err = np.abs(e_np - e_ref).reshape(B, -1).max(1) / np.abs(e_ref).reshape(B, -1).max(1)
+        assert err.max() < 1e-5, err.max()
+        # ranking: the rotation part follows energy column 0's descending order, the translation part
+        # column 1's (reward.py:145-153) -- identical to the reference's order
+        sp, se = aggregate.sort_poses_by_energy(pose, e)
+        idx = idx_ref.astype(np.int64)
+        want_rot = np.take_along_axis(pose_np, idx[..., 0:1], 1)[..., :6]
+        want_tr = np.take_along_axis(pose_np, idx[..., 1:2], 1)[..., 6:]
+        sp = sp.cpu().numpy()
+        assert np.array_equal(sp[..., :6], want_rot) and np.array_equal(sp[..., 6:], want_tr)
+        for c, want in aggs.items():
+            # from the reference's energies (the aggregation alone) and from ours (the whole leg)
+            for energies in (torch.from_numpy(e_ref).to(DEV), e):
+                got = aggregate.aggregate_pose(pose, energies, 0.4, c, 0.05, 0.1667, retain_num=keep)
+                _check_agg(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("arith", ["split_f16", "f32"])
+def test_config5_shape_vs_reference(arith):
+    """B=256, N=2048, K=100 (R=25,600: 400 PC workgroups, two passes), T=100, reference noise."""
+    import large_noise
+    from genpose2_amd.agent import NoiseFeed
+    name = "pc_cfg5_t100"
+    g = golden(f"large_{name}")
+    _, _, B, K, T, _, _ = large_noise.CASES[name]
+    pts, center, prior, z1, z2 = large_noise.inputs(name)
+    assert pts.shape == (256, 2048, 3) and B * K == 25600
+    agent = _agent(sampling_steps=T)
+    agent.heads.set_arith(arith)
+    agent.encoder.set_arith(arith)
+    agent.noise_feed = NoiseFeed(torch.from_numpy(prior), torch.from_numpy(np.ascontiguousarray(z1)),
+                                 torch.from_numpy(np.ascontiguousarray(z2)))
+    del z1, z2
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
+    pose, q = agent.pred_func(data, repeat_num=K)
+    feat = data["pts_feat"].cpu().numpy()
+    err = np.abs(feat - g["pts_feat"]).max(1) / np.abs(g["pts_feat"]).max(1)
+    assert err.max() < 1e-5, err.max()
+    p = pose.cpu().numpy()
+    stats = large_noise.check_calibrated(p, g)
+    print(name, arith, stats)
+    assert _rel(p[..., 6:], g["pred_pose"][..., 6:]) < 1e-5
+    assert torch.isfinite(q).all()
+    scale = _agent(agent_type="scale")
+    _, length = scale.pred_scale_func({"pts_feat": torch.from_numpy(g["pts_feat"]).to(DEV),
+                                       "axes": torch.from_numpy(g["scale_axes"]).to(DEV)})
+    assert _rel(length.cpu().numpy(), g["scale_length"]) < 1e-5
+
+
+@pytest.mark.parametrize("arith", ["split_f16", "f32"])
+def test_pc_single_step_pins_r12800(arith):
+    import large_noise
+    g = golden("large_steps_r12800")
+    src = str(g["src"])
+    _, _, B, K, T, _, _ = large_noise.CASES[src]
+    pts, center, prior, z1, z2 = large_noise.inputs(src)
+    agent = _agent(sampling_steps=T)
+    agent.heads.set_arith(arith)
+    agent.encoder.set_arith(arith)
+    cdev = torch.from_numpy(center).to(DEV)
+    feat = agent.encoder.forward(torch.from_numpy(pts).to(DEV))
+    pobj = agent.heads.object_proj(feat)
+    tab, tproj = agent._pc_table(T)
+    c_rows = np.repeat(center, K, 0)                     # (R,3): object of row r is r // K
+    for j in (int(s) for s in g["steps"]):
+        x = torch.from_numpy(g[f"x_{j}"]).to(DEV).contiguous()
+        zz1 = torch.from_numpy(np.ascontiguousarray(z1[j:j + 2])).to(DEV)
+        zz2 = torch.from_numpy(np.ascontiguousarray(z2[j:j + 2])).to(DEV)
+        # a 2-step call over grid rows j, j+1: its xs[:, 0] is the state after step j, + pts_center
+        _, _, xs = agent.heads.pc_sample(pobj, tproj[j:j + 2], tab[j:j + 2], x, K, cdev, z1=zz1, z2=zz2,
+                                         want_xs=True)
+        got = xs[:, 0].cpu().numpy()
+        want = g[f"x_{j + 1}"].copy()
+        want[:, 6:] = want[:, 6:] + c_rows                  # samplers.py:173 in fp32, as the kernel does
+        rot = _rot_abs(got[:, :6], want[:, :6])
+        tr = _rel(got[:, 6:], want[:, 6:])
+        print(f"step {j} ({arith}): rotation {rot:.2e} abs, translation {tr:.2e} rel")
+        assert rot < 1e-5 and tr < 1e-5, (j, rot, tr)
+
+
+def test_config5_full_t1000_properties():
+    """Config 5 at full size (B=256, N=2048, K=100, T=1000) with device Philox noise."""
+    from genpose2_amd import device, synthetic
+    B, N, K, T = 256, 2048, 100, 1000
+    R = B * K
+    pts, center = synthetic.make_batch(5, B, N)
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
+    a1 = _agent(sampling_steps=T, noise_seed=11)
+    a2 = _agent(sampling_steps=T, noise_seed=11)
+    d1 = dict(data)
+    p1, q1 = a1.pred_func(d1, repeat_num=K)
+    p2, q2 = a2.pred_func(dict(data), repeat_num=K)
+    assert p1.shape == (B, K, 9) and torch.isfinite(p1).all() and torch.isfinite(q1).all()
+    assert torch.equal(p1, p2) and torch.equal(q1, q2)
+    r = p1.reshape(-1, 9).double()
+    b1, b2 = r[:, :3], r[:, 3:6]
+    assert (b1.norm(dim=1) - 1).abs().max() < 1e-5 and (b2.norm(dim=1) - 1).abs().max() < 1e-5
+    assert (b1 * b2).sum(1).abs().max() < 1e-5
+    assert (q1[..., :4].double().norm(dim=-1) - 1).abs().max() < 1e-5
+    # the same run with its Philox draws injected (1.8 GB of noise on the device) is bit-identical
+    heads = a1.heads
+    feat = d1["pts_feat"]
+    pobj = heads.object_proj(feat)
+    tab, tproj = a1._pc_table(T)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    x0 = torch.randn((R, 9), generator=g, device=DEV) * 50.0
+    seed = 77
+    res_p, q_p, _ = heads.pc_sample(pobj, tproj, tab, x0.clone(), K, data["pts_center"], seed=seed)
+    z1 = torch.empty((T, R, 9), device=DEV)
+    z2 = torch.empty((T, R, 9), device=DEV)
+    for j in range(T):
+        z1[j] = device.randn(seed, 2 * j, R, 9, DEV)
+        z2[j] = device.randn(seed, 2 * j + 1, R, 9, DEV)
+    res_i, q_i, _ = heads.pc_sample(pobj, tproj, tab, x0.clone(), K, data["pts_center"], z1=z1, z2=z2)
+    assert torch.equal(res_p, res_i) and torch.equal(q_p, q_i)
+    del z1, z2
+    scale = _agent(agent_type="scale")
+    axes = torch.eye(3, device=DEV).expand(B, 3, 3).contiguous()
+    _, length = scale.pred_scale_func({"pts_feat": feat, "axes": axes})
+    assert length.shape == (B, 3) and torch.isfinite(length).all()

@@ -180,3 +180,30 @@ def test_fus_encoder_levels():
                 assert rel(levels[lv][k][0], g[f"l{lv}_{k}"]) < 1e-5, (lv, k)
     assert rel(levels[3]["bias"][0], g["l3_bias"]) < 1e-6
     assert rel(feat, g["feat"]) < 1e-5
+
+
+def test_energy_rank_aggregate_r12800_subset(energy_sd):
+    """golden_large_energy_r12800 (EnergyNet + sort + aggregation at config 4's shape) on its first 12
+    objects: the oracle's energies within 1e-5 of max|ref| per object, the sort order identical, the
+    aggregated 4x4 within 1e-5 -- plain and clustered candidate sets."""
+    import large_noise
+    from genpose2_amd import synthetic
+    g = golden("large_energy_r12800")
+    src = str(g["src"])
+    _, cid, B, K, _, _, _ = large_noise.CASES[src]
+    n = 12
+    pts, center = synthetic.make_batch(cid, B, 1024)
+    pts, center = pts[:n], center[:n]
+    plain = golden(f"large_{src}")["pred_pose"][:n]
+    for pose, e_ref, idx, agg_ref, c in ((plain, g["energy"], g["sort_idx"], g["aggregated_c0"], 0),
+                                         (g["cl_pose"][:n], g["cl_energy"], g["cl_sort_idx"], g["cl_aggregated_c1"], 1)):
+        e = oracle.get_energy(energy_sd, pts, center, pose, 1e-5)
+        err = np.abs(e - e_ref[:n]).reshape(n, -1).max(1) / np.abs(e_ref[:n]).reshape(n, -1).max(1)
+        assert err.max() < 1e-5
+        sp, _, _, _ = oracle.sort_poses_by_energy(pose, e)
+        ii = idx[:n].astype(np.int64)
+        np.testing.assert_array_equal(sp[..., :6], np.take_along_axis(pose, ii[..., 0:1], 1)[..., :6])
+        np.testing.assert_array_equal(sp[..., 6:], np.take_along_axis(pose, ii[..., 1:2], 1)[..., 6:])
+        agg = oracle.aggregate_pose(pose, e, clustering=c)
+        assert np.abs(agg[:, :3, :3] - agg_ref[:n, :3, :3]).max() < 1e-5
+        assert rel(agg[:, :3, 3], agg_ref[:n, :3, 3]) < 1e-5
