@@ -664,6 +664,27 @@ __device__ __forceinline__ void quat_from_gs(const T* v, T* qo) {
 // Head layer-1 t block for one time value (HT threads): tproj = W1_t . relu(W_te . [sin, cos](GFP(t)) + b_te)
 // (scorenet.py:77-88 GaussianFourierProjection + t_encoder, the t columns of the first head layer).
 // Writes out[o] for o in [o0, o1) (the caller's slice of the 768-row).
+// sum_c W[c * stride] * x[c] over N = CH * L terms as CH interleaved fp32 chains (chain j: c = j, j + CH,
+// ...) combined by a pairwise tree -- the accumulation pattern of a vectorised CPU GEMM. A single
+// N-term chain is ~sqrt(N) roundings deep; the energy's pose . score sums cancel enough to expose it
+// (the 1024-term pts block of head layer 1 was 2x the reference's own fp32 error at R=12,800).
+template <int N, int CH>
+__device__ __forceinline__ float dot_chains(const float* __restrict__ W, size_t stride, const float* x) {
+    static_assert(N % CH == 0 && (CH & (CH - 1)) == 0, "N must be a multiple of the power-of-two CH");
+    float p[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) p[j] = 0.f;
+    for (int c0 = 0; c0 < N; c0 += CH) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) p[j] = fmaf(W[(size_t)(c0 + j) * stride], x[c0 + j], p[j]);
+    }
+#pragma unroll
+    for (int s = CH / 2; s >= 1; s >>= 1)
+#pragma unroll
+        for (int j = 0; j < s; ++j) p[j] += p[j + s];
+    return p[0];
+}
+
 __device__ __forceinline__ void time_row(const gp_head_weights& w, float t, float* emb, float* tf,
                                          float* __restrict__ out, int o0 = 0, int o1 = 768) {
     const int i = threadIdx.x;
@@ -673,15 +694,7 @@ __device__ __forceinline__ void time_row(const gp_head_weights& w, float t, floa
         emb[64 + i] = cosf(a);
     }
     __syncthreads();
-    if (i < 128) {
-        float acc = 0.f;
-        for (int c = 0; c < 128; ++c) acc += w.te_w_t[c * 128 + i] * emb[c];
-        tf[i] = fmaxf(acc + w.te_b[i], 0.f);
-    }
+    if (i < 128) tf[i] = fmaxf(dot_chains<128, 16>(w.te_w_t + i, 128, emb) + w.te_b[i], 0.f);
     __syncthreads();
-    for (int o = o0 + i; o < o1; o += HT) {
-        float acc = 0.f;
-        for (int c = 0; c < 128; ++c) acc += w.h1t_t[c * 768 + o] * tf[c];
-        out[o] = acc;
-    }
+    for (int o = o0 + i; o < o1; o += HT) out[o] = dot_chains<128, 16>(w.h1t_t + o, 768, tf);
 }
