@@ -9,6 +9,9 @@
 // writes y_new and the per-workgroup sum of (err / scale)^2 of scipy's error estimator
 // (_estimate_error_norm, rk.py); ode_norm_kernel reduces it in a fixed order. The step
 // controller's scalars stay on the host (genpose2_amd/ode.py): one 8-byte read per attempt.
+#include <cstddef>
+#include <utility>
+
 #include "gp_head.h"
 
 #define ODE_NK 7   // Dormand-Prince stages incl. the FSAL derivative
@@ -671,4 +674,188 @@ extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, 
     a.part = part;
     ode_launch_stage<1>(a, nt, stream);
     return gp_check_launch("ode_stage_kernel<auto>");
+}
+
+// ============================================================================ whole sampler (C hosts)
+// cond_ode_sampler (samplers.py:180-258) in one call for hosts without Python: select_initial_step
+// (scipy _ivp/common.py) from two host-scalar RHS evaluations, then the device-controlled attempts
+// (gp_ode_auto_attempt) kept one attempt ahead of a 4-byte status read, the dense output at eps when
+// `steps` > 0 (t_eval = linspace(T0, eps, steps): only its last point reaches cond_ode_sampler), the
+// final denoise step and the epilogue (gp_ode_denoise). genpose2_amd/ode.py (rk45_device) and
+// agent.py (PoseNet._ode) are the Python form of the same sequence.
+namespace {
+// Dormand-Prince tableau exactly as scipy's RK45 class attributes (rk.py)
+const double kA6[36] = {0, 0, 0, 0, 0, 0,
+                        1.0 / 5, 0, 0, 0, 0, 0,
+                        3.0 / 40, 9.0 / 40, 0, 0, 0, 0,
+                        44.0 / 45, -56.0 / 15, 32.0 / 9, 0, 0, 0,
+                        19372.0 / 6561, -25360.0 / 2187, 64448.0 / 6561, -212.0 / 729, 0, 0,
+                        9017.0 / 3168, -355.0 / 33, 46732.0 / 5247, 49.0 / 176, -5103.0 / 18656, 0};
+const double kB6[6] = {35.0 / 384, 0, 500.0 / 1113, 125.0 / 192, -2187.0 / 6784, 11.0 / 84};
+const double kE7[7] = {-71.0 / 57600, 0, 71.0 / 16695, -71.0 / 1920, 17253.0 / 339200, -22.0 / 525, 1.0 / 40};
+const double kP74[28] = {1, -8048581381.0 / 2820520608, 8663915743.0 / 2820520608, -12715105075.0 / 11282082432,
+                         0, 0, 0, 0,
+                         0, 131558114200.0 / 32700410799, -68118460800.0 / 10900136933, 87487479700.0 / 32700410799,
+                         0, -1754552775.0 / 470086768, 14199869525.0 / 1410260304, -10690763975.0 / 1880347072,
+                         0, 127303824393.0 / 49829197408, -318862633887.0 / 49829197408, 701980252875.0 / 199316789632,
+                         0, -282668133.0 / 205662961, 2019193451.0 / 616988883, -1453857185.0 / 822651844,
+                         0, 40617522.0 / 29380423, -110615467.0 / 29380423, 69997945.0 / 29380423};
+constexpr double kSigMin = 0.01, kBase = 50.0 / 0.01;
+
+double diff_scale() { return sqrt(2.0 * (log(50.0) - log(0.01))); }
+// sigma(t32) as sde.py forms it for a float32 tensor: f32(0.01) * 5000^t32 (power correctly rounded)
+float sigma32(float t32) { return 0.01f * (float)pow(kBase, (double)t32); }
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+struct OdeSampleLayout {
+    size_t y[2], k[ODE_NK], f1, dense, scal, rhs_ws, auto_ws, total;
+};
+OdeSampleLayout ode_sample_layout(int rows) {
+    OdeSampleLayout L = {};
+    const size_t vec = align256((size_t)rows * 9 * sizeof(double));
+    size_t off = 0;
+    for (int i = 0; i < 2; ++i) { L.y[i] = off; off += vec; }
+    for (int j = 0; j < ODE_NK; ++j) { L.k[j] = off; off += vec; }
+    L.f1 = off; off += vec;
+    L.dense = off; off += vec;
+    L.scal = off; off += 256;
+    L.rhs_ws = off; off += align256(gp_ode_workspace_size(rows));
+    L.auto_ws = off; off += align256(gp_ode_auto_workspace_size(rows));
+    L.total = off;
+    return L;
+}
+
+// host resources of the status read, made once per thread (not per call)
+struct StatusReader {
+    int* pinned = nullptr;
+    hipEvent_t ev = nullptr;
+    int init() {
+        if (pinned) return 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&pinned), 64, hipHostMallocDefault) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
+        return 0;
+    }
+};
+thread_local StatusReader g_status;
+}  // namespace
+
+__global__ void f32_to_f64_kernel(const float* __restrict__ in, double* __restrict__ out, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (double)in[i];
+}
+
+extern "C" size_t gp_ode_sample_workspace_size(int rows) { return rows >= 1 ? ode_sample_layout(rows).total : 0; }
+
+extern "C" int gp_ode_sample(const gp_head_weights* w, const float* pobj, const float* x0, int rows, int k, double T0,
+                             double eps, int steps, double rtol, double atol, const float* pts_center, double* pose,
+                             double* q, int* nfev_out, int* status_out, void* workspace, size_t workspace_bytes,
+                             hipStream_t stream) {
+    GP_REQUIRE(w && pobj && x0 && pts_center && pose && q && workspace && rows >= 1 && k >= 1 && steps >= 0,
+               "ode_sample: bad arguments");
+    GP_REQUIRE(T0 != eps, "ode_sample: empty integration interval (T0 == eps)");
+    GP_REQUIRE(steps != 1, "ode_sample: steps must be 0 (t_eval unset) or >= 2");
+    const OdeSampleLayout L = ode_sample_layout(rows);
+    GP_REQUIRE(workspace_bytes >= L.total, "ode_sample: workspace too small (gp_ode_sample_workspace_size)");
+    GP_REQUIRE(g_status.init() == 0, "ode_sample: pinned status word / event");
+    char* ws = static_cast<char*>(workspace);
+    double* y[2] = {reinterpret_cast<double*>(ws + L.y[0]), reinterpret_cast<double*>(ws + L.y[1])};
+    double* K[ODE_NK];
+    for (int j = 0; j < ODE_NK; ++j) K[j] = reinterpret_cast<double*>(ws + L.k[j]);
+    double* f1 = reinterpret_cast<double*>(ws + L.f1);
+    double* dense = reinterpret_cast<double*>(ws + L.dense);
+    double* scal = reinterpret_cast<double*>(ws + L.scal);
+    void* rws = ws + L.rhs_ws;
+    void* aws = ws + L.auto_ws;
+    const size_t rws_b = gp_ode_workspace_size(rows), aws_b = gp_ode_auto_workspace_size(rows);
+    const long long n = (long long)rows * 9;
+    const double t0 = T0, tf = eps, dir = tf > t0 ? 1.0 : -1.0;
+    const double dscale = diff_scale();
+    int rc;
+    hipLaunchKernelGGL(f32_to_f64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x0, y[0], n);
+    if ((rc = gp_check_launch("f32_to_f64_kernel"))) return rc;
+
+    // ---- select_initial_step (scipy common.py), as genpose2_amd/ode.py initial_step
+    {   // f(t0): solve_ivp hands t0 as a Python float, so ode_func's g is float32 sigma * float64 scale
+        const float t32 = (float)t0;
+        const double g = (double)sigma32(t32) * dscale;
+        if ((rc = gp_ode_rhs(w, pobj, t32, sigma32(t32), -(0.5 * (g * g)), y[0], nullptr, nullptr, 0, 0.0, rows, k,
+                             K[0], rws, rws_b, stream)))
+            return rc;
+    }
+    if ((rc = gp_ode_init_norms(y[0], K[0], nullptr, n, atol, rtol, scal, stream))) return rc;
+    double hs[3];
+    GP_REQUIRE(hipMemcpyAsync(hs, scal, 2 * sizeof(double), hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                   hipStreamSynchronize(stream) == hipSuccess, "ode_sample: norm read");
+    const double d0 = hs[0], d1 = hs[1], interval = fabs(tf - t0);
+    double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+    h0 = fmin(h0, interval);
+    {   // f(t0 + h0 dir, y0 + h0 dir f0): a NumPy float64 time from here on
+        const double t = t0 + h0 * dir;
+        const double g = kSigMin * pow(kBase, t) * dscale;
+        const double a1 = 1.0;
+        const double* kin[1] = {K[0]};
+        if ((rc = gp_ode_rhs(w, pobj, (float)t, sigma32((float)t), -(0.5 * (g * g)), y[0], kin, &a1, 1, h0 * dir,
+                             rows, k, f1, rws, rws_b, stream)))
+            return rc;
+    }
+    if ((rc = gp_ode_init_norms(y[0], K[0], f1, n, atol, rtol, scal, stream))) return rc;
+    GP_REQUIRE(hipMemcpyAsync(hs + 2, scal + 2, sizeof(double), hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                   hipStreamSynchronize(stream) == hipSuccess, "ode_sample: norm read");
+    const double d2 = hs[2] / h0;
+    const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 1.0 / 5.0);
+    const double h_abs = fmin(fmin(100 * h0, h1), interval);
+
+    // ---- device-controlled attempts, one enqueued ahead of the status read
+    OdeCtl c0 = {};
+    c0.t = t0;
+    c0.h_abs = h_abs;
+    c0.nfev = 2;
+    for (int j = 0; j < ODE_NK; ++j) c0.kidx[j] = j;
+    GP_REQUIRE(hipMemcpyAsync(aws, &c0, sizeof(OdeCtl), hipMemcpyHostToDevice, stream) == hipSuccess &&
+                   hipStreamSynchronize(stream) == hipSuccess, "ode_sample: controller record");
+    auto launch = [&](int a, int what) {
+        return gp_ode_auto_attempt(w, pobj, a, what, tf, dir, rtol, atol, kSigMin, kBase, dscale, y[0], y[1], K,
+                                   kA6, kB6, kE7, rows, k, aws, aws_b, stream);
+    };
+    if ((rc = launch(0, 3))) return rc;
+    const int rec = (int)sizeof(OdeCtl);
+    const int stat_off = (int)offsetof(OdeCtl, status);
+    int a = 0;
+    for (;; ++a) {
+        GP_REQUIRE(a < 100000, "ode_sample: attempt limit reached");
+        if ((rc = launch(a + 1, 1))) return rc;   // decides attempt a, prepares a + 1
+        const char* src = static_cast<const char*>(aws) + ((a + 2) & 1) * rec + stat_off;
+        GP_REQUIRE(hipMemcpyAsync(g_status.pinned, src, 4, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                       hipEventRecord(g_status.ev, stream) == hipSuccess, "ode_sample: status read");
+        if ((rc = launch(a + 1, 2))) return rc;   // attempt a + 1 (a no-op once the solve has ended)
+        GP_REQUIRE(hipEventSynchronize(g_status.ev) == hipSuccess, "ode_sample: status wait");
+        if (*g_status.pinned != 0) break;
+    }
+    OdeCtl c;
+    GP_REQUIRE(hipMemcpyAsync(&c, static_cast<const char*>(aws) + ((a + 2) & 1) * rec, sizeof(OdeCtl),
+                              hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                   hipStreamSynchronize(stream) == hipSuccess, "ode_sample: final record");
+    if (status_out) *status_out = c.status;
+    if (nfev_out) *nfev_out = c.nfev;
+    GP_REQUIRE(!(c.status < 0 && steps > 0),
+               "ode_sample: RK45 failed (step size below the spacing of t) with t_eval set: the collected t_eval "
+               "outputs need the host controller (genpose2_amd/ode.py rk45_drive)");
+    const double* x = y[c.yi];
+    if (steps > 0 && c.status > 0) {   // res.y[:, -1]: the final step's dense output at t_eval[-1] = eps
+        const double* ks[ODE_NK];
+        for (int j = 0; j < ODE_NK; ++j) ks[j] = K[c.kidx[j]];
+        std::swap(ks[0], ks[ODE_NK - 1]);   // undo the FSAL swap of the accepted step
+        GP_REQUIRE(hipMemcpyAsync(scal + 7, &eps, sizeof(double), hipMemcpyHostToDevice, stream) == hipSuccess &&
+                       hipStreamSynchronize(stream) == hipSuccess, "ode_sample: t_eval");
+        if ((rc = gp_ode_dense(ks, kP74, y[c.yi ^ 1], scal + 7, 0, 1, 0, 0, c.t_old, c.t - c.t_old, n, dense, stream)))
+            return rc;
+        x = dense;
+    }
+    // ---- denoise (samplers.py:240-249) with eps's scalars: a float32 1-element tensor for g
+    const float te = (float)eps;
+    const float sig = sigma32(te);
+    const float g = sig * (float)dscale;
+    const float step = (float)((1.0 - eps) / (steps > 0 ? steps : 1000));
+    return gp_ode_denoise(w, pobj, te, sig, g * g, step, x, rows, k, pts_center, pose, q, rws, rws_b, stream);
 }

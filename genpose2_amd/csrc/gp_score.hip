@@ -395,6 +395,39 @@ static int pc_pick_nt(int rows, bool split) { return head_pick_nt(rows, split); 
 // the f16 planes) -- lets callers size their accounting from the kernel's real tiling.
 extern "C" int gp_pc_tile_rows(int rows, int split) { return 16 * pc_pick_nt(rows, split != 0); }
 
+// cond_pc_sampler's time grid and VE SDE scalars (samplers.py:129-130, sde.py:15-27) as float32 rows
+// {t, sigma(t), g(t), dt, sqrt(dt)} -- the table genpose2_amd/sde.py forms with torch, for hosts
+// without Python. t is torch.linspace(1, eps, T) in float32 as torch computes it on the CPU: step =
+// (eps - 1) / (T - 1) rounded once, t_i = 1 + step * i for i < T/2 and eps - step * (T - 1 - i) above,
+// each with a single rounding. sigma = f32(0.01) * 5000^t with the power correctly rounded (torch's
+// CPU pow is Sleef's 1-ulp vector routine: the two agree within 1 ulp, tests/test_cpu_host.py);
+// g = sigma * f32(sqrt(2 ln 5000)) in float32; dt = t_0 - t_1; sqrt(dt) correctly rounded (torch's
+// Sleef sqrt can be 1 ulp off it).
+extern "C" int gp_pc_step_table(int steps, float eps, float* out) {
+    GP_REQUIRE(out && steps >= 2, "pc_step_table: need steps >= 2 and an output of steps x 5 floats");
+    const float start = 1.0f, end = eps;
+    const float step = (end - start) / (float)(steps - 1);
+    const int half = steps / 2;
+    const float diff_scale = (float)sqrt(2.0 * (log(50.0) - log(0.01)));
+    float t0 = 0.f, t1 = 0.f;
+    for (int i = 0; i < steps; ++i) {
+        const float t = i < half ? fmaf(step, (float)i, start) : fmaf(-step, (float)(steps - 1 - i), end);
+        if (i == 0) t0 = t;
+        if (i == 1) t1 = t;
+        out[5 * i] = t;
+    }
+    const float dt = t0 - t1, sdt = sqrtf(t0 - t1);
+    for (int i = 0; i < steps; ++i) {
+        const float t = out[5 * i];
+        const float sig = 0.01f * (float)pow(5000.0, (double)t);
+        out[5 * i + 1] = sig;
+        out[5 * i + 2] = sig * diff_scale;
+        out[5 * i + 3] = dt;
+        out[5 * i + 4] = sdt;
+    }
+    return GP_OK;
+}
+
 extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const float* tproj, const float* step_tab,
                             int steps, float* x, int rows, int k, const float* pts_center, const float* z1,
                             const float* z2, uint64_t seed, float snr, float* res, float* q, float* xs,

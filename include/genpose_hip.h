@@ -195,6 +195,14 @@ int gp_pc_sample(const gp_head_weights *w, const float *pobj, const float *tproj
                  float snr, float *res, float *q, float *xs, void *workspace,
                  size_t workspace_bytes, hipStream_t stream);
 
+/* The step table of cond_pc_sampler (samplers.py:129-130, sde.py:15-27) for hosts without Python:
+ * out (HOST, steps x 5 fp32) = {t, sigma(t), g(t), dt, sqrt(dt)} with t = torch.linspace(1, eps,
+ * steps) in float32 (bit-identical to torch's CPU rounding), sigma = f32(0.01) * 5000^t (power
+ * correctly rounded; torch's Sleef pow is within 1 ulp of it, so sigma / g within 2 / 3 ulp of
+ * sde.py's), g = sigma * f32(sqrt(2 ln 5000)), dt, sqrt(dt) (correctly rounded, torch's within 1 ulp).
+ * Replaces genpose2_amd/sde.py pc_step_table; feeds gp_head_time_proj (column 0) and gp_pc_sample. */
+int gp_pc_step_table(int steps, float eps, float *out);
+
 /* Standard normals (Philox4x32-10 keyed by seed, counter {row, col/4, stream, 0x5EED}, Box-Muller)
  * -> out (rows, cols). The replacement of torch.randn_like in cond_pc_sampler (samplers.py:147,165):
  * gp_pc_sample with z1 = z2 = NULL draws step j's corrector / predictor noise as streams 2j / 2j+1
@@ -259,6 +267,22 @@ int gp_ode_auto_attempt(const gp_head_weights *w, const float *pobj, int n, int 
                         double *const *kslots, const double *tableau_a, const double *b,
                         const double *e, int rows, int k, void *workspace, size_t workspace_bytes,
                         hipStream_t stream);
+/* The whole ODE sampler in one call (cond_ode_sampler, samplers.py:180-258, with scipy solve_ivp
+ * RK45, samplers.py:226-234) for hosts without Python: x0 (R,9) fp32 device = the prior sample
+ * [+ init_x] at T0; select_initial_step on the host from two RHS norms, then device-controlled
+ * attempts (gp_ode_auto_attempt), the dense output at eps when steps > 0 (t_eval = linspace(T0, eps,
+ * steps); steps = 0: t_eval unset), the final denoise and epilogue (gp_ode_denoise) -> pose (R,9),
+ * q (R,7) fp64 device. HOST outs: nfev (scipy's count, including the two select_initial_step
+ * evaluations), status (1 done, -1 step size below the spacing of t: with steps > 0 that returns an
+ * error, since the t_eval outputs collected before the failure need the host controller).
+ * Workspace: gp_ode_sample_workspace_size(rows) bytes. Synchronises `stream` once per attempt (a
+ * 4-byte status read, one attempt kept enqueued ahead). Replaces genpose2_amd/ode.py rk45_device +
+ * PoseNet._ode (agent.py). */
+size_t gp_ode_sample_workspace_size(int rows);
+int gp_ode_sample(const gp_head_weights *w, const float *pobj, const float *x0, int rows, int k,
+                  double T0, double eps, int steps, double rtol, double atol,
+                  const float *pts_center, double *pose, double *q, int *nfev, int *status,
+                  void *workspace, size_t workspace_bytes, hipStream_t stream);
 /* Final denoise (samplers.py:240-249) + epilogue: grad = score(float(x), t32) fp32,
  * x + (0 - g2 * grad) * step (fp32 product, fp64 sum), GS of [:6], + pts_center, quaternion
  * (posenet_agent.py:554-556) -> pose (R,9) fp64, q (R,7) fp64. */

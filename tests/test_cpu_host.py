@@ -443,3 +443,28 @@ def test_bench_launcher_starts_world2_gloo():
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert line == {"launch_probe": True, "n_gpus": 2, "rank_sum": 1}
+
+
+def test_c_pc_step_table_matches_sde_table():
+    """gp_pc_step_table (the C host's table) against genpose2_amd/sde.py (torch, the reference's own
+    arithmetic): t and dt bit-identical for every T in 2..1500; sqrt(dt) within 1 ulp and sigma, g within 3
+    ulp (torch's CPU pow and sqrt are Sleef's 1-ulp vector routines, the C table's are correctly rounded;
+    sigma = 0.01 * pow scales pow's 1-ulp difference into up to 2 ulp of sigma, and g rounds once more)."""
+    import ctypes
+    from genpose2_amd import _lib, sde
+    lib = _lib.load()
+    worst, n_diff, n = {1: 0, 2: 0, 4: 0}, 0, 0
+    for T in list(range(2, 1501)) + [2000, 5000]:
+        tab = np.zeros((T, 5), np.float32)
+        _lib.check(lib.gp_pc_step_table(T, ctypes.c_float(1e-5), tab.ctypes.data_as(ctypes.c_void_p)))
+        ref = sde.pc_step_table(T)
+        for c in (0, 3):
+            np.testing.assert_array_equal(tab[:, c], ref[:, c], err_msg=f"T={T} column {c}")
+        for c in (1, 2, 4):
+            ulp = np.abs(tab[:, c].view(np.int32).astype(np.int64) - ref[:, c].view(np.int32).astype(np.int64))
+            worst[c] = max(worst[c], int(ulp.max()))
+            n_diff += int((ulp > 0).sum())
+        n += 3 * T
+    assert worst[1] <= 3 and worst[2] <= 3 and worst[4] <= 1, worst
+    print(f"sigma/g/sqrt(dt) entries differing: {n_diff} of {n}, worst ulp {worst}")
+    assert lib.gp_pc_step_table(1, ctypes.c_float(1e-5), None) != 0

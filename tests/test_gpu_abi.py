@@ -103,3 +103,125 @@ def test_weights_pack_scale_handle():
         assert torch.equal(out, ref)
     finally:
         lib.gp_weights_free(h)
+
+
+def _handle_features(lib, h, pts, B, N, s):
+    from genpose2_amd import _lib
+    tab = _lib.c_int64_p()
+    wbuf = lib.gp_weights_encoder(h, ctypes.byref(tab))
+    ws = torch.empty(int(lib.gp_encoder_workspace_size(B, N)), dtype=torch.uint8, device=DEV)
+    feat = torch.empty(B, 1024, device=DEV)
+    _lib.check(lib.gp_encoder_forward(ctypes.c_void_p(wbuf), tab, _vp(pts), B, N, _vp(ws), ws.numel(), _vp(feat), s))
+    hw = lib.gp_weights_heads(h)
+    pobj = torch.empty(B, 768, device=DEV)
+    _lib.check(lib.gp_head_object_proj(hw, _vp(feat), B, _vp(pobj), s))
+    return hw, pobj
+
+
+def test_c_host_pc_sampler_with_c_step_table():
+    """The PC sampler driven with nothing from genpose2_amd's Python (sde.py, PoseNet): gp_weights_pack,
+    encoder, gp_pc_step_table, gp_head_time_proj, gp_pc_sample -- against the reference's own
+    golden_pc_k10_t100 at the golden tolerances (rotation 1e-4 absolute, translation 1e-5 relative)."""
+    from conftest import golden
+    from genpose2_amd import _lib, weights
+    g = golden("pc_k10_t100")
+    K, T = int(g["K"]), int(g["T"])
+    lib, h = _pack(0, weights.synthetic_state_dict("score"))
+    try:
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        pts, center = torch.from_numpy(g["pts"]).to(DEV), torch.from_numpy(g["pts_center"]).to(DEV)
+        B = pts.shape[0]
+        hw, pobj = _handle_features(lib, h, pts, B, 1024, s)
+        tab = np.zeros((T, 5), np.float32)
+        _lib.check(lib.gp_pc_step_table(T, ctypes.c_float(1e-5), tab.ctypes.data_as(ctypes.c_void_p)))
+        tvals = torch.from_numpy(np.ascontiguousarray(tab[:, 0])).to(DEV)
+        tproj = torch.empty(T, 768, device=DEV)
+        _lib.check(lib.gp_head_time_proj(hw, _vp(tvals), T, _vp(tproj), s))
+        R = B * K
+        x = (torch.from_numpy(g["prior"]).to(DEV) * np.float32(0.01 * 5000.0 ** 1.0)).contiguous()   # sde.py:30-34
+        z1, z2 = torch.from_numpy(g["z1"]).to(DEV), torch.from_numpy(g["z2"]).to(DEV)
+        res, q = torch.empty(R, 9, device=DEV), torch.empty(R, 7, device=DEV)
+        pws = torch.empty(int(lib.gp_pc_workspace_size(R)), dtype=torch.uint8, device=DEV)
+        _lib.check(lib.gp_pc_sample(hw, _vp(pobj), _vp(tproj), tab.ctypes.data_as(ctypes.c_void_p), T, _vp(x), R, K,
+                                    _vp(center), _vp(z1), _vp(z2), ctypes.c_uint64(0), ctypes.c_float(0.16),
+                                    _vp(res), _vp(q), None, _vp(pws), pws.numel(), s), "pc_sample")
+        torch.cuda.synchronize()
+        p, ref = res.view(B, K, 9).cpu().numpy(), g["pred_pose"]
+        assert np.abs(p[..., :6] - ref[..., :6]).max() < 1e-4
+        assert np.abs(p[..., 6:] - ref[..., 6:]).max() / np.abs(ref[..., 6:]).max() < 1e-5
+    finally:
+        lib.gp_weights_free(h)
+
+
+def _c_ode(lib, hw, pobj, prior, T0, steps, K, center, s):
+    from genpose2_amd import _lib
+    R = prior.shape[0]
+    x0 = (torch.from_numpy(prior).to(DEV) * (0.01 * 5000.0 ** T0)).contiguous()   # prior(sigma(T0)), sde.py:30-34
+    pose = torch.empty(R, 9, dtype=torch.float64, device=DEV)
+    q = torch.empty(R, 7, dtype=torch.float64, device=DEV)
+    ws = torch.empty(int(lib.gp_ode_sample_workspace_size(R)), dtype=torch.uint8, device=DEV)
+    nfev, status = ctypes.c_int(0), ctypes.c_int(0)
+    _lib.check(lib.gp_ode_sample(hw, _vp(pobj), _vp(x0), R, K, T0, 1e-5, steps, 1e-5, 1e-5, _vp(center), _vp(pose),
+                                 _vp(q), ctypes.byref(nfev), ctypes.byref(status), _vp(ws), ws.numel(), s), "ode_sample")
+    torch.cuda.synchronize()
+    return pose.cpu().numpy(), q.cpu().numpy(), nfev.value, status.value
+
+
+@pytest.mark.parametrize("tag,rot_tol,tr_rel,same_nfev", [("t055_s20", 1e-4, 1e-5, True),
+                                                         ("t1_none", 5e-4, 1e-4, False)])
+def test_c_host_ode_sample_vs_golden(tag, rot_tol, tr_rel, same_nfev):
+    """gp_ode_sample (select_initial_step + device-controlled RK45 + dense output + denoise in one C
+    call) against the reference's golden_ode at the golden tolerances of test_ode_pred_func_vs_golden:
+    nfev identical at T0=0.55; from T0=1 (sigma = 50) the adaptive controller may take a different
+    accept/reject path on last-bit differences (as the oracle, which runs scipy itself, does), so there
+    nfev is only held within 5 % and the poses at 5e-4 / 1e-4."""
+    from conftest import golden
+    from genpose2_amd import weights
+    g = golden("ode")
+    steps = int(g[f"{tag}_steps"])
+    lib, h = _pack(0, weights.synthetic_state_dict("score"))
+    try:
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        pts = torch.from_numpy(g[f"{tag}_pts"]).to(DEV)
+        center = torch.from_numpy(g[f"{tag}_pts_center"]).to(DEV)
+        B = pts.shape[0]
+        hw, pobj = _handle_features(lib, h, pts, B, 1024, s)
+        pose, q, nfev, status = _c_ode(lib, hw, pobj, g[f"{tag}_prior"], float(g[f"{tag}_T0"]), max(steps, 0), 5,
+                                       center, s)
+        ref = g[f"{tag}_pred_pose"].reshape(-1, 9)
+        print(tag, "nfev", nfev, "reference", int(g[f"{tag}_nfev"]))
+        assert status == 1
+        assert nfev == int(g[f"{tag}_nfev"]) if same_nfev else abs(nfev - int(g[f"{tag}_nfev"])) <= 0.05 * nfev
+        assert np.abs(pose[:, :6] - ref[:, :6]).max() < rot_tol
+        assert np.abs(pose[:, 6:] - ref[:, 6:]).max() / np.abs(ref[:, 6:]).max() < tr_rel
+    finally:
+        lib.gp_weights_free(h)
+
+
+def test_c_host_ode_sample_large_rows():
+    """gp_ode_sample at R = 4800 (ode_r4800, the shipped T0=0.55): nfev identical to the reference's,
+    the calibrated bar against its float64 run, and equal to PoseNet's ODE path to 1e-9."""
+    import large_noise
+    from conftest import golden
+    from genpose2_amd import weights
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    name = "ode_r4800"
+    gl = golden(f"large_{name}")
+    _, _, B, K, _, T0, _ = large_noise.CASES[name]
+    pts_np, center_np, prior, _, _ = large_noise.inputs(name)
+    lib, h = _pack(0, weights.synthetic_state_dict("score"))
+    try:
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        pts, center = torch.from_numpy(pts_np).to(DEV), torch.from_numpy(center_np).to(DEV)
+        hw, pobj = _handle_features(lib, h, pts, B, 1024, s)
+        pose, q, nfev, status = _c_ode(lib, hw, pobj, prior, T0, 0, K, center, s)
+    finally:
+        lib.gp_weights_free(h)
+    assert status == 1 and nfev == int(gl["nfev"])
+    large_noise.check_calibrated(pose.reshape(B, K, 9), gl)
+    agent = PoseNet(GenPoseConfig(device=DEV, sampler_mode=["ode"], sampling_steps=None)).eval()
+    agent.noise_feed = NoiseFeed(torch.from_numpy(prior))
+    ppose, _ = agent.pred_func({"pts": pts, "pts_center": center}, repeat_num=K, T0=T0)
+    assert agent.last_nfev == nfev
+    assert np.abs(ppose.cpu().numpy().reshape(-1, 9) - pose).max() < 1e-9
