@@ -109,8 +109,10 @@ def cpu_info():
 
 
 def cpu_threads_default():
-    """All physical cores this process may use, capped by the OMP_NUM_THREADS allotment when set (the
-    GPU box exports OMP_NUM_THREADS=16: one GPU's share of the host)."""
+    """All physical cores this process may use, capped by the OMP_NUM_THREADS allotment when set. The GPU
+    box exports OMP_NUM_THREADS=16: its 128 physical cores serve 8 GPUs, and a one-GPU job's fair share
+    is 16 of them, so the baseline runs on that share rather than on cores other jobs on the host hold
+    (--cpu-threads overrides)."""
     _, phys, avail = cpu_info()
     n = min(phys, avail)
     env = os.environ.get("OMP_NUM_THREADS")
@@ -177,15 +179,32 @@ def cpu_baseline(cfg, config_id, threads, sample_objects, reps=3):
                                    "sample_16_objects_value": c["sample_16_objects"]["value"],
                                    "threads": c["threads"], "source": os.path.relpath(chk, REPO)}
     # the oracle/reference time ratio measured in the build container on identical
-    # inputs (oracle/calibrate_cpu.py); converts the port figure to reference terms
+    # inputs (oracle/calibrate_cpu.py). It is a different thread count from this run's (the build
+    # container has 8 CPUs; the reference cannot run on the GPU host), so it is reported beside the
+    # port's rate, not applied to it.
     for cal in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "cpu_calibration.json")), reverse=True):
         with open(cal) as f:
             c = json.load(f)
-        out["calibration"] = {"oracle_over_reference": round(c["oracle_over_reference"], 3),
-                              "threads": c["threads"], "source": os.path.relpath(cal, REPO)}
-        out["reference_equivalent_value"] = out["value"] * c["oracle_over_reference"]
+        out["calibration_note"] = {"oracle_over_reference_time": round(c["oracle_over_reference"], 3),
+                                   "threads": c["threads"], "source": os.path.relpath(cal, REPO),
+                                   "applied": False}
         break
     return out
+
+
+def load_rocprof(kernel_prefix):
+    """Mean duration of the dominant kernel from the newest committed rocprofv3 --stats summary of a bench
+    run (profiles/r*/config4*_kernel_stats.csv), or None."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "config4*_kernel_stats.csv")),
+                   key=lambda f: (int(os.path.basename(os.path.dirname(f))[1:] or 0), os.path.getmtime(f)))
+    import csv
+    for fn in reversed(files):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row["Name"].startswith(kernel_prefix):
+                    return {"avg_launch_us": float(row["AverageNs"]) / 1e3, "calls": int(row["Calls"]),
+                            "source": os.path.relpath(fn, REPO)}
+    return None
 
 
 def load_traffic(rows, split, tile):
@@ -203,6 +222,11 @@ def load_traffic(rows, split, tile):
         if d.get("rows") == rows and (", true>" in k) == bool(split) and k.startswith(f"void pc_step_kernel<{tile // 16},"):
             return d.get("hbm_bytes_per_launch")
     return None
+
+
+def _tile_rows(rows, split):
+    from genpose2_amd import _lib
+    return _lib.load().gp_pc_tile_rows(rows, int(split))
 
 
 def report_ode(args, B, N, K, ws, rank, elapsed, nfevs, cfgd):
@@ -291,6 +315,9 @@ def main():
                     help="1: encode batch k+1 on a side stream while batch k samples (every timed step "
                          "still encodes and samples one batch; the first encode is not overlapped). "
                          "Off by default: no gain measured (profiles/r1/ab_encoder_pipeline.txt)")
+    ap.add_argument("--f32-steps", type=int, default=2,
+                    help="PC runs: also time this many steps with every GEMM in exact fp32 (heads and encoders; "
+                         "GENPOSE2_HEAD_ARITH=f32 / GENPOSE2_ENC_ARITH=f32) and report them under 'f32_exact' (0: off)")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     # device_count() does not initialise the GPU on this image, so starting a launcher after it is safe
@@ -439,20 +466,56 @@ def main():
             dist.destroy_process_group()
         return
     ode_info = time_ode_calls(args, cfg, data0, B, K, ws, dev) if args.ode_calls > 0 else None
+    split = score.heads.arith == "split_f16"
+    f32_info = None
+    if args.f32_steps > 0 and split:
+        # the same steps with every GEMM in exact fp32 (the arithmetic the reference runs)
+        agents = [a for a in (score, energy) if a is not None]
+        for a in agents:
+            a.heads.set_arith("f32")
+            if hasattr(a.encoder, "set_arith"):
+                a.encoder.set_arith("f32")
+        n_ev = len(samp_ev)
+        one_step(last=True)
+        torch.cuda.synchronize(dev)
+        if ws > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.f32_steps):
+            one_step(record=True, last=True)
+        torch.cuda.synchronize(dev)
+        if ws > 1:
+            dist.barrier()
+        el32 = time.perf_counter() - t1
+        if ws > 1:
+            t = torch.tensor([el32], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el32 = float(t.item())
+        ms32 = float(np.mean([a.elapsed_time(b) for a, b in samp_ev[n_ev:]]))
+        del samp_ev[n_ev:]
+        for a in agents:
+            a.heads.set_arith("split_f16")
+            if hasattr(a.encoder, "set_arith"):
+                a.encoder.set_arith("split_f16")
+        us32 = ms32 / 1e3 / (T + 1) * 1e6
+        fl = B * K * arch.score_flops_per_candidate_step()
+        f32_info = {"value": B * K * T * ws * args.f32_steps / el32, "unit": "pose-candidate-steps/s",
+                    "steps": args.f32_steps, "ms_per_step": el32 / args.f32_steps * 1e3,
+                    "pc_step_avg_launch_us": us32, "achieved_tflops": fl / us32 / 1e6,
+                    "frac_of_fp32_mfma_peak": fl / us32 / 1e6 / FP32_PEAK_TFLOPS,
+                    "kernel": f"pc_step_kernel<{int(_tile_rows(B * K, False)) // 16}, ..., false>"}
     units = B * K * T * ws * args.steps
     samp_ms = float(np.mean([a.elapsed_time(b) for a, b in samp_ev]))
     per_launch_s = samp_ms / 1e3 / (T + 1)
     flop_launch = B * K * arch.score_flops_per_candidate_step()
     achieved = flop_launch / per_launch_s / 1e12
-    split = score.heads.arith == "split_f16"
     # split-f16: the two per-candidate GEMMs run 3 f16 MFMA products per fp32 MAC, so their MFMA
     # ceiling in algorithmic (fp32) FLOP/s is the dense f16 peak / 3
     peak = F16_PEAK_TFLOPS / 3 if split else FP32_PEAK_TFLOPS
     up = score.heads.up.t
     wg_bytes = sum(up[k].numel() * up[k].element_size() for k in
                    (("pe2_h", "h1p_h") if split else ("pe2_w", "h1p_w")))   # streamed per workgroup per step
-    from genpose2_amd import _lib
-    tile = int(_lib.load().gp_pc_tile_rows(B * K, int(split)))   # the kernel's real tile width
+    tile = int(_tile_rows(B * K, split))   # the kernel's real tile width
     nwg = -(-B * K // tile)
     if rank == 0:
         out = {
@@ -487,6 +550,13 @@ def main():
                                               "GBps_per_CU": wg_bytes / per_launch_s / 1e9,
                                               "TBps_chip": wg_bytes * nwg / per_launch_s / 1e12}},
         }
+        rp = load_rocprof(f"void pc_step_kernel<{tile // 16}, 8, {'true' if split else 'false'}>")
+        if rp is not None:   # the committed rocprofv3 --stats of a bench run: its mean launch, same FLOPs
+            rp["achieved"] = flop_launch / (rp["avg_launch_us"] * 1e-6) / 1e12
+            rp["frac"] = rp["achieved"] / peak
+            out["roofline"]["rocprof"] = rp
+        if f32_info is not None:
+            out["f32_exact"] = f32_info
         if ode_info is not None:
             out["ode"] = ode_info
         if not args.no_cpu_baseline and args.dino == "none":
