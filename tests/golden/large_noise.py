@@ -73,3 +73,22 @@ def check_calibrated(pose: np.ndarray, g, factor: float = 2.0) -> dict:
 
 
 check_pc_calibrated = check_calibrated
+
+
+def check_ode(pose: np.ndarray, g) -> dict:
+    """Parity bar of the large ODE fixtures: the north-star bar against the reference's fp32 run (rotation
+    1e-4 absolute, translation 1e-5 relative to max |t|) and rotation within 1e-4 of its float64 run too.
+    The calibrated 2x bar of check_calibrated does not carry over: RK45's step sizes are continuous
+    functions of its error norms, so any last-bit change in the right-hand side (a different summation
+    order anywhere in the score net) moves the whole step sequence -- with the same nfev -- and the
+    solution by up to the solver's tolerance scale (rtol = atol = 1e-5). The reference's fp32 and
+    float64 runs share their step sequence, which is why they sit closer to each other (4.7e-5 max at
+    R=12,800, 8.4e-6 at R=4,800) than two independently rounded fp32 runs do. Returns the statistics."""
+    ref64 = g["pred_pose64"]
+    ours = rotation_error_stats(pose, ref64)
+    refs = rotation_error_stats(g["pred_pose"], ref64)
+    vs32 = rotation_error_stats(pose, g["pred_pose"])
+    p = np.asarray(pose, np.float64)
+    t_rel = float(np.abs(p[..., 6:] - g["pred_pose"][..., 6:]).max() / np.abs(g["pred_pose"][..., 6:]).max())
+    assert vs32["max"] < 1e-4 and ours["max"] < 1e-4 and t_rel < 1e-5, (vs32, ours, t_rel)
+    return {"ours_vs_ref32": vs32, "ours_vs_ref64": ours, "ref32_vs_ref64": refs, "trans_rel_vs_ref32": t_rel}

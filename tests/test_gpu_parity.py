@@ -289,9 +289,9 @@ def test_pc_large_rows_vs_reference(name, arith):
 @pytest.mark.parametrize("name", ["ode_r4800", "ode_r12800"])
 def test_ode_large_rows_vs_reference(name, arith):
     """The shipped ODE setting (T0=0.55, RK45) at R = 4800 / 12,800 against the reference: identical
-    nfev; rotation against the float64 reference within 2x the reference fp32's own error
-    (check_calibrated: 9.3e-5 max at R=12,800); translation within 1e-5 relative. `arith` sets both
-    the head GEMMs and the encoder's levels 2-3."""
+    nfev; rotation within the north-star 1e-4 of both the reference's fp32 run and its float64 run,
+    translation within 1e-5 relative (large_noise.check_ode, which says why RK45 solutions differ at
+    the solver's tolerance scale). `arith` sets both the head GEMMs and the encoder's levels 2-3."""
     import large_noise
     from genpose2_amd.agent import NoiseFeed, PoseNet
     from genpose2_amd.config import GenPoseConfig
@@ -306,9 +306,7 @@ def test_ode_large_rows_vs_reference(name, arith):
     pose, q = agent.pred_func(data, repeat_num=K, T0=T0)
     p = pose.cpu().numpy()
     assert agent.last_nfev == int(g["nfev"])
-    stats = large_noise.check_calibrated(p, g)
-    print(name, arith, stats, "vs ref32 max", float(np.abs(p[..., :6] - g["pred_pose"][..., :6]).max()))
-    assert rel(p[..., 6:], g["pred_pose"][..., 6:]) < 1e-5
+    print(name, arith, large_noise.check_ode(p, g))
 
 
 # ---------------------------------------------------------------- ODE sampler
