@@ -309,8 +309,8 @@ def main():
                          "ms/step, but beside the sampler its workgroups hold CUs at ~45 of the 501 PC-step "
                          "launches per step (up to 1.1 ms each; profiles/r2/energy_overlap_ab.json)")
     ap.add_argument("--dino", choices=["none", "pointwise"], default="none",
-                    help="pointwise: the DINO-pointwise fused encoder (Pointnet2ClsMSGFus) for the score and energy "
-                         "models, fed synthetic per-point image features (B, N, 384) resident in HBM")
+                    help="pointwise: the DINO-pointwise path for the score and energy models (ImgEncoder over synthetic "
+                         "DINOv3 layers (B, 256, 384) x 3, patch gather at synthetic roi pixels, Pointnet2ClsMSGFus)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: encode batch k+1 on a side stream while batch k samples (every timed step "
                          "still encodes and samples one batch; the first encode is not overlapped). "
@@ -353,9 +353,12 @@ def main():
             broadcast_weights(a, ws)
     pts, center = synthetic.make_batch(args.config, B, N, first_object=rank * B)
     data0 = {"pts": torch.from_numpy(pts).to(dev), "pts_center": torch.from_numpy(center).to(dev)}
-    if args.dino == "pointwise":   # per-point DINOv3 features (posenet.py:136-197 output), synthetic
-        rgb = np.random.Generator(np.random.PCG64(4242 + rank)).standard_normal((B, N, 384), dtype=np.float32)
-        data0["point_rgb_feat"] = torch.from_numpy(rgb).to(dev)
+    if args.dino == "pointwise":   # the DINOv3 backbone's layers [2, 6, 11] and roi pixels, synthetic
+        rng = np.random.Generator(np.random.PCG64(4242 + rank))
+        data0["dino_layers"] = [torch.from_numpy(rng.standard_normal((B, 256, 384), dtype=np.float32)).to(dev)
+                                for _ in range(3)]
+        data0["roi_xs"] = torch.from_numpy(rng.integers(0, 224, size=(B, N)).astype(np.int32)).to(dev)
+        data0["roi_ys"] = torch.from_numpy(rng.integers(0, 224, size=(B, N)).astype(np.int32)).to(dev)
 
     stream = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(device=dev)
@@ -385,7 +388,7 @@ def main():
         if energy is not None:
             # the energy encoder needs only the points: overlap it with the score sampler
             # (as genpose2_amd.runner.EvaluationPipeline does)
-            edata = {k: data0[k] for k in ("pts", "pts_center", "point_rgb_feat") if k in data0}
+            edata = {k: data0[k] for k in ("pts", "pts_center", "dino_layers", "roi_xs", "roi_ys") if k in data0}
 
             def start_energy_encoder():
                 side.wait_stream(stream)

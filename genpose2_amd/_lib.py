@@ -98,6 +98,13 @@ _SIGS: Dict[str, tuple] = {
     "gp_ode_sample": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_int, c_int, c_double, c_double,
                               c_int, c_double, c_double, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int), c_void_p, c_size_t, c_void_p]),
+    "gp_img_encoder_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "gp_img_encoder": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
+                               c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_size_t, c_void_p]),
+    "gp_img_geo_table": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "gp_gather_patch_points": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                       c_void_p, c_void_p]),
     "gp_scale_forward": (c_int, [ctypes.POINTER(ScaleWeights), c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "gp_randn": (c_int, [c_uint64, ctypes.c_uint32, c_int, c_int, c_void_p, c_void_p]),
     "gp_points_mean": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -53,6 +53,10 @@ class PoseNet:
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(self.cfg.noise_seed)
         self.weights_source = f"synthetic(seed={self.cfg.seed})"
+        # --dino pointwise: the frozen DINOv3 backbone (posenet.py:56-62) is not part of this build; a caller
+        # that has it sets it here (an object with the reference's get_intermediate_layers), or passes its
+        # output as data["dino_layers"]
+        self.dino = None
         self._build(weights.synthetic_state_dict(self.weights_kind, seed=self.cfg.seed))
 
     @property
@@ -67,16 +71,18 @@ class PoseNet:
     # ------------------------------------------------------------------ model construction
     def _build(self, sd: weights.StateDict) -> None:
         if self.pointwise:
-            # a --dino pointwise checkpoint also holds the frozen DINOv3 backbone and the ImgEncoder
-            # (posenet.py:56-69); they produce data["point_rgb_feat"] upstream of this path
-            sd = {k: v for k, v in sd.items() if not k.startswith(("dino.", "img_encoder."))}
+            # a --dino pointwise checkpoint also holds the frozen DINOv3 backbone (posenet.py:56-62): its
+            # intermediate layers are this path's input (data["dino_layers"], or self.dino)
+            sd = {k: v for k, v in sd.items() if not k.startswith("dino.")}
         weights.check_keys(sd, self.weights_kind)
         self.state_dict = sd
         self._pc_cache = {}                        # T -> (step table, tproj) of these weights
         if self.cfg.agent_type in ("score", "energy"):
             if self.pointwise:
                 from .fus_encoder import FusEncoderModel
+                from .img_encoder import ImgEncoderModel
                 self.encoder = FusEncoderModel(sd, self.device)
+                self.img_encoder = ImgEncoderModel(sd, self.device)
             else:
                 self.encoder = dev.EncoderModel(sd, self.device)
             self.heads = dev.HeadModel(sd, self.device)
@@ -122,14 +128,28 @@ class PoseNet:
             self._pc_cache[T] = c
         return c
 
+    def dino_layers(self, data):
+        """The DINOv3 intermediate layers of posenet.py:138-144: data["dino_layers"] (three (B, 256, 384)
+        tensors), or self.dino.get_intermediate_layers(roi_rgb, ...) when a backbone is set."""
+        layers = data.get("dino_layers")
+        if layers is not None:
+            return layers
+        if self.dino is None or data.get("roi_rgb") is None:
+            raise KeyError("dino 'pointwise' needs data['dino_layers'] (the DINOv3 backbone's intermediate layers "
+                           "[2, 6, 11], three (B, 256, 384) tensors) or a backbone in PoseNet.dino with data['roi_rgb']")
+        return self.dino.get_intermediate_layers(data["roi_rgb"], n=list(arch.IMG_LAYERS), reshape=False, norm=True,
+                                                 return_class_token=False)
+
     def _encode(self, data) -> torch.Tensor:
         if self.pointwise:
-            # posenet.py:136-197 gathers DINOv3 patch features at each point; that stage (and its weights)
-            # is upstream of this path: the caller supplies its output
-            if data.get("point_rgb_feat") is None:
-                raise KeyError("dino 'pointwise' needs data['point_rgb_feat'] (B, N, 384): the per-point DINOv3 "
-                               "features of posenet.py:136-197")
-            return self.encoder.forward(data["pts"], data["point_rgb_feat"])
+            # posenet.py:136-197: ImgEncoder over the backbone's layers, the patch -> point gather at
+            # roi_xs / roi_ys, then Pointnet2ClsMSGFus over [pts | rgb_feat]. data["point_rgb_feat"]
+            # (B, N, 384) skips the image branch with per-point features computed elsewhere.
+            rgb = data.get("point_rgb_feat")
+            if rgb is None:
+                feat = self.img_encoder.forward(self.dino_layers(data))
+                rgb = self.img_encoder.gather(feat, data["roi_xs"], data["roi_ys"])
+            return self.encoder.forward(data["pts"], rgb)
         return self.encoder.forward(data["pts"])
 
     @torch.no_grad()

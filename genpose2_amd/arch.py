@@ -80,6 +80,15 @@ FUS_REDUCTION = 4         # GatedAttentionFusion reduction_ratio
 FUS_SPATIAL_K = 7         # spatial attention Conv1d(2, 1, 7, padding=3)
 LN_EPS = 1e-5             # nn.LayerNorm default
 
+# ImgEncoder(dino_dim=384, num_patches=256, patch_size=16) over DINOv3's intermediate layers [2, 6, 11]
+# (posenet.py:64, :137-143; networks/img_encoder/img_encoder.py) and the patch -> point gather
+# pos = (roi_xs // 14) * 16 + roi_ys // 14, clamped (posenet.py:146-192)
+IMG_PATCHES = 256
+IMG_GRID = 16                         # h = w = sqrt(num_patches)
+IMG_LAYERS = (2, 6, 11)               # get_intermediate_layers(n=[2, 6, 11], norm=True)
+IMG_PATCH_PX = 14                     # roi_xs // 14, roi_ys // 14
+IMG_REL_EMB = (2 * (IMG_GRID - 1)) ** 2   # nn.Embedding(max_rel * max_rel, dim // 4): 900 rows
+
 
 def fus_sa_branches() -> List[List[SABranch]]:
     """sa_branches() with the 384 image-feature channels entering level 0 (pointnet2.py:281-285:

@@ -59,8 +59,9 @@ class GenPoseConfig:
         if self.pose_mode != "rot_matrix" or self.regression_head != "Rx_Ry_and_T":
             raise NotImplementedError("only pose_mode=rot_matrix / Rx_Ry_and_T are built")
         if self.dino not in ("none", "pointwise"):
-            raise NotImplementedError("dino 'global' needs the DINOv3 backbone (out of scope); 'pointwise' takes "
-                                      "the per-point features as data['point_rgb_feat']")
+            raise NotImplementedError("dino 'global' needs the DINOv3 backbone's global head (out of scope); "
+                                      "'pointwise' takes the backbone's intermediate layers as data['dino_layers'] "
+                                      "(or a backbone in PoseNet.dino)")
         if self.pts_encoder != "pointnet2" or self.pointnet2_params != "light":
             raise NotImplementedError("only pointnet2 'light' encoder is built")
         if self.sampler_mode[0] not in ("pc", "ode"):

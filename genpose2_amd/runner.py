@@ -59,7 +59,9 @@ class EvaluationPipeline:
             main = torch.cuda.current_stream(batch["pts"].device)
             if self._side is None:
                 self._side = torch.cuda.Stream(device=batch["pts"].device)
-            edata = {"pts": batch["pts"], "pts_center": batch["pts_center"]}
+            # the energy encoder's inputs: the points, and for --dino pointwise the image branch's
+            edata = {k: batch[k] for k in ("pts", "pts_center", "roi_rgb", "roi_xs", "roi_ys", "dino_layers",
+                                           "point_rgb_feat") if k in batch}
 
             def start_energy_encoder():   # after the score encoder, beside the sampler
                 self._side.wait_stream(main)
@@ -134,7 +136,9 @@ class ShardedEvaluationPipeline:
         lo, hi = shard.shard_range(total, dist.get_world_size(), dist.get_rank())
         K = self.local.cfg.eval_repeat_num
         if hi > lo:
-            out = self.local.run({k: v[lo:hi] for k, v in batch.items()})
+            # per-object tensors, and lists of them (the DINOv3 layers of --dino pointwise)
+            out = self.local.run({k: [t[lo:hi] for t in v] if isinstance(v, (list, tuple)) else v[lo:hi]
+                                  for k, v in batch.items()})
         else:   # more ranks than objects: an empty shard still joins the gathers
             d = batch["pts"].device
             z = lambda *s: torch.zeros(s, dtype=torch.float32, device=d)  # noqa: E731

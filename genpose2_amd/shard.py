@@ -43,7 +43,7 @@ def broadcast_packed(tensors: Iterable[torch.Tensor], tables: Iterable[np.ndarra
     broadcast_tensors(tensors, src)
     out = []
     for tab in tables:
-        t = torch.from_numpy(np.ascontiguousarray(tab, np.int64).copy())
+        t = torch.from_numpy(np.ascontiguousarray(tab).copy())
         if device is not None:
             t = t.to(device)
         dist.broadcast(t, src=src)
@@ -55,7 +55,11 @@ def model_tables(agent) -> List[np.ndarray]:
     """Host-side weight-derived state of an agent (the encoder's layer table), in a fixed order --
     the same order as ``packed_host_tables``."""
     enc = getattr(agent, "encoder", None)
-    return [enc.table] if enc is not None else []
+    out = [enc.table] if enc is not None else []
+    img = getattr(agent, "img_encoder", None) if getattr(agent, "pointwise", False) else None
+    if img is not None:
+        out.append(img.table)          # ImgEncoder host scalars (layer_attn.2 bias, the two branch gates)
+    return out
 
 
 def broadcast_agent(agent, src: int = 0) -> None:
@@ -66,6 +70,8 @@ def broadcast_agent(agent, src: int = 0) -> None:
     tabs = broadcast_packed(model_tensors(agent), model_tables(agent), src, dev_)
     if tabs:
         agent.encoder.set_table(tabs[0])
+    if len(tabs) > 1:
+        agent.img_encoder.set_table(tabs[1])
     agent._pc_cache = {}
 
 
@@ -76,7 +82,8 @@ def packed_host_tables(kind: str, sd) -> List[np.ndarray]:
         return []
     if kind.endswith("_pointwise"):
         from . import arch
-        return [pack.pack_encoder(sd, arch.fus_sa_branches())[1]]
+        from .img_encoder import pack_img_scalars
+        return [pack.pack_encoder(sd, arch.fus_sa_branches())[1], pack_img_scalars(sd)]
     return [pack.pack_encoder(sd)[1]]
 
 
@@ -88,6 +95,7 @@ def model_tensors(agent) -> List[torch.Tensor]:
         out.append(agent.encoder.wbuf)
         if hasattr(agent.encoder, "t"):      # fused encoder (--dino pointwise): transformer / fusion blocks
             out += [agent.encoder.t[k] for k in sorted(agent.encoder.t)]
+            out += [agent.img_encoder.t[k] for k in sorted(agent.img_encoder.t)]   # and the ImgEncoder
         out += [agent.heads.up.t[k] for k in sorted(agent.heads.up.t)]
     if getattr(agent, "scale", None) is not None:
         out += [agent.scale.up.t[k] for k in sorted(agent.scale.up.t)]
@@ -105,9 +113,11 @@ def packed_host_tensors(kind: str, sd) -> List[torch.Tensor]:
     if kind.endswith("_pointwise"):
         from . import arch
         from .fus_encoder import pack_fus_blocks
+        from .img_encoder import pack_img_encoder
         f = pack_fus_blocks(sd)
+        im = pack_img_encoder(sd)
         enc = [torch.from_numpy(pack.pack_encoder(sd, arch.fus_sa_branches())[0])] + \
-            [torch.from_numpy(f[k]) for k in sorted(f)]
+            [torch.from_numpy(f[k]) for k in sorted(f)] + [torch.from_numpy(im[k]) for k in sorted(im)]
     else:
         enc = [torch.from_numpy(pack.pack_encoder(sd)[0])]
     return enc + [torch.from_numpy(np.ascontiguousarray(p[k])) for k in sorted(p)]

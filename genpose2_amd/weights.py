@@ -83,14 +83,30 @@ def fus_encoder_manifest() -> List[Tuple[str, Tuple[int, ...], str]]:
     return out
 
 
+def img_encoder_manifest() -> List[Tuple[str, Tuple[int, ...], str]]:
+    """ImgEncoder(384, 256, 16) (networks/img_encoder/img_encoder.py:7-46), the --dino pointwise model's
+    image branch between the DINOv3 backbone and the patch -> point gather: layer attention
+    Linear(d, d/2) -> ReLU -> Linear(d/2, 1), the relative-position embedding (900, d/4) of the geometric
+    attention, the 3x3 edge conv (d/4, d, 3, 3), and the two branch weights (nn.Parameter 0.2 / 0.1)."""
+    d = arch.DINO_DIM
+    p = "img_encoder"
+    return [(f"{p}.layer_attn.0.weight", (d // 2, d), "linear"), (f"{p}.layer_attn.0.bias", (d // 2,), f"linear_bias:{d}"),
+            (f"{p}.layer_attn.2.weight", (1, d // 2), "linear"), (f"{p}.layer_attn.2.bias", (1,), f"linear_bias:{d // 2}"),
+            (f"{p}.rel_pos_emb.weight", (arch.IMG_REL_EMB, d // 4), "embedding"),
+            (f"{p}.edge_guide.0.weight", (d // 4, d, 3, 3), "conv1d"),
+            (f"{p}.edge_guide.0.bias", (d // 4,), f"linear_bias:{d * 9}"),
+            (f"{p}.geo_weight", (), "const:0.2"), (f"{p}.edge_weight", (), "const:0.1")]
+
+
 def manifest(kind: str) -> List[Tuple[str, Tuple[int, ...], str]]:
     """(key, shape, init rule) for every tensor of the model selected by ``kind``.
-    ``*_pointwise``: the --dino pointwise model's point-cloud path (Pointnet2ClsMSGFus encoder + the
-    same heads; the DINOv3 backbone and ImgEncoder that produce the per-point features are not part
-    of it)."""
+    ``*_pointwise``: the --dino pointwise model (Pointnet2ClsMSGFus encoder, ImgEncoder, the same heads;
+    the frozen DINOv3 backbone ahead of the ImgEncoder is not part of it: its weights are absent,
+    SURVEY §8c)."""
     out: List[Tuple[str, Tuple[int, ...], str]] = []
     if kind in ("score", "energy", "score_pointwise", "energy_pointwise"):
-        out += fus_encoder_manifest() if kind.endswith("_pointwise") else _sa_manifest(arch.sa_branches())
+        out += fus_encoder_manifest() + img_encoder_manifest() if kind.endswith("_pointwise") \
+            else _sa_manifest(arch.sa_branches())
         n = "pose_score_net"
         out += [(f"{n}.pose_encoder.0.weight", (arch.POSE_HID, arch.POSE_DIM), "linear"),
                 (f"{n}.pose_encoder.0.bias", (arch.POSE_HID,), "linear_bias:9"),
@@ -144,6 +160,10 @@ def _draw(rng: np.random.Generator, shape, rule: str) -> np.ndarray:
         return rng.uniform(-0.02, 0.02, size=shape)
     if rule == "bn_var":
         return rng.uniform(0.5, 1.5, size=shape)
+    if rule == "embedding":       # nn.Embedding default: N(0, 1)
+        return rng.normal(0.0, 1.0, size=shape)
+    if rule.startswith("const:"):  # nn.Parameter(torch.tensor(v))
+        return np.full(shape, float(rule.split(":")[1]))
     if rule == "gfp":             # GaussianFourierProjection: randn(64) * 30 (scorenet.py:84)
         return rng.normal(0.0, 1.0, size=shape) * arch.GFP_SCALE
     raise ValueError(rule)

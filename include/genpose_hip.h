@@ -291,6 +291,32 @@ int gp_ode_denoise(const gp_head_weights *w, const float *pobj, float t32, float
                    double *pose, double *q, void *workspace, size_t workspace_bytes,
                    hipStream_t stream);
 
+/* ===================================================================== ImgEncoder (--dino pointwise)
+ * ImgEncoder.forward (networks/img_encoder/img_encoder.py:48-100) over the three DINOv3 intermediate
+ * layers l0, l1, l2 (b, np, d), patch-major as get_intermediate_layers(n=[2, 6, 11], norm=True) returns
+ * them (np = g*g patches, d = 384): layer attention (la_w1 (d/2, d), la_b1, la_w2 (d/2), la_b2 a host
+ * scalar), geometric attention with the (np, np) position table geo_table (gp_img_geo_table), the 3x3
+ * edge conv (conv_w (d/4, d, 3, 3) as stored, conv_b), and the final mix with geo_gate =
+ * relu(geo_weight), edge_gate = relu(edge_weight) (host scalars) -> out (b, np, d). Optional outputs
+ * (NULL to skip): layer_w (b*np, 3) layer-attention weights, edge_out (b, d/4) edge weights.
+ * Workspace: gp_img_encoder_workspace_size(b, np, d) bytes. */
+size_t gp_img_encoder_workspace_size(int b, int np, int d);
+int gp_img_encoder(const float *l0, const float *l1, const float *l2, int b, int np, int d,
+                   const float *la_w1, const float *la_b1, const float *la_w2, float la_b2,
+                   const float *geo_table, const float *conv_w, const float *conv_b, float geo_gate,
+                   float edge_gate, float *out, float *layer_w, float *edge_out, void *workspace,
+                   size_t workspace_bytes, hipStream_t stream);
+/* HOST: the geometric attention's position table rel_pos_emb(rel_pos_idx).sum(-1) (img_encoder.py:
+ * 68-76): table[i][j] = sum_k E[clamp((r_j - r_i + g - 1)(2g - 1) + (c_j - c_i + g - 1), 0, num_emb - 1)][k]
+ * for patches i, j at (row, col) = (p / g, p % g). rel_pos_emb (num_emb, edim) host -> table (g^2, g^2)
+ * host (the sum runs in order; torch's vector sum may differ from it in the last bit). */
+int gp_img_geo_table(const float *rel_pos_emb, int num_emb, int edim, int grid, float *table);
+/* The patch -> point gather of GFObjectPose.extract_pts_feature (posenet.py:146-192): out[b][i] =
+ * feat[b][clamp((xs[b][i] // patch_px) * grid + ys[b][i] // patch_px, 0, np - 1)] (floor division;
+ * the reference's patch_px = 14, grid = 16). feat (b, np, d), xs/ys (b, n) int32 -> out (b, n, d). */
+int gp_gather_patch_points(const float *feat, int b, int np, int d, const int *xs, const int *ys, int n,
+                           int patch_px, int grid, float *out, hipStream_t stream);
+
 /* ===================================================================== ScaleNet
  * ScaleNet.forward (scalenet.py:33-49): axes (b,3,3), pts_feat (b,1024) -> length (b,3). */
 typedef struct {

@@ -666,3 +666,49 @@ def fus_encoder_forward(sd, pts: np.ndarray, rgb_feat: np.ndarray, return_levels
             xyz = new_xyz
     out = feats[:, :, 0]
     return (out, levels) if return_levels else out
+
+
+# ============================================================ ImgEncoder + patch gather (--dino pointwise)
+def img_geo_bias(sd, prefix: str = "img_encoder", grid: int = arch.IMG_GRID) -> np.ndarray:
+    """rel_pos_emb(rel_pos_idx).sum(-1) of ImgEncoder.forward (img_encoder.py:68-76, rel_coords :18-34):
+    (np, np) with [i][j] = sum_d E[clamp((c_j - c_i + h - 1) . (2h - 1, 1), 0, 899)][d], c_p = (p // h, p % h)."""
+    import torch
+    h = grid
+    coords = np.stack(np.meshgrid(np.arange(h), np.arange(h), indexing="ij"), -1).reshape(-1, 2)
+    rel = coords[None, :, :] - coords[:, None, :] + (h - 1)
+    E = torch.from_numpy(np.ascontiguousarray(sd[f"{prefix}.rel_pos_emb.weight"], dtype=F32))
+    idx = np.clip(rel[..., 0] * (2 * (h - 1) + 1) + rel[..., 1], 0, E.shape[0] - 1)
+    return E.sum(dim=-1).numpy()[idx]
+
+
+def img_encoder_forward(sd, layers, prefix: str = "img_encoder", return_parts: bool = False):
+    """ImgEncoder.forward (networks/img_encoder/img_encoder.py:48-100), eval: three (B, np, d) DINOv3
+    intermediate layers -> (B, np, d): layer attention (softmax over the 3 layers), geometric attention
+    (G G^T x the position table, softmax, . fused), 3x3 edge conv -> ReLU -> mean, final mix."""
+    import torch
+    import torch.nn.functional as tf
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(sd[f"{prefix}.{k}"], dtype=F32))  # noqa: E731
+    f = torch.stack([torch.from_numpy(np.ascontiguousarray(v, dtype=F32)) for v in layers], 1)   # (B, 3, np, d)
+    B, _, n, d = f.shape
+    h = int(round(n ** 0.5))
+    s = tf.linear(torch.relu(tf.linear(f, t("layer_attn.0.weight"), t("layer_attn.0.bias"))),
+                  t("layer_attn.2.weight"), t("layer_attn.2.bias"))                           # (B, 3, np, 1)
+    w = torch.softmax(s, dim=1)
+    fused = (f * w).sum(dim=1)                                                               # (B, np, d)
+    g = fused[:, :, d // 4:]
+    attn = torch.softmax(torch.matmul(g, g.transpose(1, 2)) * torch.from_numpy(img_geo_bias(sd, prefix, h)), dim=-1)
+    geo = torch.matmul(attn, fused)
+    sp = fused.transpose(1, 2).reshape(B, d, h, h)
+    edge = torch.relu(tf.conv2d(sp, t("edge_guide.0.weight"), t("edge_guide.0.bias"), padding=1)).mean(dim=(2, 3))
+    final = fused + torch.relu(t("geo_weight")) * geo + torch.relu(t("edge_weight")) * (fused * edge.repeat(1, 4)[:, None, :])
+    if return_parts:
+        return final.numpy(), {"layer_w": w[..., 0].numpy(), "edge": edge.numpy(), "fused": fused.numpy()}
+    return final.numpy()
+
+
+def gather_patch_points(feat: np.ndarray, xs: np.ndarray, ys: np.ndarray, patch_px: int = arch.IMG_PATCH_PX,
+                        grid: int = arch.IMG_GRID) -> np.ndarray:
+    """posenet.py:146-192: pos = (roi_xs // 14) * 16 + roi_ys // 14 (floor division), clamped to the patch
+    range, then torch.gather along the patch axis: (B, np, d) -> (B, N, d)."""
+    pos = np.clip((np.asarray(xs) // patch_px) * grid + np.asarray(ys) // patch_px, 0, feat.shape[1] - 1)
+    return np.take_along_axis(feat, pos[..., None].astype(np.int64), 1)

@@ -240,3 +240,87 @@ def test_pointwise_agent_pred_func():
     assert rel(got[:, 6:], res[:, 6:]) < 1e-5
     with pytest.raises(KeyError):
         agent.pred_func({"pts": data["pts"], "pts_center": data["pts_center"]}, repeat_num=K)
+
+
+# ---------------------------------------------------------------- ImgEncoder + patch gather
+@pytest.mark.parametrize("tag", ["hard", "soft"])
+def test_img_encoder_vs_reference_golden(tag):
+    """gp_img_encoder against the reference's own ImgEncoder (golden_img.npz, make_golden_img.py): the final
+    (B, 256, 384) features, the layer-attention weights and the edge weights within 1e-5 of max|ref|; the
+    patch -> point gather (roi pixels out of range included) bit-exact against the gathered golden rows
+    and against numpy's take_along_axis of our own features."""
+    import make_golden_img as mi
+    from genpose2_amd import weights
+    from genpose2_amd.img_encoder import ImgEncoderModel
+    g = golden("img")
+    B, scale, seed = mi.CASES[tag]
+    model = ImgEncoderModel(weights.synthetic_state_dict("score_pointwise", seed=0), torch.device(DEV))
+    layers = [torch.from_numpy(v).to(DEV) for v in mi.dino_layers(B, scale, seed)]
+    final, parts = model.forward(layers, return_parts=True)
+    f = final.cpu().numpy()
+    errs = {"final0": rel(f[0], g[f"{tag}_final0"]), "edge": rel(parts["edge"].cpu().numpy(), g[f"{tag}_edge"]),
+            "layer_w": rel(parts["layer_w"].cpu().numpy().transpose(0, 2, 1), g[f"{tag}_layer_w"]),
+            "sum": float(np.abs(f.astype(np.float64).sum(axis=(1, 2)) - g[f"{tag}_final_sum"]).max()
+                         / np.abs(g[f"{tag}_final_sum"]).max())}
+    print(tag, errs)
+    assert max(errs.values()) < 1e-5, errs
+    xs, ys = mi.roi_pixels(B, 1024, seed)
+    got = model.gather(final, torch.from_numpy(xs), torch.from_numpy(ys)).cpu().numpy()
+    pos = np.clip((xs // 14) * 16 + ys // 14, 0, 255)
+    np.testing.assert_array_equal(got, np.take_along_axis(f, pos[..., None], 1))
+    assert rel(got[0, :64], g[f"{tag}_gather0"]) < 1e-5
+
+
+class _Backbone:
+    def __init__(self, layers):
+        self.layers = layers
+        self.calls = 0
+
+    def get_intermediate_layers(self, x, n, reshape, norm, return_class_token):
+        assert list(n) == [2, 6, 11] and not reshape and norm and not return_class_token
+        self.calls += 1
+        return tuple(v[: x.shape[0]] for v in self.layers)
+
+
+def test_pointwise_pred_func_end_to_end_vs_reference():
+    """PoseNet(dino='pointwise').pred_func with the reference's keys (pts, pts_center, roi_xs, roi_ys, and the
+    DINOv3 backbone's layers) against the reference's own pred_func run end to end (golden_img.npz e2e_*:
+    ImgEncoder -> gather -> Pointnet2ClsMSGFus -> heads -> PC sampler, injected noise; the backbone replaced
+    by fixed layers on both sides): pts_feat within 1e-5, rotation 1e-4, translation 1e-5 relative. The
+    same call through a backbone object set on PoseNet.dino with roi_rgb gives the identical result."""
+    import make_golden_img as mi
+    from genpose2_amd import synthetic
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("img")
+    e = mi.E2E
+    B, N, K, T = e["B"], e["N"], e["K"], e["T"]
+    pts, _ = synthetic.make_batch(e["cid"], B, N)
+    xs, ys = mi.roi_pixels(B, N, e["seed"])
+    layers = [torch.from_numpy(v).to(DEV) for v in mi.dino_layers(B, e["scale"], e["seed"])]
+    agent = PoseNet(GenPoseConfig(device=DEV, sampling_steps=T, dino="pointwise")).eval()
+    base = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(g["e2e_pts_center"]).to(DEV),
+            "roi_xs": torch.from_numpy(xs), "roi_ys": torch.from_numpy(ys)}
+    outs = []
+    for how in ("layers", "backbone"):
+        agent.noise_feed = NoiseFeed(*(torch.from_numpy(g[k]) for k in ("e2e_prior", "e2e_z1", "e2e_z2")))
+        data = dict(base)
+        if how == "layers":
+            data["dino_layers"] = layers
+        else:
+            agent.dino = _Backbone(layers)
+            data["roi_rgb"] = torch.zeros(B, 3, 224, 224, device=DEV)
+        pose, q = agent.pred_func(data, repeat_num=K)
+        outs.append((data["pts_feat"].clone(), pose.clone()))
+        assert data["rgb_feat"] is None
+    assert agent.dino.calls == 1
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    feat, pose = outs[0][0].cpu().numpy(), outs[0][1].cpu().numpy()
+    ref = g["e2e_pred_pose"]
+    print("e2e: pts_feat", rel(feat, g["e2e_pts_feat"]), "rotation", np.abs(pose[..., :6] - ref[..., :6]).max())
+    assert rel(feat, g["e2e_pts_feat"]) < 1e-5
+    assert np.abs(pose[..., :6] - ref[..., :6]).max() < 1e-4
+    assert rel(pose[..., 6:], ref[..., 6:]) < 1e-5
+    agent.dino = None
+    with pytest.raises(KeyError):
+        agent.pred_func(dict(base), repeat_num=K)

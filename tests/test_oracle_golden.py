@@ -207,3 +207,23 @@ def test_energy_rank_aggregate_r12800_subset(energy_sd):
         agg = oracle.aggregate_pose(pose, e, clustering=c)
         assert np.abs(agg[:, :3, :3] - agg_ref[:n, :3, :3]).max() < 1e-5
         assert rel(agg[:, :3, 3], agg_ref[:n, :3, 3]) < 1e-5
+
+
+def test_img_encoder_and_gather_vs_reference():
+    """ImgEncoder (img_encoder.py:48-100) and the patch -> point gather (posenet.py:146-192) restated in the
+    oracle, against the reference's own outputs (golden_img.npz, tests/golden/make_golden_img.py):
+    near-one-hot ("hard") and spread ("soft") geometric attention, out-of-range roi pixels clamped."""
+    import make_golden_img as mi
+    from genpose2_amd import weights
+    g = golden("img")
+    sd = weights.synthetic_state_dict("score_pointwise", seed=0)
+    for tag, (B, scale, seed) in mi.CASES.items():
+        layers = mi.dino_layers(B, scale, seed)
+        final, parts = oracle.img_encoder_forward(sd, layers, return_parts=True)
+        assert rel(final[0], g[f"{tag}_final0"]) < 1e-5, tag
+        np.testing.assert_allclose(final.astype(np.float64).sum(axis=(1, 2)), g[f"{tag}_final_sum"], rtol=1e-5)
+        assert rel(parts["edge"], g[f"{tag}_edge"]) < 1e-5
+        assert rel(parts["layer_w"], g[f"{tag}_layer_w"]) < 1e-5
+        xs, ys = mi.roi_pixels(B, 1024, seed)
+        gathered = oracle.gather_patch_points(final, xs, ys)
+        assert rel(gathered[0, :64], g[f"{tag}_gather0"]) < 1e-5
