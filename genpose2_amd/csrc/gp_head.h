@@ -674,6 +674,7 @@ __device__ __forceinline__ float dot_chains(const float* __restrict__ W, size_t 
     float p[CH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) p[j] = 0.f;
+#pragma unroll 1
     for (int c0 = 0; c0 < N; c0 += CH) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) p[j] = fmaf(W[(size_t)(c0 + j) * stride], x[c0 + j], p[j]);

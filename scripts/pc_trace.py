@@ -70,6 +70,11 @@ def main():
     out["gap_prev_end_to_start_cycles"] = float(tr[:, :, 0].min() - prev[:, :, 8].max())
     out["gap_per_xcd"] = [float(tr[x::8, :, 0].min() - prev[x::8, :, 8].max()) for x in range(8)]
     out["launch_span_cycles"] = float(tr[:, :, 8].max() - tr[:, :, 0].min())
+    full = buf.reshape(2, 256, 8, 16)[(T - 1) & 1, :nwg, :, :].astype(np.int64)
+    for nm, (a, b) in {"pe0: exponents": (1, 13), "pe0: init loads issued": (13, 14), "pe0: compute+lds": (14, 15),
+                       "pe0: barrier": (15, 2)}.items():
+        if full[..., b].any():
+            out.setdefault("pe0_sub_cycles_mean", {})[nm] = float((full[..., b] - full[..., a]).mean())
     print(json.dumps(out, indent=1))
 
 
