@@ -4,8 +4,8 @@
 //   * residual + LayerNorm (TransformerBlockWithRelativePE, attention.py:505-533);
 //   * the relative-PE bias of EfficientRelativePositionalEncoding (attention.py:680-735), all 8 heads of
 //     a point pair from one evaluation of its distance / direction MLPs;
-//   * biased multi-head attention (MultiheadAttentionWithRelativePE, attention.py:436-488) with the
-//     head's K and V staged in LDS and torch's two-pass softmax order (max, then exp / sum);
+//   * biased multi-head attention (MultiheadAttentionWithRelativePE, attention.py:436-488), flash-style:
+//     QK^T and PV on exact-fp32 MFMA, K / V staged in LDS, an online softmax;
 //   * GatedAttentionFusion's channel / spatial attention and gating (attention.py:284-325).
 // Token tensors are point-major (b, n, C): the reference's (b, C, n) transposed, so one token's channels
 // are contiguous and every linear is a row-major GEMM over b*n rows.
@@ -343,71 +343,138 @@ extern "C" int gp_relpe_bias(const float* pe, const float* xyz, int b, int n, fl
 }
 
 // ============================================================================ biased attention
-// Workgroup = (QPW queries, head, object); LPQ lanes per query, each holding HD/LPQ channels of q and of
-// the output (LPQ = 1 for head dims <= 32: no cross-lane sum per key). The head's K and V (n x hd) are
-// staged in LDS; all queries of a wave read the same key row (broadcast). The bias is key-major, so
-// for each key the wave's queries read consecutive floats. Softmax as torch evaluates it: pass 1 the
-// row max of s = q.k / sqrt(hd) + bias, pass 2 p = exp(s - max), sum p and sum p v; out = sum p v / sum.
-// (q.k / sqrt(hd) is taken as q.k * (1 / sqrt(hd)): within an ulp of torch's division.)
-template <int HD, int LPQ>
+// Flash-style on exact-fp32 MFMA (v_mfma_f32_16x16x4_f32). Workgroup = 64 queries (4 waves x 16) of one
+// (object, head); a wave keeps its 16 queries' Q^T fragments and O^T accumulators in registers and walks
+// the keys in LDS chunks of KC (K row-major, V transposed), 64 keys per softmax block:
+//   S^T = K Q^T          A = K rows (keys), B = Q^T: the D tile holds keys 4q + r of query l & 15 -- which is
+//                        exactly the B-operand layout of the next product, so P never leaves registers;
+//   s = S^T / sqrt(hd) + bias (key-major bias: 16 consecutive queries per key per load), keys >= n masked;
+//   online softmax per query: m' = max(m, block max), O *= exp(m - m'), l = l exp(m - m') + sum exp(s - m');
+//   O^T += V^T P^T       A = V^T (dims x keys, from the transposed LDS copy), B = P^T.
+// out = O / l. Head dims are zero-padded to a multiple of 16 (12 -> 16). The grid is 1-D and XCD-aware:
+// the query blocks of one (object, head) land on one XCD, so its K / V are read into one L2.
+// (q.k / sqrt(hd) is taken as q.k * (1 / sqrt(hd)): within an ulp of torch's division. The softmax is
+// torch's result up to rounding: the online rescaling replaces its two passes.)
+__device__ __forceinline__ float rows_max(float v) {   // max over lanes l, l^16, l^32, l^48
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+}
+
+template <int HDP>
 __global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restrict__ qkv,
-                                                          const float* __restrict__ bias, int n, int d,
-                                                          float* __restrict__ out) {
-#pragma clang fp contract(off)
-    constexpr int HL = HD / LPQ;                  // channels per lane
-    constexpr int QPW = FUS_THREADS / LPQ;        // queries per workgroup
-    static_assert(HL % 4 == 0 || HL == 12 || HL == 3, "float4 slices");
-    extern __shared__ __attribute__((aligned(16))) float kv[];
-    float* sk = kv;
-    float* sv = kv + (size_t)n * HD;
-    const int h = blockIdx.y, b = blockIdx.z;
+                                                          const float* __restrict__ bias, int n, int d, int hd,
+                                                          int nqb, float* __restrict__ out) {
+    constexpr int NG = HDP / 16;      // 16-deep k-groups of S, 16-row dim tiles of O
+    constexpr int KC = 4096 / HDP;    // keys per LDS chunk (37 KB at every head dim)
+    constexpr int KS = HDP + 4;       // K row stride (floats)
+    constexpr int VS = KC + 4;        // V^T row stride
+    __shared__ __attribute__((aligned(16))) float ks[KC * KS];
+    __shared__ __attribute__((aligned(16))) float vt[HDP * VS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int qg = lane >> 4, nl = lane & 15;
+    const int G = gridDim.x;                                   // a multiple of 8 (8 heads)
+    const int t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+    const int qb = t % nqb, hb = t / nqb, h = hb & (FUS_HEADS - 1), b = hb / FUS_HEADS;
     const size_t ld = 3 * (size_t)d;
     const float* base = qkv + (size_t)b * n * ld;
-    for (int e = threadIdx.x; e < n * (HD / 4); e += FUS_THREADS) {
-        const int j = e / (HD / 4), c4 = e - j * (HD / 4);
-        st4(sk + (size_t)j * HD + 4 * c4, ld4(base + (size_t)j * ld + d + h * HD + 4 * c4));
-        st4(sv + (size_t)j * HD + 4 * c4, ld4(base + (size_t)j * ld + 2 * d + h * HD + 4 * c4));
-    }
-    __syncthreads();
-    const int part = LPQ > 1 ? (threadIdx.x & (LPQ - 1)) : 0;
-    const int i = blockIdx.x * QPW + threadIdx.x / LPQ;
+    const int i = qb * 64 + wid * 16 + nl;
     const int ii = i < n ? i : n - 1;
-    float qv[HL], o[HL];
-    const float* qp = base + (size_t)ii * ld + h * HD + part * HL;
+    f32x4 qf[NG], o[NG];
 #pragma unroll
-    for (int c = 0; c < HL; ++c) {
-        qv[c] = qp[c];
-        o[c] = 0.f;
+    for (int g = 0; g < NG; ++g) {
+        const int c = 16 * g + 4 * qg;
+        qf[g] = c < hd ? ld4(base + (size_t)ii * ld + h * hd + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        o[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const float inv = 1.0f / sqrtf((float)HD);
-    const float* bcol = bias ? bias + ((size_t)b * FUS_HEADS + h) * n * n + ii : nullptr;   // + j * n
-    auto score = [&](int j) {
-        const float* kr = sk + (size_t)j * HD + part * HL;
-        float s = 0.f;
-#pragma unroll
-        for (int c = 0; c < HL; ++c) s += qv[c] * kr[c];
-        if constexpr (LPQ == 4) {   // quad sum (lanes 4t..4t+3), the same order in every lane
-            s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
-            s = s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
+    const float inv = 1.0f / sqrtf((float)hd);
+    const float* bcol = bias ? bias + ((size_t)b * FUS_HEADS + h) * n * n + ii : nullptr;   // + key * n
+    float m = -INFINITY, lsum = 0.f;
+    for (int c0 = 0; c0 < n; c0 += KC) {
+        const int kn = min(KC, n - c0), k16 = (kn + 15) & ~15;
+        __syncthreads();
+        for (int e = threadIdx.x; e < k16 * (HDP / 4); e += FUS_THREADS) {
+            const int j = e / (HDP / 4), c = 4 * (e - j * (HDP / 4));
+            f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+            if (j < kn && c < hd) {
+                const float* row = base + (size_t)(c0 + j) * ld + h * hd + c;
+                kv = ld4(row + d);
+                vv = ld4(row + 2 * d);
+            }
+            st4(ks + j * KS + c, kv);
+            vt[(c + 0) * VS + j] = vv.x;
+            vt[(c + 1) * VS + j] = vv.y;
+            vt[(c + 2) * VS + j] = vv.z;
+            vt[(c + 3) * VS + j] = vv.w;
         }
-        s = s * inv;
-        return bcol ? s + bcol[(size_t)j * n] : s;
-    };
-    float mx = -INFINITY;
-    for (int j = 0; j < n; ++j) mx = fmaxf(mx, score(j));
-    float l = 0.f;
-    for (int j = 0; j < n; ++j) {
-        const float p = expf(score(j) - mx);
-        l += p;
-        const float* vr = sv + (size_t)j * HD + part * HL;
+        __syncthreads();
+        for (int kb = 0; kb < k16; kb += 64) {
+            const int nt = min(4, (k16 - kb) >> 4);
+            f32x4 s[4], bv[4];
 #pragma unroll
-        for (int c = 0; c < HL; ++c) o[c] += p * vr[c];
+            for (int u = 0; u < 4; ++u) {      // bias loads first: their latency hides under the S MFMAs
+                bv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (bcol && u < nt) {
+                    const int j0 = c0 + kb + 16 * u + 4 * qg;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (j0 + r < n) bv[u][r] = bcol[(size_t)(j0 + r) * n];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (u < nt) {
+                    const float* kr = ks + (kb + 16 * u + nl) * KS + 4 * qg;
+#pragma unroll
+                    for (int g = 0; g < NG; ++g) s[u] = mfma_kgroup(ld4(kr + 16 * g), qf[g], s[u]);
+                }
+            }
+            float bmax = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j0 = c0 + kb + 16 * u + 4 * qg;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v;
+                    {
+#pragma clang fp contract(off)
+                        v = s[u][r] * inv + bv[u][r];
+                    }
+                    s[u][r] = (u < nt && j0 + r < n) ? v : -INFINITY;
+                    bmax = fmaxf(bmax, s[u][r]);
+                }
+            }
+            const float mn = fmaxf(m, rows_max(bmax));
+            const float alpha = expf(m - mn);
+            m = mn;
+            float ps = 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    s[u][r] = expf(s[u][r] - mn);
+                    ps += s[u][r];
+                }
+            lsum = lsum * alpha + ps;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) o[g] *= alpha;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (u < nt) {
+                    const float* vr = vt + nl * VS + kb + 16 * u + 4 * qg;
+#pragma unroll
+                    for (int g = 0; g < NG; ++g) o[g] = mfma_kgroup(ld4(vr + 16 * g * VS), s[u], o[g]);
+                }
+        }
     }
+    const float rl = 1.0f / rows_sum(lsum);
     if (i < n) {
-        float* op = out + ((size_t)b * n + i) * d + h * HD + part * HL;
-        const float rl = 1.0f / l;
+        float* op = out + ((size_t)b * n + i) * d + h * hd;
 #pragma unroll
-        for (int c = 0; c < HL; ++c) op[c] = o[c] * rl;
+        for (int g = 0; g < NG; ++g)
+            if (16 * g + 4 * qg < hd) st4(op + 16 * g + 4 * qg, o[g] * rl);
     }
 }
 
@@ -417,18 +484,15 @@ extern "C" int gp_mha_attention(const float* qkv, const float* bias, int b, int 
     GP_REQUIRE(((uintptr_t)qkv | (uintptr_t)out) % 16 == 0, "mha_attention: pointers must be 16-byte aligned");
     if (!b) return GP_OK;
     const int hd = d / FUS_HEADS;
-    const size_t lds = sizeof(float) * 2 * (size_t)n * hd;
-    GP_REQUIRE(lds <= 64 * 1024, "mha_attention: K/V of a head (%zu bytes) exceed 64 KiB", lds);
-#define GP_MHA(HD, LPQ)                                                                                    \
-    hipLaunchKernelGGL((mha_kernel<HD, LPQ>), dim3((n + FUS_THREADS / LPQ - 1) / (FUS_THREADS / LPQ), FUS_HEADS, b), \
-                       dim3(FUS_THREADS), lds, st, qkv, bias, n, d, out)
-    switch (hd) {
-        case 12: GP_MHA(12, 1); break;
-        case 32: GP_MHA(32, 1); break;
-        case 64: GP_MHA(64, 4); break;
-        case 128: GP_MHA(128, 4); break;
-        default: gp_set_error("mha_attention: head dim %d not in {12, 32, 64, 128}", hd); return GP_ERR_UNSUPPORTED;
-    }
+    const int nqb = (n + 63) / 64;
+    GP_REQUIRE((long long)nqb * FUS_HEADS * b < (1LL << 31), "mha_attention: grid too large");
+    const dim3 grid((unsigned)(nqb * FUS_HEADS * b));
+#define GP_MHA(HDP) hipLaunchKernelGGL((mha_kernel<HDP>), grid, dim3(FUS_THREADS), 0, st, qkv, bias, n, d, hd, nqb, out)
+    if (hd <= 16) GP_MHA(16);
+    else if (hd <= 32) GP_MHA(32);
+    else if (hd <= 64) GP_MHA(64);
+    else if (hd <= 128) GP_MHA(128);
+    else { gp_set_error("mha_attention: head dim %d > 128", hd); return GP_ERR_UNSUPPORTED; }
 #undef GP_MHA
     return gp_check_launch("mha_kernel");
 }

@@ -31,10 +31,14 @@ def main():
     pts_np, _ = synthetic.make_batch(4, B, 1024)
     pts = torch.from_numpy(pts_np).to(dev)
     rgb = torch.from_numpy(np.random.Generator(np.random.PCG64(1)).standard_normal((B, 1024, 384), dtype=np.float32)).to(dev)
-    light = EncoderModel(weights.synthetic_state_dict("score"), dev)
-    fus = FusEncoderModel(weights.synthetic_state_dict("score_pointwise"), dev)
-    out = {"B": B, "light_ms": timed(lambda: light.forward(pts), reps),
-           "fus_ms": timed(lambda: fus.forward(pts, rgb), reps)}
+    which = sys.argv[3] if len(sys.argv) > 3 else "both"
+    out = {"B": B}
+    if which in ("both", "light"):
+        light = EncoderModel(weights.synthetic_state_dict("score"), dev)
+        out["light_ms"] = timed(lambda: light.forward(pts), reps)
+    if which in ("both", "fus"):
+        fus = FusEncoderModel(weights.synthetic_state_dict("score_pointwise"), dev)
+        out["fus_ms"] = timed(lambda: fus.forward(pts, rgb), reps)
     print(json.dumps(out), flush=True)
 
 

@@ -8,6 +8,7 @@
 #   bench[:ARGS]     python bench.py ARGS (comma-separated, e.g. bench:--config,5,--steps,2)
 #   prof[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS (--steps 3 --warmup 1 by default)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS
+#   kprof:SCRIPT[:ARGS] rocprofv3 --kernel-trace --stats of python3 SCRIPT ARGS
 #   pmc[:ARGS]       scripts/pmc_passes.sh over scripts/pmc_target.py ARGS
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -33,6 +34,9 @@ for step in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o k -- python3 bench.py "${A[@]}" > $out.log 2>&1 ;;
     py)
       s=${A[0]}; timeout -k 10 600 python -u $s "${A[@]:1}" > $out.out 2> $out.err ;;
+    kprof)
+      s=${A[0]}; rm -rf $out
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o k -- python3 $s "${A[@]:1}" > $out.log 2>&1 ;;
     pmc)
       bash scripts/pmc_passes.sh $out "${A[@]}" > $out.log 2>&1 ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
