@@ -528,87 +528,128 @@ extern "C" int gp_interp_points(const float* x, int b, int n_in, int c, int n_ou
     return gp_check_launch("interp_points_kernel");
 }
 
-// One workgroup per object: channel attention (AdaptiveAvgPool1d -> Conv1d -> ReLU -> Conv1d -> sigmoid)
-// of [cur | ot], spatial attention (sigmoid(Conv1d(2,1,7,pad 3)) over [max_c cur ; mean_c cur]), and
-// gcat = [cur | (ot * ca) * sp].
-__global__ __launch_bounds__(FUS_THREADS) void fusion_attend_kernel(const float* __restrict__ cur,
-                                                                    const float* __restrict__ ot, int n, int c,
-                                                                    const float* __restrict__ ca1_w,
-                                                                    const float* __restrict__ ca1_b,
-                                                                    const float* __restrict__ ca3_w,
-                                                                    const float* __restrict__ ca3_b,
-                                                                    const float* __restrict__ sp_w,
-                                                                    float* __restrict__ gcat) {
+// GatedAttentionFusion's attention stage as four chip-filling steps (the per-object statistics are
+// batch-parallel reductions; the two 1x1 convs of the channel attention are (b x 2c) GEMMs on MFMA):
+//   1. colmean[b][ch] = mean over tokens of [cur | ot] (AdaptiveAvgPool1d(1));
+//   2. tstat[b][t] = (max, mean) over channels of cur (the spatial attention's two input rows);
+//   3. ca = sigmoid(ca3(relu(ca1(colmean)))) via gp_linear;
+//   4. gcat = [cur | (ot * ca) * sp], sp[t] = sigmoid(conv1d_7([max ; mean]))[t] (zero padding 3).
+// Step 1: lanes are channels (coalesced rows), the 4 waves take tokens t = w mod 4, summed in a fixed order.
+__global__ __launch_bounds__(FUS_THREADS) void fusion_colmean_kernel(const float* __restrict__ cur,
+                                                                     const float* __restrict__ ot, int n, int c,
+                                                                     float* __restrict__ colmean) {
 #pragma clang fp contract(off)
-    __shared__ float colmean[2048];
-    __shared__ float hid[512];
-    __shared__ float ca[1024];
-    __shared__ float tmax[1024], tmean[1024], sp[1024];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const float* cb = cur + (size_t)b * n * c;
-    const float* ob = ot + (size_t)b * n * c;
-    const int c2 = 2 * c, cr = c2 / 4;
-    for (int ch = tid; ch < c2; ch += FUS_THREADS) {
-        const float* src = ch < c ? cb + ch : ob + (ch - c);
-        float s = 0.f;
-        for (int t = 0; t < n; ++t) s += src[(size_t)t * c];
-        colmean[ch] = s / (float)n;
-    }
-    // per-token max / mean over channels (a wave per token)
-    for (int t = wid; t < n; t += FUS_THREADS / 64) {
-        float mxv = -INFINITY, s = 0.f;
-        for (int ch = lane; ch < c; ch += 64) {
-            const float v = cb[(size_t)t * c + ch];
-            mxv = fmaxf(mxv, v);
-            s += v;
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, b = blockIdx.y;
+    const int ch = blockIdx.x * 64 + lane;
+    float s = 0.f;
+    if (ch < 2 * c) {
+        const float* src = (ch < c ? cur + ch : ot + (ch - c)) + (size_t)b * n * c;
+        int t = wid;
+        for (; t + 12 < n; t += 16) {
+            const float v0 = src[(size_t)t * c], v1 = src[(size_t)(t + 4) * c];
+            const float v2 = src[(size_t)(t + 8) * c], v3 = src[(size_t)(t + 12) * c];
+            s += v0;
+            s += v1;
+            s += v2;
+            s += v3;
         }
-        for (int off = 32; off >= 1; off >>= 1) mxv = fmaxf(mxv, __shfl_xor(mxv, off, 64));
-        s = wave_sum(s);
-        if (lane == 0) {
-            tmax[t] = mxv;
-            tmean[t] = s / (float)c;
-        }
+        for (; t < n; t += 4) s += src[(size_t)t * c];
     }
+    part[wid][lane] = s;
     __syncthreads();
-    for (int o = tid; o < cr; o += FUS_THREADS) {
-        const float* wr = ca1_w + (size_t)o * c2;
-        float s = 0.f;
-        for (int k = 0; k < c2; ++k) s += wr[k] * colmean[k];
-        hid[o] = fmaxf(s + ca1_b[o], 0.f);
+    if (wid == 0 && ch < 2 * c)
+        colmean[(size_t)b * 2 * c + ch] = ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane])) / (float)n;
+}
+
+// Step 2: a wave per token.
+__global__ __launch_bounds__(FUS_THREADS) void fusion_tokstat_kernel(const float* __restrict__ cur, int n, int c,
+                                                                     float* __restrict__ tstat) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63, b = blockIdx.y;
+    const int t = blockIdx.x * (FUS_THREADS / 64) + (threadIdx.x >> 6);
+    if (t >= n) return;
+    const float* row = cur + ((size_t)b * n + t) * c;
+    float mxv = -INFINITY, s = 0.f;
+    for (int ch = lane; ch < c; ch += 64) {
+        const float v = row[ch];
+        mxv = fmaxf(mxv, v);
+        s += v;
     }
-    for (int t = tid; t < n; t += FUS_THREADS) {
-        float s = 0.f;
-        for (int u = 0; u < 7; ++u) {
-            const int tt = t + u - 3;
-            if (tt >= 0 && tt < n) s += sp_w[u] * tmax[tt] + sp_w[7 + u] * tmean[tt];
-        }
-        sp[t] = sigmoidf(s);
+    for (int off = 32; off >= 1; off >>= 1) mxv = fmaxf(mxv, __shfl_xor(mxv, off, 64));
+    s = wave_sum(s);
+    if (lane == 0) {
+        tstat[((size_t)b * n + t) * 2] = mxv;
+        tstat[((size_t)b * n + t) * 2 + 1] = s / (float)c;
     }
-    __syncthreads();
-    for (int o = tid; o < c; o += FUS_THREADS) {
-        const float* wr = ca3_w + (size_t)o * cr;
-        float s = 0.f;
-        for (int k = 0; k < cr; ++k) s += wr[k] * hid[k];
-        ca[o] = sigmoidf(s + ca3_b[o]);
+}
+
+// Step 4: a thread per 4 channels of one token (c % 4 == 0).
+__global__ __launch_bounds__(FUS_THREADS) void fusion_gcat_kernel(const float* __restrict__ cur,
+                                                                  const float* __restrict__ ot, int n, int c,
+                                                                  const float* __restrict__ ca,
+                                                                  const float* __restrict__ tstat,
+                                                                  const float* __restrict__ sp_w,
+                                                                  float* __restrict__ gcat) {
+#pragma clang fp contract(off)
+    const int c4 = c >> 2, b = blockIdx.y;
+    const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
+    if (e >= (long long)n * c4) return;
+    const int t = (int)(e / c4), ch = 4 * (int)(e - (long long)t * c4);
+    const float* ts = tstat + (size_t)b * n * 2;
+    float sv = 0.f;
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+        const int tt = t + u - 3;
+        if (tt >= 0 && tt < n) sv += sp_w[u] * ts[2 * tt] + sp_w[7 + u] * ts[2 * tt + 1];
     }
-    __syncthreads();
-    float* gb = gcat + (size_t)b * n * c2;
-    for (long long e = tid; e < (long long)n * c; e += FUS_THREADS) {
-        const int t = (int)(e / c), ch = (int)(e - (long long)t * c);
-        gb[(size_t)t * c2 + ch] = cb[e];
-        gb[(size_t)t * c2 + c + ch] = (ob[e] * ca[ch]) * sp[t];
-    }
+    const float sp = sigmoidf(sv);
+    const size_t src = ((size_t)b * n + t) * c + ch;
+    const f32x4 cv = ld4(cur + src), ov = ld4(ot + src), cav = ld4(ca + (size_t)b * c + ch);
+    float* g = gcat + ((size_t)b * n + t) * 2 * c;
+    st4(g + ch, cv);
+    st4(g + c + ch, f32x4{(ov.x * cav.x) * sp, (ov.y * cav.y) * sp, (ov.z * cav.z) * sp, (ov.w * cav.w) * sp});
+}
+
+#define FUS_TRY(x)                        \
+    do {                                  \
+        const int rc_ = (x);              \
+        if (rc_ != GP_OK) return rc_;     \
+    } while (0)
+
+static size_t fus_align(size_t floats) { return (floats + 63) & ~(size_t)63; }
+
+extern "C" size_t gp_fusion_attend_workspace_size(int b, int n, int c) {
+    if (b < 0 || n < 1 || c < 1) return 0;
+    const size_t B = (size_t)b;
+    return sizeof(float) * (fus_align(B * 2 * c) + fus_align(B * (c / 2)) + fus_align(B * c) + fus_align(B * 2 * n));
 }
 
 extern "C" int gp_fusion_attend(const float* cur, const float* ot, int b, int n, int c, const float* ca1_w,
                                 const float* ca1_b, const float* ca3_w, const float* ca3_b, const float* sp_w,
-                                float* gcat, hipStream_t st) {
+                                float* gcat, void* ws, size_t ws_bytes, hipStream_t st) {
     GP_REQUIRE(cur && ot && ca1_w && ca1_b && ca3_w && ca3_b && sp_w && gcat && b >= 0, "fusion_attend: null pointer");
-    GP_REQUIRE(n >= 1 && n <= 1024 && c >= 4 && c <= 1024 && c % 2 == 0, "fusion_attend: n=%d c=%d out of range", n, c);
+    GP_REQUIRE(n >= 1 && c >= 32 && c % 32 == 0, "fusion_attend: n=%d c=%d (c must be a multiple of 32)", n, c);
+    GP_REQUIRE(((uintptr_t)cur | (uintptr_t)ot | (uintptr_t)gcat | (uintptr_t)ws) % 16 == 0,
+               "fusion_attend: pointers must be 16-byte aligned");
     if (!b) return GP_OK;
-    hipLaunchKernelGGL(fusion_attend_kernel, dim3(b), dim3(FUS_THREADS), 0, st, cur, ot, n, c, ca1_w, ca1_b, ca3_w,
-                       ca3_b, sp_w, gcat);
-    return gp_check_launch("fusion_attend_kernel");
+    GP_REQUIRE(ws && ws_bytes >= gp_fusion_attend_workspace_size(b, n, c), "fusion_attend: workspace %zu < %zu bytes",
+               ws_bytes, gp_fusion_attend_workspace_size(b, n, c));
+    const size_t B = (size_t)b;
+    float* colmean = static_cast<float*>(ws);
+    float* hid = colmean + fus_align(B * 2 * c);
+    float* ca = hid + fus_align(B * (c / 2));
+    float* tstat = ca + fus_align(B * c);
+    hipLaunchKernelGGL(fusion_colmean_kernel, dim3((2 * c + 63) / 64, b), dim3(FUS_THREADS), 0, st, cur, ot, n, c, colmean);
+    FUS_TRY(gp_check_launch("fusion_colmean_kernel"));
+    hipLaunchKernelGGL(fusion_tokstat_kernel, dim3((n + 3) / 4, b), dim3(FUS_THREADS), 0, st, cur, n, c, tstat);
+    FUS_TRY(gp_check_launch("fusion_tokstat_kernel"));
+    FUS_TRY(gp_linear(colmean, 2 * c, b, 2 * c, ca1_w, ca1_b, c / 2, 1, hid, c / 2, st));
+    FUS_TRY(gp_linear(hid, c / 2, b, c / 2, ca3_w, ca3_b, c, 2, ca, c, st));
+    const long long e = (long long)n * (c / 4);
+    hipLaunchKernelGGL(fusion_gcat_kernel, dim3((unsigned)((e + FUS_THREADS - 1) / FUS_THREADS), b), dim3(FUS_THREADS), 0,
+                       st, cur, ot, n, c, ca, tstat, sp_w, gcat);
+    return gp_check_launch("fusion_gcat_kernel");
 }
 
 __global__ __launch_bounds__(FUS_THREADS) void fusion_mix_kernel(const float* __restrict__ g,

@@ -88,6 +88,7 @@ class FusEncoderModel:
         self.t = {k: torch.from_numpy(v).to(device) for k, v in pack_fus_blocks(sd).items()}
         self._ws: Optional[torch.Tensor] = None
         self._bias: Optional[torch.Tensor] = None
+        self._fws: Optional[torch.Tensor] = None
 
     @property
     def table(self) -> np.ndarray:
@@ -142,9 +143,12 @@ class FusEncoderModel:
         ot = self.linear(orig, f"fu{k}.original_transform", "relu")
         gcat = torch.empty((B, n, 2 * c), dtype=torch.float32, device=self.device)
         t = self.t
+        need = int(self.lib.gp_fusion_attend_workspace_size(B, n, c))
+        if self._fws is None or self._fws.numel() < need:
+            self._fws = torch.empty(need, dtype=torch.uint8, device=self.device)
         check(self.lib.gp_fusion_attend(_vp(cur), _vp(ot), B, n, c, _vp(t[f"fu{k}.ca1.w"]), _vp(t[f"fu{k}.ca1.b"]),
                                         _vp(t[f"fu{k}.ca3.w"]), _vp(t[f"fu{k}.ca3.b"]), _vp(t[f"fu{k}.sp.w"]),
-                                        _vp(gcat), self._s()), "fusion_attend")
+                                        _vp(gcat), _vp(self._fws), self._fws.numel(), self._s()), "fusion_attend")
         g = self.linear(gcat, f"fu{k}.gate", "sigmoid")
         fused = torch.empty_like(cur)
         check(self.lib.gp_fusion_mix(_vp(g), _vp(gcat), B * n, c, _vp(fused), self._s()), "fusion_mix")

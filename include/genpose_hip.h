@@ -30,7 +30,7 @@ enum { GP_OK = 0, GP_ERR_INVALID = -1, GP_ERR_LAUNCH = -2, GP_ERR_UNSUPPORTED = 
 const char *gp_last_error(void);
 /* ABI version of this header. */
 int gp_abi_version(void);
-#define GP_ABI_VERSION 5
+#define GP_ABI_VERSION 6
 
 /* ===================================================================== operator level
  * Drop-in forward ops of `pointnet2_cuda` (same argument meaning and layouts). */
@@ -122,10 +122,12 @@ int gp_interp_points(const float *x, int b, int n_in, int c, int n_out, float *y
 /* GatedAttentionFusion's attention stage (attention.py:298-313) per object: cur (b, n, c), ot (b, n, c)
  * (original_transform output) -> gcat (b, n, 2c) = [cur | ot * ca * sp] with ca = channel attention
  * of mean_n [cur | ot] (ca1: (2c/4, 2c) + bias, ReLU, ca3: (c, 2c/4) + bias, sigmoid) and sp =
- * sigmoid(conv1d_7([max_c cur ; mean_c cur])) (sp_w: (2, 7), zero padding 3). c <= 1024, n <= 1024. */
+ * sigmoid(conv1d_7([max_c cur ; mean_c cur])) (sp_w: (2, 7), zero padding 3). c % 32 == 0.
+ * ws: gp_fusion_attend_workspace_size(b, n, c) bytes of device scratch (the per-object statistics). */
+size_t gp_fusion_attend_workspace_size(int b, int n, int c);
 int gp_fusion_attend(const float *cur, const float *ot, int b, int n, int c, const float *ca1_w,
                      const float *ca1_b, const float *ca3_w, const float *ca3_b, const float *sp_w,
-                     float *gcat, hipStream_t stream);
+                     float *gcat, void *ws, size_t ws_bytes, hipStream_t stream);
 /* fused = g * cur + (1 - g) * att with cur = gcat[:, :c], att = gcat[:, c:] (attention.py:318-320):
  * g (rows, c), gcat (rows, 2c) -> out (rows, c). */
 int gp_fusion_mix(const float *g, const float *gcat, int rows, int c, float *out, hipStream_t stream);
