@@ -49,6 +49,9 @@ _SIGS: Dict[str, tuple] = {
     "gp_sa_level": (c_int, [c_void_p, c_int64_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t,
                             c_void_p, c_void_p]),
     "gp_linear": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "gp_linear_split_words": (c_size_t, [c_int, c_int]),
+    "gp_linear_split": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int,
+                                c_void_p, c_void_p]),
     "gp_add_layernorm": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
     "gp_relpe_bias_bytes": (c_size_t, [c_int, c_int]),
     "gp_relpe_bias": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),

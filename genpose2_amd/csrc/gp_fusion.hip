@@ -10,8 +10,14 @@
 // Token tensors are point-major (b, n, C): the reference's (b, C, n) transposed, so one token's channels
 // are contiguous and every linear is a row-major GEMM over b*n rows.
 #include "gp_common.h"
+#include "gp_head.h"   // split-f16 helpers: f16x8, mfma_h, exp2i, ilog2f, rows_max
 
 constexpr int FUS_THREADS = 256;
+#define FUS_TRY(x)                        \
+    do {                                  \
+        const int rc_ = (x);              \
+        if (rc_ != GP_OK) return rc_;     \
+    } while (0)
 constexpr int FUS_HEADS = 8;
 
 __device__ __forceinline__ float sigmoidf(float v) { return 1.0f / (1.0f + expf(-v)); }
@@ -232,6 +238,181 @@ extern "C" int gp_linear(const float* x, int ldx, int m, int k, const float* w, 
     return gp_check_launch("linear_kernel");
 }
 
+// ============================================================================ token linear (split-f16 MFMA)
+// The same y = act(x W^T + b) with each fp32 operand split into f16 hi / lo planes at a power-of-two scale
+// (W: one exponent per matrix, packed on the host by pack.pack_h16_fragments; x: per token from its row
+// max |x|, split on the way into LDS) and three v_mfma_f32_16x16x32_f16 products (hi.hi + hi.lo + lo.hi)
+// accumulated in fp32 -- the encoder's split arithmetic (tok_split_gemm_kernel), 16x the MACs per MFMA of
+// the fp32 path. Workgroup: 64*WO outputs x 64*(8/WO) tokens, 8 waves of 64 x 64, two LDS stages of one
+// 32-deep chunk, one barrier per chunk.
+constexpr int SL_THREADS = 512;
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+struct SplitLinArgs {
+    const float* x;
+    int ldx, m, k;
+    const float* rmax;    // per-token max |x| (m)
+    const int32_t* w;     // [ew, 0, 0, 0] (W was scaled by 2^ew), then the planes [tile][chunk][plane][lane] f16x8
+    const float* bias;
+    int n;
+    float* y;
+    int ldy;
+};
+template <int WO>
+constexpr size_t sl_lds_bytes() {
+    return 2 * (size_t)(4 * WO + 4 * (8 / WO)) * 2048 + sizeof(int) * 64 * (8 / WO);
+}
+
+__global__ __launch_bounds__(256) void fus_rowmax_kernel(const float* __restrict__ x, int ldx, int m, int k,
+                                                         float* __restrict__ rmax) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= m) return;
+    const float* row = x + (size_t)r * ldx;
+    float v = 0.f;
+    for (int c = 4 * lane; c < k; c += 256) {
+        const f32x4 t = ld4(row + c);
+        v = fmaxf(v, fmaxf(fmaxf(fabsf(t.x), fabsf(t.y)), fmaxf(fabsf(t.z), fabsf(t.w))));
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    if (lane == 0) rmax[r] = v;
+}
+
+template <int WO, int ACT>
+__global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a) {
+    constexpr int WT = 8 / WO, BM = 64 * WT;
+    constexpr int NA = 4 * WO * 128, NB = 4 * WT * 128;   // f16x8 fragments per stage
+    extern __shared__ __attribute__((aligned(16))) f16x8 sl_lds[];
+    auto sA = [&](int st) { return sl_lds + st * (NA + NB); };
+    auto sB = [&](int st) { return sl_lds + st * (NA + NB) + NA; };
+    int* eT = reinterpret_cast<int*>(sl_lds + 2 * (NA + NB));
+    const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, nn = lane & 15;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = blockIdx.y * BM, T0 = blockIdx.x * 4 * WO;
+    const int KC = a.k >> 5;
+    const int g = tid & 7;
+    const int ew = a.w[0];
+    const f16x8* W = reinterpret_cast<const f16x8*>(a.w + 4);
+    int row[WT];
+    float sc[WT];
+#pragma unroll
+    for (int u = 0; u < WT; ++u) {
+        const int r = (tid + SL_THREADS * u) >> 3;
+        row[u] = m0 + r;
+        const float mx = row[u] < a.m ? a.rmax[row[u]] : 0.f;
+        const int E = mx > 1e-30f ? ilog2f(mx) : -100;
+        sc[u] = exp2i(14 - E);
+        if (g == 0) eT[r] = E;
+    }
+    auto load = [&](int c, f32x4 (&ra)[WO], f32x4 (&rb)[WT]) {
+#pragma unroll
+        for (int u = 0; u < WO; ++u) {
+            const int idx = tid + SL_THREADS * u;
+            ra[u] = ld4(reinterpret_cast<const float*>(W + ((size_t)(T0 + (idx >> 7)) * KC + c) * 128 + (idx & 127)));
+        }
+#pragma unroll
+        for (int u = 0; u < WT; ++u)
+            rb[u] = row[u] < a.m ? ld4(a.x + (size_t)row[u] * a.ldx + 32 * c + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto store = [&](int s, const f32x4 (&ra)[WO], const f32x4 (&rb)[WT]) {
+#pragma unroll
+        for (int u = 0; u < WO; ++u) sA(s)[tid + SL_THREADS * u] = __builtin_bit_cast(f16x8, ra[u]);
+#pragma unroll
+        for (int u = 0; u < WT; ++u) {
+#pragma clang fp contract(off)
+            const int r = (tid + SL_THREADS * u) >> 3, ln = 16 * (g & 3) + (r & 15), half = g >> 2;
+            f16x4 hi, lo;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float x = rb[u][j] * sc[u];
+                const _Float16 h = (_Float16)x;
+                hi[j] = h;
+                lo[j] = (_Float16)(x - (float)h);
+            }
+            reinterpret_cast<f16x4*>(&sB(s)[((r >> 4) * 2 + 0) * 64 + ln])[half] = hi;
+            reinterpret_cast<f16x4*>(&sB(s)[((r >> 4) * 2 + 1) * 64 + ln])[half] = lo;
+        }
+    };
+    const int wo = wid % WO, wt = wid / WO;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 ra[WO], rb[WT];
+    load(0, ra, rb);
+    store(0, ra, rb);
+    __syncthreads();
+    for (int c = 0; c < KC; ++c) {
+        const int s = c & 1;
+        if (c + 1 < KC) load(c + 1, ra, rb);
+        f16x8 bh[4], bl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bh[j] = sB(s)[((4 * wt + j) * 2 + 0) * 64 + lane];
+            bl[j] = sB(s)[((4 * wt + j) * 2 + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f16x8 ah = sA(s)[((4 * wo + i) * 2 + 0) * 64 + lane];
+            const f16x8 al = sA(s)[((4 * wo + i) * 2 + 1) * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(al, bh[j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(ah, bl[j], acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(ah, bh[j], acc[i][j]);
+        }
+        if (c + 1 < KC) store(s ^ 1, ra, rb);
+        __syncthreads();
+    }
+    // epilogue: unscale (exact powers of two), bias, activation; the accumulator of tile (i, j) holds outputs
+    // 4q..4q+3 of output tile T0 + 4 wo + i for token (4 wt + j) * 16 + nn
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int pc = (4 * wt + j) * 16 + nn, r = m0 + pc;
+        const float u = exp2i(eT[pc] - 14 - ew);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int o = (T0 + 4 * wo + i) * 16 + 4 * q;
+            if (o >= a.n || r >= a.m) continue;
+            f32x4 v = acc[i][j] * u + ld4(a.bias + o);
+            if (ACT == 1) v = relu4(v);
+            if (ACT == 2) v = f32x4{sigmoidf(v.x), sigmoidf(v.y), sigmoidf(v.z), sigmoidf(v.w)};
+            st4(a.y + (size_t)r * a.ldy + o, v);
+        }
+    }
+}
+
+extern "C" size_t gp_linear_split_words(int n, int k) {
+    if (n < 1 || k < 32) return 0;
+    return 4 + (size_t)((n + 127) / 128 * 128) * k;
+}
+
+extern "C" int gp_linear_split(const float* x, int ldx, int m, int k, const int32_t* wpk, const float* bias, int n,
+                               int act, float* y, int ldy, float* rmax, hipStream_t st) {
+    GP_REQUIRE(x && wpk && bias && y && rmax && m >= 0, "linear_split: null pointer");
+    GP_REQUIRE(k >= 32 && k % 32 == 0 && n >= 16 && n % 16 == 0, "linear_split: k=%d (multiple of 32), n=%d (of 16)", k, n);
+    GP_REQUIRE(ldx >= k && ldy >= n && ldx % 4 == 0 && ldy % 4 == 0, "linear_split: strides ldx=%d ldy=%d", ldx, ldy);
+    GP_REQUIRE(((uintptr_t)x | (uintptr_t)wpk | (uintptr_t)y | (uintptr_t)bias) % 16 == 0,
+               "linear_split: pointers must be 16-byte aligned");
+    GP_REQUIRE(act >= 0 && act <= 2, "linear_split: act %d", act);
+    if (!m) return GP_OK;
+    hipLaunchKernelGGL(fus_rowmax_kernel, dim3((m + 3) / 4), dim3(256), 0, st, x, ldx, m, k, rmax);
+    FUS_TRY(gp_check_launch("fus_rowmax_kernel"));
+    SplitLinArgs a{x, ldx, m, k, rmax, wpk, bias, n, y, ldy};
+    const int npad = (n + 127) / 128 * 128;
+#define GP_LSPLIT(WO)                                                                                              \
+    {                                                                                                          \
+        const dim3 grid(npad / (64 * WO), (m + 64 * (8 / WO) - 1) / (64 * (8 / WO)));                          \
+        if (act == 0) hipLaunchKernelGGL((linear_split_kernel<WO, 0>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
+        else if (act == 1) hipLaunchKernelGGL((linear_split_kernel<WO, 1>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
+        else hipLaunchKernelGGL((linear_split_kernel<WO, 2>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
+    }
+    if (npad % 256 == 0) GP_LSPLIT(4) else GP_LSPLIT(2)
+#undef GP_LSPLIT
+    return gp_check_launch("linear_split_kernel");
+}
+
 // ============================================================================ residual + LayerNorm
 // One wave per row (d <= 1024: up to 16 values per lane in registers), torch's biased variance.
 __global__ __launch_bounds__(FUS_THREADS) void add_layernorm_kernel(const float* x,
@@ -355,13 +536,6 @@ extern "C" int gp_relpe_bias(const float* pe, const float* xyz, int b, int n, fl
 // the query blocks of one (object, head) land on one XCD, so its K / V are read into one L2.
 // (q.k / sqrt(hd) is taken as q.k * (1 / sqrt(hd)): within an ulp of torch's division. The softmax is
 // torch's result up to rounding: the online rescaling replaces its two passes.)
-__device__ __forceinline__ float rows_max(float v) {   // max over lanes l, l^16, l^32, l^48
-    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-    const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
-}
-
 template <int HDP>
 __global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restrict__ qkv,
                                                           const float* __restrict__ bias, int n, int d, int hd,
@@ -610,12 +784,6 @@ __global__ __launch_bounds__(FUS_THREADS) void fusion_gcat_kernel(const float* _
     st4(g + ch, cv);
     st4(g + c + ch, f32x4{(ov.x * cav.x) * sp, (ov.y * cav.y) * sp, (ov.z * cav.z) * sp, (ov.w * cav.w) * sp});
 }
-
-#define FUS_TRY(x)                        \
-    do {                                  \
-        const int rc_ = (x);              \
-        if (rc_ != GP_OK) return rc_;     \
-    } while (0)
 
 static size_t fus_align(size_t floats) { return (floats + 63) & ~(size_t)63; }
 

@@ -22,6 +22,7 @@ level (pointnet2.py:370-377) is not executed.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -72,7 +73,25 @@ def pack_fus_blocks(sd: weights.StateDict) -> Dict[str, np.ndarray]:
         out[f"fu{k}.ca3.w"] = sd[f"{g}.channel_attention.3.weight"][:, :, 0]
         out[f"fu{k}.ca3.b"] = sd[f"{g}.channel_attention.3.bias"]
         out[f"fu{k}.sp.w"] = sd[f"{g}.spatial_attention.0.weight"].reshape(2, arch.FUS_SPATIAL_K)
-    return {k: np.ascontiguousarray(v, np.float32) for k, v in out.items()}
+    out = {k: np.ascontiguousarray(v, np.float32) for k, v in out.items()}
+    for name in SPLIT_LINEARS:
+        out[f"{name}.wh"] = pack_split_linear(out[f"{name}.w"])
+    return out
+
+
+# token linears that also carry split-f16 planes (gp_linear_split): every one with k % 32 == 0
+SPLIT_LINEARS = tuple(f"tf{lv}.{m}" for lv in range(arch.N_LEVELS) for m in ("qkv", "wo", "linear1", "linear2")) + \
+    tuple(f"fu{k}.{m}" for k in range(1, arch.N_LEVELS) for m in ("original_transform", "gate", "output_conv"))
+
+
+def pack_split_linear(w: np.ndarray) -> np.ndarray:
+    """gp_linear_split's weight buffer (int32 words): [e, 0, 0, 0] then the f16 hi / lo planes of W * 2**e
+    (pack.pack_h16_fragments) with W's rows zero-padded to a multiple of 128."""
+    n, k = w.shape
+    wp = np.zeros((-(-n // 128) * 128, k), np.float32)
+    wp[:n] = w
+    e = pack.split_exponent(w)
+    return np.concatenate([np.array([e, 0, 0, 0], np.int32), pack.pack_h16_fragments(wp, e)])
 
 
 class FusEncoderModel:
@@ -84,11 +103,13 @@ class FusEncoderModel:
         buf, offs = pack.pack_encoder(sd, arch.fus_sa_branches())
         self.wbuf = torch.from_numpy(buf).to(device)
         self._table = np.ascontiguousarray(offs, np.int64)
-        self.offsets = self._table.reshape(-1)
+        self.arith = "split_f16"
         self.t = {k: torch.from_numpy(v).to(device) for k, v in pack_fus_blocks(sd).items()}
         self._ws: Optional[torch.Tensor] = None
         self._bias: Optional[torch.Tensor] = None
         self._fws: Optional[torch.Tensor] = None
+        self._rmax: Optional[torch.Tensor] = None
+        self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
 
     @property
     def table(self) -> np.ndarray:
@@ -97,7 +118,19 @@ class FusEncoderModel:
 
     def set_table(self, table: np.ndarray) -> None:
         self._table = np.ascontiguousarray(table, np.int64).reshape(self._table.shape)
-        self.offsets = self._table.reshape(-1)
+        self.set_arith(self.arith)
+
+    def set_arith(self, arith: str) -> None:
+        """GEMM arithmetic of the SA levels and of the token linears: "split_f16" (f16 hi/lo MFMA products
+        with per-token activation scaling; gp_linear_split for every linear of >= 1024 tokens) or "f32"
+        (exact fp32 MFMA everywhere)."""
+        if arith not in ("split_f16", "f32"):
+            raise ValueError(f"unknown encoder arithmetic {arith!r} (split_f16 | f32)")
+        t = self._table.copy()
+        if arith == "f32":
+            t[..., 2] = -1
+        self.arith = arith
+        self.offsets = np.ascontiguousarray(t.reshape(-1), np.int64)
 
     def _s(self):
         return ctypes.c_void_p(stream_handle(self.device))
@@ -109,7 +142,14 @@ class FusEncoderModel:
         m = int(np.prod(lead)) if lead else 1
         n = W.shape[0]
         y = torch.empty(lead + (n,), dtype=torch.float32, device=self.device) if out is None else out
-        check(self.lib.gp_linear(_vp(x), k, m, k, _vp(W), _vp(b), n, _ACT[act], _vp(y), n, self._s()), f"linear {w}")
+        if self.arith == "split_f16" and m >= 1024 and f"{w}.wh" in self.t:
+            if self._rmax is None or self._rmax.numel() < m:
+                self._rmax = torch.empty(m, dtype=torch.float32, device=self.device)
+            check(self.lib.gp_linear_split(_vp(x), k, m, k, _vp(self.t[f"{w}.wh"]), _vp(b), n, _ACT[act], _vp(y), n,
+                                           _vp(self._rmax), self._s()), f"linear_split {w}")
+        else:
+            check(self.lib.gp_linear(_vp(x), k, m, k, _vp(W), _vp(b), n, _ACT[act], _vp(y), n, self._s()),
+                  f"linear {w}")
         return y
 
     def add_ln(self, x: torch.Tensor, r: torch.Tensor, name: str) -> torch.Tensor:

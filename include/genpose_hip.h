@@ -99,6 +99,14 @@ int gp_sa_level(const float *wbuf, const int64_t *layer_off, int level, int c_pr
  * 2 sigmoid. Exact fp32 MFMA (v_mfma_f32_16x16x4_f32). */
 int gp_linear(const float *x, int ldx, int m, int k, const float *w, const float *bias, int n,
               int act, float *y, int ldy, hipStream_t stream);
+/* The same linear in split-f16 arithmetic (three v_mfma_f32_16x16x32_f16 products of hi / lo f16
+ * planes, fp32 accumulation; x scaled per row by a power of two from its max |x|). wpk: int32 words
+ * [e, 0, 0, 0] + the planes of W * 2^e, rows zero-padded to a multiple of 128, in
+ * genpose2_amd/fus_encoder.py pack_split_linear's layout (gp_linear_split_words(n, k) words).
+ * k % 32 == 0, n % 16 == 0; rmax: m floats of device scratch (the row maxima). */
+size_t gp_linear_split_words(int n, int k);
+int gp_linear_split(const float *x, int ldx, int m, int k, const int32_t *wpk, const float *bias, int n,
+                    int act, float *y, int ldy, float *rmax, hipStream_t stream);
 /* y = LayerNorm(x + r) over the last dim d (gamma, beta, eps), m rows; y may alias x. */
 int gp_add_layernorm(const float *x, const float *r, int m, int d, const float *gamma,
                      const float *beta, float eps, float *y, hipStream_t stream);

@@ -73,6 +73,39 @@ def test_linear_vs_torch(lib, m, k, n, act, pad):
         assert torch.all(y[:, n:] == 0)          # ldy: nothing written past n
 
 
+@pytest.mark.parametrize("m,k,n,act,pad", [(100, 96, 288, 0, 0), (4096, 256, 1024, 1, 0), (37, 384, 96, 2, 0),
+                                           (513, 1024, 192, 1, 32), (1500, 96, 288, 1, 0), (2000, 384, 96, 2, 16),
+                                           (1031, 4096, 1024, 0, 0), (4096, 1024, 4096, 1, 0), (3000, 192, 48, 0, 0)])
+def test_linear_split_vs_torch(lib, m, k, n, act, pad):
+    """gp_linear_split (split-f16 MFMA) against the fp64 linear: the split arithmetic's bound (about 3
+    fp32 roundings per product) stays well inside the fused encoder's 1e-5 budget. Rows of very different
+    magnitudes (per-row scaling) and an all-zero row are included."""
+    from genpose2_amd._lib import check
+    from genpose2_amd.fus_encoder import pack_split_linear
+    g = torch.Generator().manual_seed(m + k + n + 1)
+    x = torch.randn(m, k + pad, generator=g) * torch.exp(torch.randn(m, 1, generator=g) * 3)
+    x[m // 2] = 0.0
+    w = torch.randn(n, k, generator=g) / k ** 0.5
+    b = torch.randn(n, generator=g)
+    ref = tf.linear(x[:, :k].double(), w.double(), b.double())
+    ref = [ref, torch.relu(ref), torch.sigmoid(ref)][act]
+    wpk = pack_split_linear(w.numpy())
+    assert wpk.size == lib.gp_linear_split_words(n, k)
+    y = torch.zeros(m, n + pad, device=DEV)
+    xd, wd, bd = x.to(DEV), torch.from_numpy(wpk).to(DEV), b.to(DEV)
+    rmax = torch.empty(m, device=DEV)
+    check(lib.gp_linear_split(_vp(xd), k + pad, m, k, _vp(wd), _vp(bd), n, act, _vp(y), n + pad, _vp(rmax), _s()),
+          "linear_split")
+    torch.cuda.synchronize()
+    # per-row bound: |err| <= 4 * 2^-22 * sum_k |x||w| (+ the bias rounding)
+    bound = tf.linear(x[:, :k].double().abs(), w.double().abs()) * 4 * 2.0 ** -22 + 1e-7 * (1 + ref.abs())
+    err = (y[:, :n].cpu().double() - ref).abs()
+    assert torch.all(err <= bound), float((err / bound).max())
+    assert torch.equal(rmax.cpu(), x[:, :k].abs().max(1).values)   # row maxima over the k columns read
+    if pad:
+        assert torch.all(y[:, n:] == 0)
+
+
 def test_add_layernorm_vs_torch(lib):
     from genpose2_amd._lib import check
     for m, d in ((777, 96), (300, 1024), (5, 512), (64, 256)):
