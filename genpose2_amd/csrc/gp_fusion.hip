@@ -463,52 +463,54 @@ extern "C" int gp_add_layernorm(const float* x, const float* r, int m, int d, co
 
 // ============================================================================ relative-PE bias
 // Packed pe (gp_relpe_bias in genpose_hip.h): distance Linear(1,16)/ReLU/Linear(16,8), direction
-// Linear(3,16)/ReLU/Linear(16,8), fusion Linear(16,8) over [distance | direction]. One thread per
-// pair evaluates all 8 heads. Stored key-major, bias[b][h][j][i] (query i, key j): the attention
-// kernel's lanes are queries, so for each key a wave reads 64 consecutive floats; consecutive
-// threads here take consecutive queries i, so the writes are coalesced too.
+// Linear(3,16)/ReLU/Linear(16,8), fusion Linear(16,8) over [distance | direction]. The fusion layer is
+// linear, so the host composes it with the two second layers: bias_h = A_h . hd + B_h . ho + c_h
+// (pe[512:776), composed in float64) -- 256 multiply-adds per pair instead of 384, done as packed fp32
+// FMAs over head pairs with the weights in scalar registers (uniform loads). One thread per pair, all 8
+// heads. Stored key-major, bias[b][h][j][i] (query i, key j): consecutive threads take consecutive
+// queries i, so the stores are coalesced and the attention kernel reads 16 consecutive queries per key.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __restrict__ pe,
                                                                  const float* __restrict__ xyz, int n,
                                                                  float* __restrict__ bias) {
-#pragma clang fp contract(off)
-    __shared__ float sp[512];
-    for (int i = threadIdx.x; i < 504; i += FUS_THREADS) sp[i] = pe[i];
-    __syncthreads();
     const int b = blockIdx.y;
     const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
     if (e >= (long long)n * n) return;
     const int j = (int)(e / n), i = (int)(e - (long long)j * n);
     const float* pi = xyz + ((size_t)b * n + i) * 3;
     const float* pj = xyz + ((size_t)b * n + j) * 3;
-    const float rx = pj[0] - pi[0], ry = pj[1] - pi[1], rz = pj[2] - pi[2];   // xyz[j] - xyz[i]
-    const float dist = sqrtf((rx * rx + ry * ry) + rz * rz);
-    const float den = dist + 1e-7f;
-    const float dx = rx / den, dy = ry / den, dz = rz / den;
     float hd[16], ho[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        hd[u] = fmaxf(dist * sp[u] + sp[16 + u], 0.f);
-        const float* w = sp + 168 + 3 * u;
-        ho[u] = fmaxf(((dx * w[0] + dy * w[1]) + dz * w[2]) + sp[216 + u], 0.f);
-    }
-    float cat[16];
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-        float a = 0.f, c = 0.f;
+    {
+#pragma clang fp contract(off)
+        const float rx = pj[0] - pi[0], ry = pj[1] - pi[1], rz = pj[2] - pi[2];   // xyz[j] - xyz[i]
+        const float dist = sqrtf((rx * rx + ry * ry) + rz * rz);
+        const float den = dist + 1e-7f;
+        const float dx = rx / den, dy = ry / den, dz = rz / den;
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            a += hd[u] * sp[32 + 16 * h + u];
-            c += ho[u] * sp[232 + 16 * h + u];
+            hd[u] = fmaxf(dist * pe[u] + pe[16 + u], 0.f);
+            const float* w = pe + 168 + 3 * u;
+            ho[u] = fmaxf(((dx * w[0] + dy * w[1]) + dz * w[2]) + pe[216 + u], 0.f);
         }
-        cat[h] = a + sp[160 + h];
-        cat[8 + h] = c + sp[360 + h];
     }
+    const f32x2* A2 = reinterpret_cast<const f32x2*>(pe + 512);   // [u][head pair]: A[2p][u], A[2p+1][u]
+    const f32x2* B2 = reinterpret_cast<const f32x2*>(pe + 640);
+    const f32x2* C2 = reinterpret_cast<const f32x2*>(pe + 768);
+    f32x2 acc[4];
 #pragma unroll
-    for (int h = 0; h < 8; ++h) {
-        float f = 0.f;
+    for (int p = 0; p < 4; ++p) acc[p] = C2[p];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) f += cat[u] * sp[368 + 16 * h + u];
-        bias[(((size_t)b * FUS_HEADS + h) * n + j) * n + i] = f + sp[496 + h];
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[p] = __builtin_elementwise_fma(f32x2{hd[u], hd[u]}, A2[4 * u + p], acc[p]);
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[p] = __builtin_elementwise_fma(f32x2{ho[u], ho[u]}, B2[4 * u + p], acc[p]);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        bias[(((size_t)b * FUS_HEADS + 2 * p) * n + j) * n + i] = acc[p].x;
+        bias[(((size_t)b * FUS_HEADS + 2 * p + 1) * n + j) * n + i] = acc[p].y;
     }
 }
 

@@ -40,15 +40,27 @@ def _vp(t: Optional[torch.Tensor]):
 
 
 def pack_relpe(sd: weights.StateDict, prefix: str) -> np.ndarray:
-    """The 512-float layout gp_relpe_bias reads (include/genpose_hip.h)."""
+    """The 1024-float layout gp_relpe_bias reads (include/genpose_hip.h): the 504 raw parameters, then the
+    fusion layer composed with the two second layers (float64, rounded once): A = Wf[:, :8] Wd2 and
+    B = Wf[:, 8:] Wo2 stored [u][head] (the kernel's packed head pairs), c = Wf [bd2; bo2] + bf."""
     g = lambda k: np.asarray(sd[f"{prefix}.{k}"], np.float32).reshape(-1)  # noqa: E731
-    out = np.zeros(512, np.float32)
+    out = np.zeros(1024, np.float32)
     parts = [g("distance_encoder.0.weight"), g("distance_encoder.0.bias"), g("distance_encoder.2.weight"),
              g("distance_encoder.2.bias"), g("direction_encoder.0.weight"), g("direction_encoder.0.bias"),
              g("direction_encoder.2.weight"), g("direction_encoder.2.bias"), g("fusion.weight"), g("fusion.bias")]
     v = np.concatenate(parts)
     assert v.size == 504
     out[:504] = v
+    h, hid = arch.FUS_HEADS, arch.FUS_PE_HID
+    wd2 = v[32:160].reshape(h, hid).astype(np.float64)
+    bd2 = v[160:168].astype(np.float64)
+    wo2 = v[232:360].reshape(h, hid).astype(np.float64)
+    bo2 = v[360:368].astype(np.float64)
+    wf = v[368:496].reshape(h, 2 * h).astype(np.float64)
+    bf = v[496:504].astype(np.float64)
+    out[512:640] = (wf[:, :h] @ wd2).T.reshape(-1)
+    out[640:768] = (wf[:, h:] @ wo2).T.reshape(-1)
+    out[768:776] = wf[:, :h] @ bd2 + wf[:, h:] @ bo2 + bf
     return out
 
 

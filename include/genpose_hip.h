@@ -112,10 +112,12 @@ int gp_add_layernorm(const float *x, const float *r, int m, int d, const float *
                      const float *beta, float eps, float *y, hipStream_t stream);
 /* Relative-PE bias of EfficientRelativePositionalEncoding (8 heads): xyz (b, n, 3) ->
  * bias (b, 8, n, n) KEY-MAJOR: bias[b][h][j][i] is the reference's relative_bias[b, h, i, j]
- * (query i, key j, rel = xyz[j] - xyz[i]). pe (host-packed, 512 floats):
+ * (query i, key j, rel = xyz[j] - xyz[i]). pe (host-packed, 1024 floats):
  * [0:16) dist.0.w, [16:32) dist.0.b, [32:160) dist.2.w (8x16), [160:168) dist.2.b,
  * [168:216) dir.0.w (16x3), [216:232) dir.0.b, [232:360) dir.2.w, [360:368) dir.2.b,
- * [368:496) fusion.w (8x16), [496:504) fusion.b. */
+ * [368:496) fusion.w (8x16), [496:504) fusion.b; then the fusion layer composed with the second
+ * layers: [512:640) A[u][h] = (fusion.w[:, :8] dist.2.w)[h][u], [640:768) B[u][h] likewise with
+ * dir.2.w, [768:776) c = fusion.w [dist.2.b; dir.2.b] + fusion.b. */
 size_t gp_relpe_bias_bytes(int b, int n);
 int gp_relpe_bias(const float *pe, const float *xyz, int b, int n, float *bias, hipStream_t stream);
 /* Multi-head attention with an additive bias (MultiheadAttentionWithRelativePE core,
