@@ -51,12 +51,13 @@ _SIGS: Dict[str, tuple] = {
     "gp_linear": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     "gp_linear_split_words": (c_size_t, [c_int, c_int]),
     "gp_linear_split": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int,
-                                c_void_p, c_void_p]),
-    "gp_add_layernorm": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
+                                c_void_p, c_int, c_void_p, c_void_p]),
+    "gp_add_layernorm": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                 c_void_p]),
     "gp_relpe_bias_bytes": (c_size_t, [c_int, c_int]),
     "gp_relpe_bias": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "gp_mha_attention": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
-    "gp_interp_points": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "gp_interp_points": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "gp_fusion_attend_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "gp_fusion_attend": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

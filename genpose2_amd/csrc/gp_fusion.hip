@@ -195,10 +195,9 @@ static void launch_linear_lds(const float* x, int ldx, int m, int k, const float
     hipLaunchKernelGGL((linear_lds_kernel<WN, ACT>), grid, dim3(FUS_THREADS), 0, st, x, ldx, m, k, w, bias, n, y, ldy);
 }
 
-template <int TN, int ACT>
+template <int TN, int ACT, int TM = 2>
 static void launch_linear(const float* x, int ldx, int m, int k, const float* w, const float* bias, int n, float* y,
                           int ldy, hipStream_t st) {
-    constexpr int TM = 2;
     const dim3 grid((m + 32 * TM - 1) / (32 * TM), ((n >> 4) + 2 * TN - 1) / (2 * TN));
     hipLaunchKernelGGL((linear_kernel<TM, TN, ACT>), grid, dim3(FUS_THREADS), 0, st, x, ldx, m, k, w, bias, n, y, ldy);
 }
@@ -230,6 +229,14 @@ extern "C" int gp_linear(const float* x, int ldx, int m, int k, const float* w, 
 #undef GP_LIN_LDS
         return gp_check_launch("linear_lds_kernel");
     }
+    // few tokens (the GroupAll level's one token per object): 32 x 32 tiles, so that the grid still covers the
+    // chip (m = 256, n = 1024: 256 workgroups instead of 32)
+    if ((long long)((m + 63) / 64) * ((n + 127) / 128) < 256 && n % 32 == 0) {
+        if (act == 0) launch_linear<1, 0, 1>(x, ldx, m, k, w, bias, n, y, ldy, st);
+        else if (act == 1) launch_linear<1, 1, 1>(x, ldx, m, k, w, bias, n, y, ldy, st);
+        else launch_linear<1, 2, 1>(x, ldx, m, k, w, bias, n, y, ldy, st);
+        return gp_check_launch("linear_kernel");
+    }
     // output tiles per wave: the widest that divides n into whole workgroup columns
     if (n % 128 == 0) launch_linear_act<4>(act, x, ldx, m, k, w, bias, n, y, ldy, st);
     else if (n % 96 == 0) launch_linear_act<3>(act, x, ldx, m, k, w, bias, n, y, ldy, st);
@@ -256,6 +263,7 @@ struct SplitLinArgs {
     int n;
     float* y;
     int ldy;
+    unsigned* ymax;       // or null: per-row max |y| (bits of a float >= 0 order as unsigned: atomicMax)
 };
 template <int WO>
 constexpr size_t sl_lds_bytes() {
@@ -371,14 +379,26 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
     for (int j = 0; j < 4; ++j) {
         const int pc = (4 * wt + j) * 16 + nn, r = m0 + pc;
         const float u = exp2i(eT[pc] - 14 - ew);
+        float ym = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int o = (T0 + 4 * wo + i) * 16 + 4 * q;
             if (o >= a.n || r >= a.m) continue;
             f32x4 v = acc[i][j] * u + ld4(a.bias + o);
             if (ACT == 1) v = relu4(v);
-            if (ACT == 2) v = f32x4{sigmoidf(v.x), sigmoidf(v.y), sigmoidf(v.z), sigmoidf(v.w)};
+            if (ACT >= 2) v = f32x4{sigmoidf(v.x), sigmoidf(v.y), sigmoidf(v.z), sigmoidf(v.w)};
+            if (ACT == 3) {   // GatedAttentionFusion's mix: g * cur + (1 - g) * att, x = [cur | att]
+#pragma clang fp contract(off)
+                const f32x4 cu = ld4(a.x + (size_t)r * a.ldx + o), at = ld4(a.x + (size_t)r * a.ldx + a.n + o);
+                v = f32x4{v.x * cu.x + (1.0f - v.x) * at.x, v.y * cu.y + (1.0f - v.y) * at.y,
+                          v.z * cu.z + (1.0f - v.z) * at.z, v.w * cu.w + (1.0f - v.w) * at.w};
+            }
+            ym = fmaxf(ym, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
             st4(a.y + (size_t)r * a.ldy + o, v);
+        }
+        if (a.ymax) {   // one atomic per (row, wave): the max over the wave's 64 outputs of the row
+            ym = rows_max(ym);
+            if (q == 0 && r < a.m) atomicMax(a.ymax + r, __float_as_uint(ym));
         }
     }
 }
@@ -389,24 +409,30 @@ extern "C" size_t gp_linear_split_words(int n, int k) {
 }
 
 extern "C" int gp_linear_split(const float* x, int ldx, int m, int k, const int32_t* wpk, const float* bias, int n,
-                               int act, float* y, int ldy, float* rmax, hipStream_t st) {
+                               int act, float* y, int ldy, float* rmax, int flags, float* ymax, hipStream_t st) {
     GP_REQUIRE(x && wpk && bias && y && rmax && m >= 0, "linear_split: null pointer");
     GP_REQUIRE(k >= 32 && k % 32 == 0 && n >= 16 && n % 16 == 0, "linear_split: k=%d (multiple of 32), n=%d (of 16)", k, n);
     GP_REQUIRE(ldx >= k && ldy >= n && ldx % 4 == 0 && ldy % 4 == 0, "linear_split: strides ldx=%d ldy=%d", ldx, ldy);
     GP_REQUIRE(((uintptr_t)x | (uintptr_t)wpk | (uintptr_t)y | (uintptr_t)bias) % 16 == 0,
                "linear_split: pointers must be 16-byte aligned");
-    GP_REQUIRE(act >= 0 && act <= 2, "linear_split: act %d", act);
+    GP_REQUIRE(act >= 0 && act <= 3 && (flags & ~GP_LINEAR_RMAX_GIVEN) == 0, "linear_split: act %d flags %d", act, flags);
+    GP_REQUIRE(act != 3 || k == 2 * n, "linear_split: the gate mix (act 3) takes x = [cur | att], k = 2n (k=%d n=%d)", k, n);
     if (!m) return GP_OK;
-    hipLaunchKernelGGL(fus_rowmax_kernel, dim3((m + 3) / 4), dim3(256), 0, st, x, ldx, m, k, rmax);
-    FUS_TRY(gp_check_launch("fus_rowmax_kernel"));
-    SplitLinArgs a{x, ldx, m, k, rmax, wpk, bias, n, y, ldy};
+    if (!(flags & GP_LINEAR_RMAX_GIVEN)) {
+        hipLaunchKernelGGL(fus_rowmax_kernel, dim3((m + 3) / 4), dim3(256), 0, st, x, ldx, m, k, rmax);
+        FUS_TRY(gp_check_launch("fus_rowmax_kernel"));
+    }
+    if (ymax && hipMemsetAsync(ymax, 0, sizeof(float) * (size_t)m, st) != hipSuccess)
+        return gp_check_launch("linear_split ymax memset");
+    SplitLinArgs a{x, ldx, m, k, rmax, wpk, bias, n, y, ldy, reinterpret_cast<unsigned*>(ymax)};
     const int npad = (n + 127) / 128 * 128;
 #define GP_LSPLIT(WO)                                                                                              \
     {                                                                                                          \
         const dim3 grid(npad / (64 * WO), (m + 64 * (8 / WO) - 1) / (64 * (8 / WO)));                          \
         if (act == 0) hipLaunchKernelGGL((linear_split_kernel<WO, 0>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
         else if (act == 1) hipLaunchKernelGGL((linear_split_kernel<WO, 1>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
-        else hipLaunchKernelGGL((linear_split_kernel<WO, 2>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
+        else if (act == 2) hipLaunchKernelGGL((linear_split_kernel<WO, 2>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
+        else hipLaunchKernelGGL((linear_split_kernel<WO, 3>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
     }
     if (npad % 256 == 0) GP_LSPLIT(4) else GP_LSPLIT(2)
 #undef GP_LSPLIT
@@ -414,50 +440,77 @@ extern "C" int gp_linear_split(const float* x, int ldx, int m, int k, const int3
 }
 
 // ============================================================================ residual + LayerNorm
-// One wave per row (d <= 1024: up to 16 values per lane in registers), torch's biased variance.
+// L lanes per row (16 for d <= 256, else 64; up to 4 float4 per lane in registers), torch's biased variance.
+// ymax (optional): max |y| per row, for a split-arithmetic consumer (gp_linear_split's GP_LINEAR_RMAX_GIVEN).
+template <int L>
+__device__ __forceinline__ float group_sum(float v) { return L == 16 ? row16_sum(v) : wave_sum(v); }
+template <int L>
+__device__ __forceinline__ float group_max(float v) {
+    v = row16_max(v);
+    if constexpr (L == 64) v = rows_max(v);
+    return v;
+}
+template <int L>
 __global__ __launch_bounds__(FUS_THREADS) void add_layernorm_kernel(const float* x,
                                                                     const float* __restrict__ r, int m, int d,
                                                                     const float* __restrict__ gamma,
                                                                     const float* __restrict__ beta, float eps,
-                                                                    float* y) {   // y may alias x
+                                                                    float* y, float* __restrict__ ymax) {   // y may alias x
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * (FUS_THREADS / 64) + (threadIdx.x >> 6);
-    if (row >= m) return;
+    const int sub = threadIdx.x & (L - 1);
+    const int row = (int)(((long long)blockIdx.x * FUS_THREADS + threadIdx.x) / L);
+    if (row >= m) return;   // whole L-lane groups leave together
     const float* xr = x + (size_t)row * d;
     const float* rr = r + (size_t)row * d;
-    float v[16];
+    f32x4 v[4];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int c = lane + 64 * i;
-        v[i] = c < d ? xr[c] + rr[c] : 0.f;
-        s += v[i];
+    for (int i = 0; i < 4; ++i) {
+        const int c = 4 * (sub + L * i);
+        v[i] = c < d ? ld4(xr + c) + ld4(rr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     }
-    const float mean = wave_sum(s) / (float)d;
+    const float mean = group_sum<L>(s) / (float)d;
     float s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int c = lane + 64 * i;
-        const float u = c < d ? v[i] - mean : 0.f;
-        s2 += u * u;
+    for (int i = 0; i < 4; ++i) {
+        const int c = 4 * (sub + L * i);
+        if (c < d) {
+            const f32x4 u = v[i] - mean;
+            s2 += (u.x * u.x + u.y * u.y) + (u.z * u.z + u.w * u.w);
+        }
     }
-    const float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)d + eps);
+    const float rstd = 1.0f / sqrtf(group_sum<L>(s2) / (float)d + eps);
     float* yr = y + (size_t)row * d;
+    float mx = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int c = lane + 64 * i;
-        if (c < d) yr[c] = ((v[i] - mean) * rstd) * gamma[c] + beta[c];
+    for (int i = 0; i < 4; ++i) {
+        const int c = 4 * (sub + L * i);
+        if (c < d) {
+            const f32x4 o = ((v[i] - mean) * rstd) * ld4(gamma + c) + ld4(beta + c);
+            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+            st4(yr + c, o);
+        }
+    }
+    if (ymax) {
+        mx = group_max<L>(mx);
+        if (sub == 0) ymax[row] = mx;
     }
 }
 
 extern "C" int gp_add_layernorm(const float* x, const float* r, int m, int d, const float* gamma, const float* beta,
-                                float eps, float* y, hipStream_t st) {
+                                float eps, float* y, float* ymax, hipStream_t st) {
     GP_REQUIRE(x && r && gamma && beta && y && m >= 0, "add_layernorm: null pointer");
-    GP_REQUIRE(d >= 1 && d <= 1024, "add_layernorm: d=%d not in [1, 1024]", d);
+    GP_REQUIRE(d >= 4 && d <= 1024 && d % 4 == 0, "add_layernorm: d=%d not a multiple of 4 in [4, 1024]", d);
+    GP_REQUIRE(((uintptr_t)x | (uintptr_t)r | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) % 16 == 0,
+               "add_layernorm: pointers must be 16-byte aligned");
     if (!m) return GP_OK;
-    hipLaunchKernelGGL(add_layernorm_kernel, dim3((m + 3) / 4), dim3(FUS_THREADS), 0, st, x, r, m, d, gamma, beta, eps,
-                       y);
+    if (d <= 256)
+        hipLaunchKernelGGL(add_layernorm_kernel<16>, dim3((unsigned)(((long long)m * 16 + FUS_THREADS - 1) / FUS_THREADS)),
+                           dim3(FUS_THREADS), 0, st, x, r, m, d, gamma, beta, eps, y, ymax);
+    else
+        hipLaunchKernelGGL(add_layernorm_kernel<64>, dim3((m + 3) / 4), dim3(FUS_THREADS), 0, st, x, r, m, d, gamma, beta,
+                           eps, y, ymax);
     return gp_check_launch("add_layernorm_kernel");
 }
 
@@ -466,9 +519,13 @@ extern "C" int gp_add_layernorm(const float* x, const float* r, int m, int d, co
 // Linear(3,16)/ReLU/Linear(16,8), fusion Linear(16,8) over [distance | direction]. The fusion layer is
 // linear, so the host composes it with the two second layers: bias_h = A_h . hd + B_h . ho + c_h
 // (pe[512:776), composed in float64) -- 256 multiply-adds per pair instead of 384, done as packed fp32
-// FMAs over head pairs with the weights in scalar registers (uniform loads). One thread per pair, all 8
-// heads. Stored key-major, bias[b][h][j][i] (query i, key j): consecutive threads take consecutive
-// queries i, so the stores are coalesced and the attention kernel reads 16 consecutive queries per key.
+// FMAs over pairs of hidden units like the first layers (direction weights transposed at pe[776:824)). The result is the reference's
+// up to rounding order (fused multiply-adds, the composition); the distance and direction are as it
+// rounds them.
+// with the weights in scalar registers (uniform loads). One thread per pair, all 8
+// heads. Stored as the reference's relative_bias, bias[b][h][i][j] (query i, key j): consecutive threads
+// take consecutive keys j, so the stores are coalesced, and an attention lane reads its 4 consecutive
+// keys of a 16-key tile as one 16-byte load.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __restrict__ pe,
                                                                  const float* __restrict__ xyz, int n,
@@ -476,41 +533,48 @@ __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __
     const int b = blockIdx.y;
     const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
     if (e >= (long long)n * n) return;
-    const int j = (int)(e / n), i = (int)(e - (long long)j * n);
+    const int i = (int)(e / n), j = (int)(e - (long long)i * n);
     const float* pi = xyz + ((size_t)b * n + i) * 3;
     const float* pj = xyz + ((size_t)b * n + j) * 3;
-    float hd[16], ho[16];
+    float dist, dx, dy, dz;
     {
 #pragma clang fp contract(off)
         const float rx = pj[0] - pi[0], ry = pj[1] - pi[1], rz = pj[2] - pi[2];   // xyz[j] - xyz[i]
-        const float dist = sqrtf((rx * rx + ry * ry) + rz * rz);
+        dist = sqrtf((rx * rx + ry * ry) + rz * rz);
         const float den = dist + 1e-7f;
-        const float dx = rx / den, dy = ry / den, dz = rz / den;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            hd[u] = fmaxf(dist * pe[u] + pe[16 + u], 0.f);
-            const float* w = pe + 168 + 3 * u;
-            ho[u] = fmaxf(((dx * w[0] + dy * w[1]) + dz * w[2]) + pe[216 + u], 0.f);
-        }
+        dx = rx / den;
+        dy = ry / den;
+        dz = rz / den;
     }
-    const f32x2* A2 = reinterpret_cast<const f32x2*>(pe + 512);   // [u][head pair]: A[2p][u], A[2p+1][u]
+    // first layers as fused multiply-adds (bias first), hidden units u = 2 u2, 2 u2 + 1 per packed FMA
+    const f32x2* W1d = reinterpret_cast<const f32x2*>(pe);          // dist.0.w
+    const f32x2* B1d = reinterpret_cast<const f32x2*>(pe + 16);     // dist.0.b
+    const f32x2* W1o = reinterpret_cast<const f32x2*>(pe + 776);    // dir.0.w transposed: [axis][u]
+    const f32x2* B1o = reinterpret_cast<const f32x2*>(pe + 216);    // dir.0.b
+    f32x2 hd[8], ho[8];
+    const f32x2 d2 = {dist, dist}, x2 = {dx, dx}, y2 = {dy, dy}, z2 = {dz, dz};
+#pragma unroll
+    for (int u2 = 0; u2 < 8; ++u2) {
+        const f32x2 a = __builtin_elementwise_fma(d2, W1d[u2], B1d[u2]);
+        f32x2 c = __builtin_elementwise_fma(x2, W1o[u2], B1o[u2]);
+        c = __builtin_elementwise_fma(y2, W1o[8 + u2], c);
+        c = __builtin_elementwise_fma(z2, W1o[16 + u2], c);
+        hd[u2] = f32x2{fmaxf(a.x, 0.f), fmaxf(a.y, 0.f)};
+        ho[u2] = f32x2{fmaxf(c.x, 0.f), fmaxf(c.y, 0.f)};
+    }
+    // composed second layers: head h accumulates the even / odd hidden units in the two halves
+    const f32x2* A2 = reinterpret_cast<const f32x2*>(pe + 512);   // [h][u]
     const f32x2* B2 = reinterpret_cast<const f32x2*>(pe + 640);
-    const f32x2* C2 = reinterpret_cast<const f32x2*>(pe + 768);
-    f32x2 acc[4];
+    const size_t hs = (size_t)n * n;
+    float* bp = bias + (size_t)b * FUS_HEADS * hs + (size_t)i * n + j;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) acc[p] = C2[p];
+    for (int h = 0; h < FUS_HEADS; ++h) {
+        f32x2 acc = {pe[768 + h], 0.f};
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
+        for (int u2 = 0; u2 < 8; ++u2) acc = __builtin_elementwise_fma(hd[u2], A2[8 * h + u2], acc);
 #pragma unroll
-        for (int p = 0; p < 4; ++p) acc[p] = __builtin_elementwise_fma(f32x2{hd[u], hd[u]}, A2[4 * u + p], acc[p]);
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-#pragma unroll
-        for (int p = 0; p < 4; ++p) acc[p] = __builtin_elementwise_fma(f32x2{ho[u], ho[u]}, B2[4 * u + p], acc[p]);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        bias[(((size_t)b * FUS_HEADS + 2 * p) * n + j) * n + i] = acc[p].x;
-        bias[(((size_t)b * FUS_HEADS + 2 * p + 1) * n + j) * n + i] = acc[p].y;
+        for (int u2 = 0; u2 < 8; ++u2) acc = __builtin_elementwise_fma(ho[u2], B2[8 * h + u2], acc);
+        bp[h * hs] = acc.x + acc.y;
     }
 }
 
@@ -531,7 +595,8 @@ extern "C" int gp_relpe_bias(const float* pe, const float* xyz, int b, int n, fl
 // the keys in LDS chunks of KC (K row-major, V transposed), 64 keys per softmax block:
 //   S^T = K Q^T          A = K rows (keys), B = Q^T: the D tile holds keys 4q + r of query l & 15 -- which is
 //                        exactly the B-operand layout of the next product, so P never leaves registers;
-//   s = S^T / sqrt(hd) + bias (key-major bias: 16 consecutive queries per key per load), keys >= n masked;
+//   s = S^T / sqrt(hd) + bias (a lane's 4 keys are consecutive in the bias row: one 16-byte load), keys >= n
+//   masked;
 //   online softmax per query: m' = max(m, block max), O *= exp(m - m'), l = l exp(m - m') + sum exp(s - m');
 //   O^T += V^T P^T       A = V^T (dims x keys, from the transposed LDS copy), B = P^T.
 // out = O / l. Head dims are zero-padded to a multiple of 16 (12 -> 16). The grid is 1-D and XCD-aware:
@@ -565,7 +630,8 @@ __global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restric
         o[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const float inv = 1.0f / sqrtf((float)hd);
-    const float* bcol = bias ? bias + ((size_t)b * FUS_HEADS + h) * n * n + ii : nullptr;   // + key * n
+    const float* brow = bias ? bias + (((size_t)b * FUS_HEADS + h) * n + ii) * n : nullptr;   // + key
+    const bool bvec = (n & 3) == 0;   // 16-byte aligned rows
     float m = -INFINITY, lsum = 0.f;
     for (int c0 = 0; c0 < n; c0 += KC) {
         const int kn = min(KC, n - c0), k16 = (kn + 15) & ~15;
@@ -591,11 +657,15 @@ __global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restric
 #pragma unroll
             for (int u = 0; u < 4; ++u) {      // bias loads first: their latency hides under the S MFMAs
                 bv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if (bcol && u < nt) {
+                if (brow && u < nt) {
                     const int j0 = c0 + kb + 16 * u + 4 * qg;
+                    if (bvec && j0 < n) {
+                        bv[u] = ld4(brow + j0);
+                    } else {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (j0 + r < n) bv[u][r] = bcol[(size_t)(j0 + r) * n];
+                        for (int r = 0; r < 4; ++r)
+                            if (j0 + r < n) bv[u][r] = brow[j0 + r];
+                    }
                 }
             }
 #pragma unroll
@@ -674,14 +744,15 @@ extern "C" int gp_mha_attention(const float* qkv, const float* bias, int b, int 
 }
 
 // ============================================================================ gated fusion
-// F.interpolate(linear, align_corners=False) along points (upsample_linear1d's source index and lambda).
+// F.interpolate(linear, align_corners=False) along points (upsample_linear1d's source index and lambda): a
+// wave per output point, float4 channels; ymax (optional): max |y| per output row.
 __global__ __launch_bounds__(FUS_THREADS) void interp_points_kernel(const float* __restrict__ x, int n_in, int c,
-                                                                    int n_out, float* __restrict__ y) {
+                                                                    int n_out, float* __restrict__ y,
+                                                                    float* __restrict__ ymax) {
 #pragma clang fp contract(off)
-    const int b = blockIdx.y;
-    const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
-    if (e >= (long long)n_out * c) return;
-    const int o = (int)(e / c), ch = (int)(e - (long long)o * c);
+    const int b = blockIdx.y, lane = threadIdx.x & 63;
+    const int o = blockIdx.x * (FUS_THREADS / 64) + (threadIdx.x >> 6);
+    if (o >= n_out) return;
     const float scale = (float)n_in / (float)n_out;
     float src = scale * ((float)o + 0.5f) - 0.5f;
     src = src < 0.f ? 0.f : src;
@@ -691,16 +762,29 @@ __global__ __launch_bounds__(FUS_THREADS) void interp_points_kernel(const float*
     float l1 = src - (float)i0;
     l1 = fminf(fmaxf(l1, 0.f), 1.f);
     const float l0 = 1.0f - l1;
-    const float* xb = x + (size_t)b * n_in * c;
-    y[((size_t)b * n_out + o) * c + ch] = l0 * xb[(size_t)i0 * c + ch] + l1 * xb[(size_t)i1 * c + ch];
+    const float* x0 = x + ((size_t)b * n_in + i0) * c;
+    const float* x1 = x + ((size_t)b * n_in + i1) * c;
+    float* yr = y + ((size_t)b * n_out + o) * c;
+    float mx = 0.f;
+    for (int ch = 4 * lane; ch < c; ch += 256) {
+        const f32x4 a = ld4(x0 + ch), v = ld4(x1 + ch);
+        const f32x4 r = f32x4{l0 * a.x + l1 * v.x, l0 * a.y + l1 * v.y, l0 * a.z + l1 * v.z, l0 * a.w + l1 * v.w};
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w))));
+        st4(yr + ch, r);
+    }
+    if (ymax) {
+        mx = rows_max(row16_max(mx));
+        if (lane == 0) ymax[(size_t)b * n_out + o] = mx;
+    }
 }
 
-extern "C" int gp_interp_points(const float* x, int b, int n_in, int c, int n_out, float* y, hipStream_t st) {
-    GP_REQUIRE(x && y && b >= 0 && n_in >= 1 && n_out >= 1 && c >= 1, "interp_points: bad arguments");
+extern "C" int gp_interp_points(const float* x, int b, int n_in, int c, int n_out, float* y, float* ymax,
+                                hipStream_t st) {
+    GP_REQUIRE(x && y && b >= 0 && n_in >= 1 && n_out >= 1 && c >= 4 && c % 4 == 0,
+               "interp_points: bad arguments (c must be a multiple of 4)");
+    GP_REQUIRE(((uintptr_t)x | (uintptr_t)y) % 16 == 0, "interp_points: pointers must be 16-byte aligned");
     if (!b) return GP_OK;
-    const long long e = (long long)n_out * c;
-    hipLaunchKernelGGL(interp_points_kernel, dim3((unsigned)((e + FUS_THREADS - 1) / FUS_THREADS), b),
-                       dim3(FUS_THREADS), 0, st, x, n_in, c, n_out, y);
+    hipLaunchKernelGGL(interp_points_kernel, dim3((n_out + 3) / 4, b), dim3(FUS_THREADS), 0, st, x, n_in, c, n_out, y, ymax);
     return gp_check_launch("interp_points_kernel");
 }
 

@@ -32,7 +32,7 @@ from . import _lib, arch, pack, weights
 from ._lib import check
 from .device import require_device_tensor, stream_handle
 
-_ACT = {"none": 0, "relu": 1, "sigmoid": 2}
+_ACT = {"none": 0, "relu": 1, "sigmoid": 2, "gate_mix": 3}   # gate_mix: gp_linear_split only
 
 
 def _vp(t: Optional[torch.Tensor]):
@@ -42,7 +42,8 @@ def _vp(t: Optional[torch.Tensor]):
 def pack_relpe(sd: weights.StateDict, prefix: str) -> np.ndarray:
     """The 1024-float layout gp_relpe_bias reads (include/genpose_hip.h): the 504 raw parameters, then the
     fusion layer composed with the two second layers (float64, rounded once): A = Wf[:, :8] Wd2 and
-    B = Wf[:, 8:] Wo2 stored [u][head] (the kernel's packed head pairs), c = Wf [bd2; bo2] + bf."""
+    B = Wf[:, 8:] Wo2 stored [head][u], c = Wf [bd2; bo2] + bf; then the
+    direction encoder's first weight transposed to [axis][u]."""
     g = lambda k: np.asarray(sd[f"{prefix}.{k}"], np.float32).reshape(-1)  # noqa: E731
     out = np.zeros(1024, np.float32)
     parts = [g("distance_encoder.0.weight"), g("distance_encoder.0.bias"), g("distance_encoder.2.weight"),
@@ -58,9 +59,10 @@ def pack_relpe(sd: weights.StateDict, prefix: str) -> np.ndarray:
     bo2 = v[360:368].astype(np.float64)
     wf = v[368:496].reshape(h, 2 * h).astype(np.float64)
     bf = v[496:504].astype(np.float64)
-    out[512:640] = (wf[:, :h] @ wd2).T.reshape(-1)
-    out[640:768] = (wf[:, h:] @ wo2).T.reshape(-1)
+    out[512:640] = (wf[:, :h] @ wd2).reshape(-1)
+    out[640:768] = (wf[:, h:] @ wo2).reshape(-1)
     out[768:776] = wf[:, :h] @ bd2 + wf[:, h:] @ bo2 + bf
+    out[776:824] = v[168:216].reshape(hid, 3).T.reshape(-1)     # direction_encoder.0 weight as [axis][u]
     return out
 
 
@@ -148,51 +150,84 @@ class FusEncoderModel:
         return ctypes.c_void_p(stream_handle(self.device))
 
     # ------------------------------------------------------------ primitives
-    def linear(self, x: torch.Tensor, w: str, act: str = "none", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def linear(self, x: torch.Tensor, w: str, act: str = "none", out: Optional[torch.Tensor] = None,
+               rmax: Optional[torch.Tensor] = None, ymax: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """y = act(x W^T + b). Split arithmetic: ``rmax`` = x's row maxima when the producer already has
+        them; ``ymax`` (m floats) receives y's row maxima for the next linear."""
         W, b = self.t[f"{w}.w"], self.t[f"{w}.b"]
         lead, k = x.shape[:-1], x.shape[-1]
         m = int(np.prod(lead)) if lead else 1
         n = W.shape[0]
         y = torch.empty(lead + (n,), dtype=torch.float32, device=self.device) if out is None else out
-        if self.arith == "split_f16" and m >= 1024 and f"{w}.wh" in self.t:
-            if self._rmax is None or self._rmax.numel() < m:
-                self._rmax = torch.empty(m, dtype=torch.float32, device=self.device)
+        if self.split_linear(w, m):
+            flags = 0
+            if rmax is not None:
+                flags = 1
+            else:
+                if self._rmax is None or self._rmax.numel() < m:
+                    self._rmax = torch.empty(m, dtype=torch.float32, device=self.device)
+                rmax = self._rmax
             check(self.lib.gp_linear_split(_vp(x), k, m, k, _vp(self.t[f"{w}.wh"]), _vp(b), n, _ACT[act], _vp(y), n,
-                                           _vp(self._rmax), self._s()), f"linear_split {w}")
+                                           _vp(rmax), flags, _vp(ymax), self._s()), f"linear_split {w}")
         else:
             check(self.lib.gp_linear(_vp(x), k, m, k, _vp(W), _vp(b), n, _ACT[act], _vp(y), n, self._s()),
                   f"linear {w}")
         return y
 
-    def add_ln(self, x: torch.Tensor, r: torch.Tensor, name: str) -> torch.Tensor:
+    def split_linear(self, w: str, m: int) -> bool:
+        return self.arith == "split_f16" and m >= 1024 and f"{w}.wh" in self.t
+
+    def add_ln(self, x: torch.Tensor, r: torch.Tensor, name: str, ymax: Optional[torch.Tensor] = None) -> torch.Tensor:
         d = x.shape[-1]
         y = torch.empty_like(x)
         check(self.lib.gp_add_layernorm(_vp(x), _vp(r), x.numel() // d, d, _vp(self.t[f"{name}.w"]),
-                                        _vp(self.t[f"{name}.b"]), ctypes.c_float(arch.LN_EPS), _vp(y), self._s()),
-              f"add_layernorm {name}")
+                                        _vp(self.t[f"{name}.b"]), ctypes.c_float(arch.LN_EPS), _vp(y), _vp(ymax),
+                                        self._s()), f"add_layernorm {name}")
         return y
+
+    def _rowmax_buf(self, m: int, use: bool) -> Optional[torch.Tensor]:
+        return torch.empty(m, dtype=torch.float32, device=self.device) if use else None
 
     def transformer(self, lv: int, x: torch.Tensor, xyz: Optional[torch.Tensor]) -> torch.Tensor:
         """TransformerBlockWithRelativePE.forward (attention.py:505-533), eval mode."""
         B, n, d = x.shape
-        bias = None
-        if xyz is not None:
+        if n == 1 and xyz is None:
+            # one token per object (GroupAll level): softmax over one key is exactly 1, so the attention
+            # output is v itself -- only the wv rows of the fused QKV are evaluated
+            W, bq = self.t[f"tf{lv}.qkv.w"][2 * d:], self.t[f"tf{lv}.qkv.b"][2 * d:]
+            att = torch.empty_like(x)
+            check(self.lib.gp_linear(_vp(x), d, B, d, _vp(W), _vp(bq), d, 0, _vp(att), d, self._s()), "linear wv")
+        else:
+            att = self.attention(lv, x, xyz)
+        # split linears take their input's row maxima from the producer (LayerNorm, linear1's epilogue)
+        xmax = self._rowmax_buf(B * n, self.split_linear(f"tf{lv}.linear1", B * n))
+        hmax = self._rowmax_buf(B * n, self.split_linear(f"tf{lv}.linear2", B * n))
+        x1 = self.add_ln(x, self.linear(att, f"tf{lv}.wo"), f"tf{lv}.norm1", ymax=xmax)
+        f = self.linear(self.linear(x1, f"tf{lv}.linear1", "relu", rmax=xmax, ymax=hmax), f"tf{lv}.linear2", rmax=hmax)
+        return self.add_ln(x1, f, f"tf{lv}.norm2")
+
+    def attention(self, lv: int, x: torch.Tensor, xyz: Optional[torch.Tensor]) -> torch.Tensor:
+        """MultiheadAttentionWithRelativePE core (attention.py:436-488): fused QKV, relative-PE bias, heads."""
+        B, n, d = x.shape
+        qkv = self.linear(x, f"tf{lv}.qkv")
+        att = torch.empty_like(x)
+        if xyz is None:
+            check(self.lib.gp_mha_attention(_vp(qkv), None, B, n, d, _vp(att), self._s()), "mha_attention")
+        else:
             need = int(self.lib.gp_relpe_bias_bytes(B, n)) // 4
             if self._bias is None or self._bias.numel() < need:
                 self._bias = torch.empty(need, dtype=torch.float32, device=self.device)
-            bias = self._bias
-            check(self.lib.gp_relpe_bias(_vp(self.t[f"pe{lv}"]), _vp(xyz), B, n, _vp(bias), self._s()), "relpe_bias")
-        qkv = self.linear(x, f"tf{lv}.qkv")
-        att = torch.empty_like(x)
-        check(self.lib.gp_mha_attention(_vp(qkv), _vp(bias), B, n, d, _vp(att), self._s()), "mha_attention")
-        x1 = self.add_ln(x, self.linear(att, f"tf{lv}.wo"), f"tf{lv}.norm1")
-        f = self.linear(self.linear(x1, f"tf{lv}.linear1", "relu"), f"tf{lv}.linear2")
-        return self.add_ln(x1, f, f"tf{lv}.norm2")
+            check(self.lib.gp_relpe_bias(_vp(self.t[f"pe{lv}"]), _vp(xyz), B, n, _vp(self._bias), self._s()),
+                  "relpe_bias")
+            check(self.lib.gp_mha_attention(_vp(qkv), _vp(self._bias), B, n, d, _vp(att), self._s()), "mha_attention")
+        return att
 
-    def fusion(self, k: int, cur: torch.Tensor, orig: torch.Tensor) -> torch.Tensor:
-        """GatedAttentionFusion.forward (attention.py:284-325) with orig already at cur's point count."""
+    def fusion(self, k: int, cur: torch.Tensor, orig: torch.Tensor, omax: Optional[torch.Tensor] = None
+               ) -> torch.Tensor:
+        """GatedAttentionFusion.forward (attention.py:284-325) with orig already at cur's point count (omax: its
+        row maxima, when the interpolation produced them)."""
         B, n, c = cur.shape
-        ot = self.linear(orig, f"fu{k}.original_transform", "relu")
+        ot = self.linear(orig, f"fu{k}.original_transform", "relu", rmax=omax)
         gcat = torch.empty((B, n, 2 * c), dtype=torch.float32, device=self.device)
         t = self.t
         need = int(self.lib.gp_fusion_attend_workspace_size(B, n, c))
@@ -201,15 +236,19 @@ class FusEncoderModel:
         check(self.lib.gp_fusion_attend(_vp(cur), _vp(ot), B, n, c, _vp(t[f"fu{k}.ca1.w"]), _vp(t[f"fu{k}.ca1.b"]),
                                         _vp(t[f"fu{k}.ca3.w"]), _vp(t[f"fu{k}.ca3.b"]), _vp(t[f"fu{k}.sp.w"]),
                                         _vp(gcat), _vp(self._fws), self._fws.numel(), self._s()), "fusion_attend")
+        if self.split_linear(f"fu{k}.gate", B * n):   # the gate linear's epilogue does the mix
+            fmax = self._rowmax_buf(B * n, self.split_linear(f"fu{k}.output_conv", B * n))
+            fused = self.linear(gcat, f"fu{k}.gate", "gate_mix", ymax=fmax)
+            return self.linear(fused, f"fu{k}.output_conv", "relu", rmax=fmax)
         g = self.linear(gcat, f"fu{k}.gate", "sigmoid")
         fused = torch.empty_like(cur)
         check(self.lib.gp_fusion_mix(_vp(g), _vp(gcat), B * n, c, _vp(fused), self._s()), "fusion_mix")
         return self.linear(fused, f"fu{k}.output_conv", "relu")
 
-    def interp(self, x: torch.Tensor, n_out: int) -> torch.Tensor:
+    def interp(self, x: torch.Tensor, n_out: int, ymax: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, n_in, c = x.shape
         y = torch.empty((B, n_out, c), dtype=torch.float32, device=self.device)
-        check(self.lib.gp_interp_points(_vp(x), B, n_in, c, n_out, _vp(y), self._s()), "interp_points")
+        check(self.lib.gp_interp_points(_vp(x), B, n_in, c, n_out, _vp(y), _vp(ymax), self._s()), "interp_points")
         return y
 
     # ------------------------------------------------------------ forward
@@ -236,9 +275,12 @@ class FusEncoderModel:
         for lv in range(arch.N_LEVELS):
             rec = {}
             if lv > 0:
+                omax = None
                 if orig.shape[1] != feats.shape[1]:
-                    orig = self.interp(orig, feats.shape[1])
-                feats = self.fusion(lv, feats, orig)
+                    omax = self._rowmax_buf(B * feats.shape[1],
+                                            self.split_linear(f"fu{lv}.original_transform", B * feats.shape[1]))
+                    orig = self.interp(orig, feats.shape[1], ymax=omax)
+                feats = self.fusion(lv, feats, orig, omax)
                 rec["fused"] = feats
             m = arch.NPOINTS[lv] if lv < 4 else 1
             cout = arch.level_out_channels(lv)

@@ -103,32 +103,39 @@ int gp_linear(const float *x, int ldx, int m, int k, const float *w, const float
  * planes, fp32 accumulation; x scaled per row by a power of two from its max |x|). wpk: int32 words
  * [e, 0, 0, 0] + the planes of W * 2^e, rows zero-padded to a multiple of 128, in
  * genpose2_amd/fus_encoder.py pack_split_linear's layout (gp_linear_split_words(n, k) words).
- * k % 32 == 0, n % 16 == 0; rmax: m floats of device scratch (the row maxima). */
+ * k % 32 == 0, n % 16 == 0. rmax: m floats, x's row maxima max_k |x| -- computed here, or given
+ * by the caller with flags |= GP_LINEAR_RMAX_GIVEN (e.g. the ymax of the linear that produced x).
+ * ymax: NULL, or m floats that receive max |y| per row. act 3 is GatedAttentionFusion's gate with its
+ * mix (attention.py:316-320): x = [cur | att] (k = 2n), y = g * cur + (1 - g) * att with
+ * g = sigmoid(x W^T + b). */
+#define GP_LINEAR_RMAX_GIVEN 1
 size_t gp_linear_split_words(int n, int k);
 int gp_linear_split(const float *x, int ldx, int m, int k, const int32_t *wpk, const float *bias, int n,
-                    int act, float *y, int ldy, float *rmax, hipStream_t stream);
-/* y = LayerNorm(x + r) over the last dim d (gamma, beta, eps), m rows; y may alias x. */
+                    int act, float *y, int ldy, float *rmax, int flags, float *ymax, hipStream_t stream);
+/* y = LayerNorm(x + r) over the last dim d (gamma, beta, eps; d % 4 == 0), m rows; y may alias x.
+ * ymax: NULL, or m floats that receive max |y| per row. */
 int gp_add_layernorm(const float *x, const float *r, int m, int d, const float *gamma,
-                     const float *beta, float eps, float *y, hipStream_t stream);
+                     const float *beta, float eps, float *y, float *ymax, hipStream_t stream);
 /* Relative-PE bias of EfficientRelativePositionalEncoding (8 heads): xyz (b, n, 3) ->
- * bias (b, 8, n, n) KEY-MAJOR: bias[b][h][j][i] is the reference's relative_bias[b, h, i, j]
- * (query i, key j, rel = xyz[j] - xyz[i]). pe (host-packed, 1024 floats):
+ * bias (b, 8, n, n) = the reference's relative_bias[b, h, i, j] (query i, key j,
+ * rel = xyz[j] - xyz[i]). pe (host-packed, 1024 floats):
  * [0:16) dist.0.w, [16:32) dist.0.b, [32:160) dist.2.w (8x16), [160:168) dist.2.b,
  * [168:216) dir.0.w (16x3), [216:232) dir.0.b, [232:360) dir.2.w, [360:368) dir.2.b,
  * [368:496) fusion.w (8x16), [496:504) fusion.b; then the fusion layer composed with the second
- * layers: [512:640) A[u][h] = (fusion.w[:, :8] dist.2.w)[h][u], [640:768) B[u][h] likewise with
- * dir.2.w, [768:776) c = fusion.w [dist.2.b; dir.2.b] + fusion.b. */
+ * layers: [512:640) A[h][u] = (fusion.w[:, :8] dist.2.w)[h][u], [640:768) B[h][u] likewise with
+ * dir.2.w, [768:776) c = fusion.w [dist.2.b; dir.2.b] + fusion.b, [776:824) dir.0.w as [axis][u]. */
 size_t gp_relpe_bias_bytes(int b, int n);
 int gp_relpe_bias(const float *pe, const float *xyz, int b, int n, float *bias, hipStream_t stream);
 /* Multi-head attention with an additive bias (MultiheadAttentionWithRelativePE core,
  * attention.py:436-488, eval): qkv (b, n, 3d) rows [q | k | v] (heads of d/8 channels),
- * bias (b, 8, n, n) key-major as gp_relpe_bias writes it, or NULL ->
+ * bias (b, 8, n, n) [b][h][query][key] as gp_relpe_bias writes it, or NULL ->
  * out (b, n, d) = softmax(q k^T / sqrt(d/8) + bias) v per head. */
 int gp_mha_attention(const float *qkv, const float *bias, int b, int n, int d, float *out,
                      hipStream_t stream);
 /* F.interpolate(mode="linear", align_corners=False) along the point index: x (b, n_in, c) ->
- * y (b, n_out, c) (pointnet2.py:344-350). */
-int gp_interp_points(const float *x, int b, int n_in, int c, int n_out, float *y, hipStream_t stream);
+ * y (b, n_out, c) (pointnet2.py:344-350); c % 4 == 0. ymax: NULL, or b * n_out floats (max |y| per row). */
+int gp_interp_points(const float *x, int b, int n_in, int c, int n_out, float *y, float *ymax,
+                     hipStream_t stream);
 /* GatedAttentionFusion's attention stage (attention.py:298-313) per object: cur (b, n, c), ot (b, n, c)
  * (original_transform output) -> gcat (b, n, 2c) = [cur | ot * ca * sp] with ca = channel attention
  * of mean_n [cur | ot] (ca1: (2c/4, 2c) + bias, ReLU, ca3: (c, 2c/4) + bias, sigmoid) and sp =

@@ -75,7 +75,8 @@ def test_linear_vs_torch(lib, m, k, n, act, pad):
 
 @pytest.mark.parametrize("m,k,n,act,pad", [(100, 96, 288, 0, 0), (4096, 256, 1024, 1, 0), (37, 384, 96, 2, 0),
                                            (513, 1024, 192, 1, 32), (1500, 96, 288, 1, 0), (2000, 384, 96, 2, 16),
-                                           (1031, 4096, 1024, 0, 0), (4096, 1024, 4096, 1, 0), (3000, 192, 48, 0, 0)])
+                                           (1031, 4096, 1024, 0, 0), (4096, 1024, 4096, 1, 0), (3000, 192, 48, 0, 0),
+                                           (2500, 192, 96, 3, 0), (1100, 2048, 1024, 3, 16)])
 def test_linear_split_vs_torch(lib, m, k, n, act, pad):
     """gp_linear_split (split-f16 MFMA) against the fp64 linear: the split arithmetic's bound (about 3
     fp32 roundings per product) stays well inside the fused encoder's 1e-5 budget. Rows of very different
@@ -88,17 +89,32 @@ def test_linear_split_vs_torch(lib, m, k, n, act, pad):
     w = torch.randn(n, k, generator=g) / k ** 0.5
     b = torch.randn(n, generator=g)
     ref = tf.linear(x[:, :k].double(), w.double(), b.double())
-    ref = [ref, torch.relu(ref), torch.sigmoid(ref)][act]
+    if act == 3:   # the gate with GatedAttentionFusion's mix, x = [cur | att]
+        gte = torch.sigmoid(ref)
+        ref = gte * x[:, :n].double() + (1 - gte) * x[:, n:2 * n].double()
+    else:
+        ref = [ref, torch.relu(ref), torch.sigmoid(ref)][act]
     wpk = pack_split_linear(w.numpy())
     assert wpk.size == lib.gp_linear_split_words(n, k)
     y = torch.zeros(m, n + pad, device=DEV)
     xd, wd, bd = x.to(DEV), torch.from_numpy(wpk).to(DEV), b.to(DEV)
     rmax = torch.empty(m, device=DEV)
-    check(lib.gp_linear_split(_vp(xd), k + pad, m, k, _vp(wd), _vp(bd), n, act, _vp(y), n + pad, _vp(rmax), _s()),
-          "linear_split")
+    ymax = torch.full((m,), -1.0, device=DEV) if act else None
+    check(lib.gp_linear_split(_vp(xd), k + pad, m, k, _vp(wd), _vp(bd), n, act, _vp(y), n + pad, _vp(rmax), 0,
+                              _vp(ymax), _s()), "linear_split")
     torch.cuda.synchronize()
-    # per-row bound: |err| <= 4 * 2^-22 * sum_k |x||w| (+ the bias rounding)
+    if act:   # the epilogue's row maxima of y
+        assert torch.equal(ymax, y[:, :n].abs().max(1).values)
+        y2 = torch.zeros_like(y)   # the same call with the row maxima handed over
+        check(lib.gp_linear_split(_vp(xd), k + pad, m, k, _vp(wd), _vp(bd), n, act, _vp(y2), n + pad, _vp(rmax), 1,
+                                  None, _s()), "linear_split (rmax given)")
+        torch.cuda.synchronize()
+        assert torch.equal(y, y2)
+    # per-row bound: |err| <= 4 * 2^-22 * sum_k |x||w| (+ the bias rounding; the mix: times max(|cur|, |att|))
     bound = tf.linear(x[:, :k].double().abs(), w.double().abs()) * 4 * 2.0 ** -22 + 1e-7 * (1 + ref.abs())
+    if act == 3:
+        bound = bound * torch.maximum(x[:, :n].double().abs(), x[:, n:2 * n].double().abs()) + \
+            4e-7 * (x[:, :n].double().abs() + x[:, n:2 * n].double().abs())
     err = (y[:, :n].cpu().double() - ref).abs()
     assert torch.all(err <= bound), float((err / bound).max())
     assert torch.equal(rmax.cpu(), x[:, :k].abs().max(1).values)   # row maxima over the k columns read
@@ -114,11 +130,13 @@ def test_add_layernorm_vs_torch(lib):
         gam, bet = torch.rand(d, generator=g) + 0.5, torch.randn(d, generator=g) * 0.1
         ref = tf.layer_norm(x + r, (d,), gam, bet, 1e-5)
         y = torch.empty(m, d, device=DEV)
+        ymax = torch.empty(m, device=DEV)
         xd, rd, gd, bd = (t.to(DEV) for t in (x, r, gam, bet))    # held: the call only enqueues
-        check(lib.gp_add_layernorm(_vp(xd), _vp(rd), m, d, _vp(gd), _vp(bd), ctypes.c_float(1e-5), _vp(y), _s()),
-              "add_layernorm")
+        check(lib.gp_add_layernorm(_vp(xd), _vp(rd), m, d, _vp(gd), _vp(bd), ctypes.c_float(1e-5), _vp(y),
+                                   _vp(ymax), _s()), "add_layernorm")
         torch.cuda.synchronize()
         assert rel(y, ref) < 2e-6, (m, d)
+        assert torch.equal(ymax, y.abs().max(1).values)
 
 
 @pytest.mark.parametrize("n", [64, 100, 512])
@@ -136,7 +154,7 @@ def test_relpe_bias_vs_oracle(lib, fus_sd, n):
     xyz_d = torch.from_numpy(xyz).to(DEV)
     check(lib.gp_relpe_bias(_vp(pe), _vp(xyz_d), 2, n, _vp(out), _s()), "relpe_bias")
     torch.cuda.synchronize()
-    assert rel(out.transpose(2, 3), ref) < 1e-5      # stored key-major
+    assert rel(out, ref) < 1e-5
 
 
 @pytest.mark.parametrize("n,d,with_bias", [(512, 96, True), (256, 256, True), (128, 512, True), (64, 1024, True),
@@ -154,7 +172,7 @@ def test_mha_attention_vs_torch(lib, n, d, with_bias):
         s = s + bias.double()
     ref = torch.matmul(torch.softmax(s, -1), v).transpose(1, 2).reshape(B, n, d).float()
     out = torch.empty(B, n, d, device=DEV)
-    qkv_d, bias_d = qkv.to(DEV), (None if bias is None else bias.transpose(2, 3).contiguous().to(DEV))
+    qkv_d, bias_d = qkv.to(DEV), (None if bias is None else bias.to(DEV))
     check(lib.gp_mha_attention(_vp(qkv_d), _vp(bias_d), B, n, d, _vp(out), _s()), "mha_attention")
     torch.cuda.synchronize()
     assert rel(out, ref) < 2e-5
@@ -166,10 +184,12 @@ def test_interp_points_vs_torch(lib, n_in, n_out, c):
     x = torch.randn(2, n_in, c, generator=torch.Generator().manual_seed(n_in))
     ref = tf.interpolate(x.transpose(1, 2), size=n_out, mode="linear", align_corners=False).transpose(1, 2)
     y = torch.empty(2, n_out, c, device=DEV)
+    ymax = torch.empty(2 * n_out, device=DEV)
     xd = x.to(DEV)
-    check(lib.gp_interp_points(_vp(xd), 2, n_in, c, n_out, _vp(y), _s()), "interp_points")
+    check(lib.gp_interp_points(_vp(xd), 2, n_in, c, n_out, _vp(y), _vp(ymax), _s()), "interp_points")
     torch.cuda.synchronize()
     assert rel(y, ref) < 1e-6
+    assert torch.equal(ymax, y.reshape(2 * n_out, c).abs().max(1).values)
 
 
 @pytest.mark.parametrize("k", [1, 2, 3, 4])
