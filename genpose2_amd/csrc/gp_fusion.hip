@@ -606,7 +606,7 @@ extern "C" int gp_relpe_bias(const float* pe, const float* xyz, int b, int n, fl
 template <int HDP>
 __global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restrict__ qkv,
                                                           const float* __restrict__ bias, int n, int d, int hd,
-                                                          int nqb, float* __restrict__ out) {
+                                                          int nqb, float* __restrict__ out, unsigned* __restrict__ ymax) {
     constexpr int NG = HDP / 16;      // 16-deep k-groups of S, 16-row dim tiles of O
     constexpr int KC = 4096 / HDP;    // keys per LDS chunk (37 KB at every head dim)
     constexpr int KS = HDP + 4;       // K row stride (floats)
@@ -716,15 +716,25 @@ __global__ __launch_bounds__(FUS_THREADS) void mha_kernel(const float* __restric
         }
     }
     const float rl = 1.0f / rows_sum(lsum);
+    float mx = 0.f;
     if (i < n) {
         float* op = out + ((size_t)b * n + i) * d + h * hd;
 #pragma unroll
         for (int g = 0; g < NG; ++g)
-            if (16 * g + 4 * qg < hd) st4(op + 16 * g + 4 * qg, o[g] * rl);
+            if (16 * g + 4 * qg < hd) {
+                const f32x4 v = o[g] * rl;
+                mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+                st4(op + 16 * g + 4 * qg, v);
+            }
+    }
+    if (ymax) {   // the query row's max |out| over this head, merged over the 8 heads' workgroups
+        mx = rows_max(mx);
+        if (qg == 0 && i < n) atomicMax(ymax + (size_t)b * n + i, __float_as_uint(mx));
     }
 }
 
-extern "C" int gp_mha_attention(const float* qkv, const float* bias, int b, int n, int d, float* out, hipStream_t st) {
+extern "C" int gp_mha_attention(const float* qkv, const float* bias, int b, int n, int d, float* out, float* ymax,
+                                hipStream_t st) {
     GP_REQUIRE(qkv && out && b >= 0 && n >= 1, "mha_attention: bad arguments");
     GP_REQUIRE(d % (4 * FUS_HEADS) == 0, "mha_attention: d=%d must be a multiple of 32", d);
     GP_REQUIRE(((uintptr_t)qkv | (uintptr_t)out) % 16 == 0, "mha_attention: pointers must be 16-byte aligned");
@@ -733,7 +743,10 @@ extern "C" int gp_mha_attention(const float* qkv, const float* bias, int b, int 
     const int nqb = (n + 63) / 64;
     GP_REQUIRE((long long)nqb * FUS_HEADS * b < (1LL << 31), "mha_attention: grid too large");
     const dim3 grid((unsigned)(nqb * FUS_HEADS * b));
-#define GP_MHA(HDP) hipLaunchKernelGGL((mha_kernel<HDP>), grid, dim3(FUS_THREADS), 0, st, qkv, bias, n, d, hd, nqb, out)
+    if (ymax && hipMemsetAsync(ymax, 0, sizeof(float) * (size_t)b * n, st) != hipSuccess)
+        return gp_check_launch("mha_attention ymax memset");
+    unsigned* ym = reinterpret_cast<unsigned*>(ymax);
+#define GP_MHA(HDP) hipLaunchKernelGGL((mha_kernel<HDP>), grid, dim3(FUS_THREADS), 0, st, qkv, bias, n, d, hd, nqb, out, ym)
     if (hd <= 16) GP_MHA(16);
     else if (hd <= 32) GP_MHA(32);
     else if (hd <= 64) GP_MHA(64);
@@ -844,18 +857,17 @@ __global__ __launch_bounds__(FUS_THREADS) void fusion_tokstat_kernel(const float
     }
 }
 
-// Step 4: a thread per 4 channels of one token (c % 4 == 0).
+// Step 4: a wave per token (c % 4 == 0); gmax (optional): max |gcat| per token, for the gate linear.
 __global__ __launch_bounds__(FUS_THREADS) void fusion_gcat_kernel(const float* __restrict__ cur,
                                                                   const float* __restrict__ ot, int n, int c,
                                                                   const float* __restrict__ ca,
                                                                   const float* __restrict__ tstat,
                                                                   const float* __restrict__ sp_w,
-                                                                  float* __restrict__ gcat) {
+                                                                  float* __restrict__ gcat, float* __restrict__ gmax) {
 #pragma clang fp contract(off)
-    const int c4 = c >> 2, b = blockIdx.y;
-    const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
-    if (e >= (long long)n * c4) return;
-    const int t = (int)(e / c4), ch = 4 * (int)(e - (long long)t * c4);
+    const int b = blockIdx.y, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * (FUS_THREADS / 64) + (threadIdx.x >> 6);
+    if (t >= n) return;
     const float* ts = tstat + (size_t)b * n * 2;
     float sv = 0.f;
 #pragma unroll
@@ -864,11 +876,21 @@ __global__ __launch_bounds__(FUS_THREADS) void fusion_gcat_kernel(const float* _
         if (tt >= 0 && tt < n) sv += sp_w[u] * ts[2 * tt] + sp_w[7 + u] * ts[2 * tt + 1];
     }
     const float sp = sigmoidf(sv);
-    const size_t src = ((size_t)b * n + t) * c + ch;
-    const f32x4 cv = ld4(cur + src), ov = ld4(ot + src), cav = ld4(ca + (size_t)b * c + ch);
+    const size_t src = ((size_t)b * n + t) * c;
     float* g = gcat + ((size_t)b * n + t) * 2 * c;
-    st4(g + ch, cv);
-    st4(g + c + ch, f32x4{(ov.x * cav.x) * sp, (ov.y * cav.y) * sp, (ov.z * cav.z) * sp, (ov.w * cav.w) * sp});
+    float mx = 0.f;
+    for (int ch = 4 * lane; ch < c; ch += 256) {
+        const f32x4 cv = ld4(cur + src + ch), ov = ld4(ot + src + ch), cav = ld4(ca + (size_t)b * c + ch);
+        const f32x4 av = f32x4{(ov.x * cav.x) * sp, (ov.y * cav.y) * sp, (ov.z * cav.z) * sp, (ov.w * cav.w) * sp};
+        st4(g + ch, cv);
+        st4(g + c + ch, av);
+        mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(cv.x), fabsf(cv.y)), fmaxf(fabsf(cv.z), fabsf(cv.w))),
+                             fmaxf(fmaxf(fabsf(av.x), fabsf(av.y)), fmaxf(fabsf(av.z), fabsf(av.w)))));
+    }
+    if (gmax) {
+        mx = rows_max(row16_max(mx));
+        if (lane == 0) gmax[(size_t)b * n + t] = mx;
+    }
 }
 
 static size_t fus_align(size_t floats) { return (floats + 63) & ~(size_t)63; }
@@ -881,7 +903,7 @@ extern "C" size_t gp_fusion_attend_workspace_size(int b, int n, int c) {
 
 extern "C" int gp_fusion_attend(const float* cur, const float* ot, int b, int n, int c, const float* ca1_w,
                                 const float* ca1_b, const float* ca3_w, const float* ca3_b, const float* sp_w,
-                                float* gcat, void* ws, size_t ws_bytes, hipStream_t st) {
+                                float* gcat, float* gmax, void* ws, size_t ws_bytes, hipStream_t st) {
     GP_REQUIRE(cur && ot && ca1_w && ca1_b && ca3_w && ca3_b && sp_w && gcat && b >= 0, "fusion_attend: null pointer");
     GP_REQUIRE(n >= 1 && c >= 32 && c % 32 == 0, "fusion_attend: n=%d c=%d (c must be a multiple of 32)", n, c);
     GP_REQUIRE(((uintptr_t)cur | (uintptr_t)ot | (uintptr_t)gcat | (uintptr_t)ws) % 16 == 0,
@@ -900,9 +922,8 @@ extern "C" int gp_fusion_attend(const float* cur, const float* ot, int b, int n,
     FUS_TRY(gp_check_launch("fusion_tokstat_kernel"));
     FUS_TRY(gp_linear(colmean, 2 * c, b, 2 * c, ca1_w, ca1_b, c / 2, 1, hid, c / 2, st));
     FUS_TRY(gp_linear(hid, c / 2, b, c / 2, ca3_w, ca3_b, c, 2, ca, c, st));
-    const long long e = (long long)n * (c / 4);
-    hipLaunchKernelGGL(fusion_gcat_kernel, dim3((unsigned)((e + FUS_THREADS - 1) / FUS_THREADS), b), dim3(FUS_THREADS), 0,
-                       st, cur, ot, n, c, ca, tstat, sp_w, gcat);
+    hipLaunchKernelGGL(fusion_gcat_kernel, dim3((n + 3) / 4, b), dim3(FUS_THREADS), 0, st, cur, ot, n, c, ca, tstat, sp_w,
+                       gcat, gmax);
     return gp_check_launch("fusion_gcat_kernel");
 }
 

@@ -197,29 +197,34 @@ class FusEncoderModel:
             W, bq = self.t[f"tf{lv}.qkv.w"][2 * d:], self.t[f"tf{lv}.qkv.b"][2 * d:]
             att = torch.empty_like(x)
             check(self.lib.gp_linear(_vp(x), d, B, d, _vp(W), _vp(bq), d, 0, _vp(att), d, self._s()), "linear wv")
+            amax = None
         else:
-            att = self.attention(lv, x, xyz)
+            amax = self._rowmax_buf(B * n, self.split_linear(f"tf{lv}.wo", B * n))
+            att = self.attention(lv, x, xyz, amax)
         # split linears take their input's row maxima from the producer (LayerNorm, linear1's epilogue)
         xmax = self._rowmax_buf(B * n, self.split_linear(f"tf{lv}.linear1", B * n))
         hmax = self._rowmax_buf(B * n, self.split_linear(f"tf{lv}.linear2", B * n))
-        x1 = self.add_ln(x, self.linear(att, f"tf{lv}.wo"), f"tf{lv}.norm1", ymax=xmax)
+        x1 = self.add_ln(x, self.linear(att, f"tf{lv}.wo", rmax=amax), f"tf{lv}.norm1", ymax=xmax)
         f = self.linear(self.linear(x1, f"tf{lv}.linear1", "relu", rmax=xmax, ymax=hmax), f"tf{lv}.linear2", rmax=hmax)
         return self.add_ln(x1, f, f"tf{lv}.norm2")
 
-    def attention(self, lv: int, x: torch.Tensor, xyz: Optional[torch.Tensor]) -> torch.Tensor:
-        """MultiheadAttentionWithRelativePE core (attention.py:436-488): fused QKV, relative-PE bias, heads."""
+    def attention(self, lv: int, x: torch.Tensor, xyz: Optional[torch.Tensor],
+                  amax: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """MultiheadAttentionWithRelativePE core (attention.py:436-488): fused QKV, relative-PE bias, heads
+        (amax: receives the output's row maxima)."""
         B, n, d = x.shape
         qkv = self.linear(x, f"tf{lv}.qkv")
         att = torch.empty_like(x)
         if xyz is None:
-            check(self.lib.gp_mha_attention(_vp(qkv), None, B, n, d, _vp(att), self._s()), "mha_attention")
+            check(self.lib.gp_mha_attention(_vp(qkv), None, B, n, d, _vp(att), _vp(amax), self._s()), "mha_attention")
         else:
             need = int(self.lib.gp_relpe_bias_bytes(B, n)) // 4
             if self._bias is None or self._bias.numel() < need:
                 self._bias = torch.empty(need, dtype=torch.float32, device=self.device)
             check(self.lib.gp_relpe_bias(_vp(self.t[f"pe{lv}"]), _vp(xyz), B, n, _vp(self._bias), self._s()),
                   "relpe_bias")
-            check(self.lib.gp_mha_attention(_vp(qkv), _vp(self._bias), B, n, d, _vp(att), self._s()), "mha_attention")
+            check(self.lib.gp_mha_attention(_vp(qkv), _vp(self._bias), B, n, d, _vp(att), _vp(amax), self._s()),
+                  "mha_attention")
         return att
 
     def fusion(self, k: int, cur: torch.Tensor, orig: torch.Tensor, omax: Optional[torch.Tensor] = None
@@ -233,12 +238,14 @@ class FusEncoderModel:
         need = int(self.lib.gp_fusion_attend_workspace_size(B, n, c))
         if self._fws is None or self._fws.numel() < need:
             self._fws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        gmax = self._rowmax_buf(B * n, self.split_linear(f"fu{k}.gate", B * n))
         check(self.lib.gp_fusion_attend(_vp(cur), _vp(ot), B, n, c, _vp(t[f"fu{k}.ca1.w"]), _vp(t[f"fu{k}.ca1.b"]),
                                         _vp(t[f"fu{k}.ca3.w"]), _vp(t[f"fu{k}.ca3.b"]), _vp(t[f"fu{k}.sp.w"]),
-                                        _vp(gcat), _vp(self._fws), self._fws.numel(), self._s()), "fusion_attend")
+                                        _vp(gcat), _vp(gmax), _vp(self._fws), self._fws.numel(), self._s()),
+              "fusion_attend")
         if self.split_linear(f"fu{k}.gate", B * n):   # the gate linear's epilogue does the mix
             fmax = self._rowmax_buf(B * n, self.split_linear(f"fu{k}.output_conv", B * n))
-            fused = self.linear(gcat, f"fu{k}.gate", "gate_mix", ymax=fmax)
+            fused = self.linear(gcat, f"fu{k}.gate", "gate_mix", rmax=gmax, ymax=fmax)
             return self.linear(fused, f"fu{k}.output_conv", "relu", rmax=fmax)
         g = self.linear(gcat, f"fu{k}.gate", "sigmoid")
         fused = torch.empty_like(cur)

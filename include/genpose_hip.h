@@ -129,9 +129,10 @@ int gp_relpe_bias(const float *pe, const float *xyz, int b, int n, float *bias, 
 /* Multi-head attention with an additive bias (MultiheadAttentionWithRelativePE core,
  * attention.py:436-488, eval): qkv (b, n, 3d) rows [q | k | v] (heads of d/8 channels),
  * bias (b, 8, n, n) [b][h][query][key] as gp_relpe_bias writes it, or NULL ->
- * out (b, n, d) = softmax(q k^T / sqrt(d/8) + bias) v per head. */
+ * out (b, n, d) = softmax(q k^T / sqrt(d/8) + bias) v per head. ymax: NULL, or b * n floats that
+ * receive max |out| per token. */
 int gp_mha_attention(const float *qkv, const float *bias, int b, int n, int d, float *out,
-                     hipStream_t stream);
+                     float *ymax, hipStream_t stream);
 /* F.interpolate(mode="linear", align_corners=False) along the point index: x (b, n_in, c) ->
  * y (b, n_out, c) (pointnet2.py:344-350); c % 4 == 0. ymax: NULL, or b * n_out floats (max |y| per row). */
 int gp_interp_points(const float *x, int b, int n_in, int c, int n_out, float *y, float *ymax,
@@ -140,11 +141,12 @@ int gp_interp_points(const float *x, int b, int n_in, int c, int n_out, float *y
  * (original_transform output) -> gcat (b, n, 2c) = [cur | ot * ca * sp] with ca = channel attention
  * of mean_n [cur | ot] (ca1: (2c/4, 2c) + bias, ReLU, ca3: (c, 2c/4) + bias, sigmoid) and sp =
  * sigmoid(conv1d_7([max_c cur ; mean_c cur])) (sp_w: (2, 7), zero padding 3). c % 32 == 0.
- * ws: gp_fusion_attend_workspace_size(b, n, c) bytes of device scratch (the per-object statistics). */
+ * ws: gp_fusion_attend_workspace_size(b, n, c) bytes of device scratch (the per-object statistics).
+ * gmax: NULL, or b * n floats that receive max |gcat| per token. */
 size_t gp_fusion_attend_workspace_size(int b, int n, int c);
 int gp_fusion_attend(const float *cur, const float *ot, int b, int n, int c, const float *ca1_w,
                      const float *ca1_b, const float *ca3_w, const float *ca3_b, const float *sp_w,
-                     float *gcat, void *ws, size_t ws_bytes, hipStream_t stream);
+                     float *gcat, float *gmax, void *ws, size_t ws_bytes, hipStream_t stream);
 /* fused = g * cur + (1 - g) * att with cur = gcat[:, :c], att = gcat[:, c:] (attention.py:318-320):
  * g (rows, c), gcat (rows, 2c) -> out (rows, c). */
 int gp_fusion_mix(const float *g, const float *gcat, int rows, int c, float *out, hipStream_t stream);

@@ -35,7 +35,7 @@ def main():
     dev = torch.device("cuda:0")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     g = torch.Generator(device=dev).manual_seed(0)
-    pe = torch.randn(512, device=dev, generator=g) * 0.3
+    pe = torch.randn(1024, device=dev, generator=g) * 0.3   # gp_relpe_bias reads 824 floats
     res = {"B": B}
     for n, d in ((512, 96), (256, 256), (128, 512), (64, 1024)):
         qkv = torch.randn(B, n, 3 * d, device=dev, generator=g)
@@ -43,7 +43,7 @@ def main():
         bias = torch.empty(B, 8, n, n, device=dev)
         out = torch.empty(B, n, d, device=dev)
         tb = timed(lambda: check(lib.gp_relpe_bias(vp(pe), vp(xyz), B, n, vp(bias), st), "relpe"), reps)
-        ta = timed(lambda: check(lib.gp_mha_attention(vp(qkv), vp(bias), B, n, d, vp(out), st), "mha"), reps)
+        ta = timed(lambda: check(lib.gp_mha_attention(vp(qkv), vp(bias), B, n, d, vp(out), None, st), "mha"), reps)
         flops = 4.0 * B * 8 * n * n * (d // 8)
         res[f"n{n}"] = {"relpe_ms": round(tb, 4), "attn_ms": round(ta, 4),
                         "attn_tflops": round(flops / ta / 1e9, 2),

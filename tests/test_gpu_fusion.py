@@ -172,10 +172,12 @@ def test_mha_attention_vs_torch(lib, n, d, with_bias):
         s = s + bias.double()
     ref = torch.matmul(torch.softmax(s, -1), v).transpose(1, 2).reshape(B, n, d).float()
     out = torch.empty(B, n, d, device=DEV)
+    ymax = torch.full((B * n,), -1.0, device=DEV)
     qkv_d, bias_d = qkv.to(DEV), (None if bias is None else bias.to(DEV))
-    check(lib.gp_mha_attention(_vp(qkv_d), _vp(bias_d), B, n, d, _vp(out), _s()), "mha_attention")
+    check(lib.gp_mha_attention(_vp(qkv_d), _vp(bias_d), B, n, d, _vp(out), _vp(ymax), _s()), "mha_attention")
     torch.cuda.synchronize()
     assert rel(out, ref) < 2e-5
+    assert torch.equal(ymax, out.reshape(B * n, d).abs().max(1).values)
 
 
 @pytest.mark.parametrize("n_in,n_out,c", [(1024, 512, 384), (512, 256, 384), (300, 77, 40), (64, 64, 8)])
