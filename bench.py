@@ -308,6 +308,10 @@ def main():
                          "EvaluationPipeline). Config 4: 23.12 vs 22.83 "
                          "ms/step, but beside the sampler its workgroups hold CUs at ~45 of the 501 PC-step "
                          "launches per step (up to 1.1 ms each; profiles/r2/energy_overlap_ab.json)")
+    ap.add_argument("--share-geometry", type=int, default=1, choices=[0, 1],
+                    help="1 (default): the ScoreNet and EnergyNet encoders share one geometry pass per batch "
+                         "(FPS indices, centroids and ball lists of every level: gp_encoder_geometry, then "
+                         "gp_encoder_forward_geom for both); 0: each encoder computes its own")
     ap.add_argument("--dino", choices=["none", "pointwise"], default="none",
                     help="pointwise: the DINO-pointwise path for the score and energy models (ImgEncoder over synthetic "
                          "DINOv3 layers (B, 256, 384) x 3, patch gather at synthetic roi pixels, Pointnet2ClsMSGFus)")
@@ -389,6 +393,9 @@ def main():
             # the energy encoder needs only the points: overlap it with the score sampler
             # (as genpose2_amd.runner.EvaluationPipeline does)
             edata = {k: data0[k] for k in ("pts", "pts_center", "dino_layers", "roi_xs", "roi_ys") if k in data0}
+            if args.share_geometry and not pipe and args.dino == "none":
+                score.encode_geometry(data)          # one geometry pass for both encoders of this batch
+                edata["enc_geometry"] = data["enc_geometry"]
 
             def start_energy_encoder():
                 side.wait_stream(stream)
@@ -540,6 +547,8 @@ def main():
                                    f"{', DINO-pointwise fused encoders' if args.dino == 'pointwise' else ''}",
                        "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)",
                        "encoder_pipelined": bool(args.pipeline),
+                       "shared_geometry": bool(args.share_geometry and cfgd["energy"] and args.dino == "none"
+                                               and not args.pipeline),
                        "energy_encoder": (["after the sampler", "beside the sampler", "beside the score encoder"]
                                           [args.energy_overlap] if cfgd["energy"] else None)},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",

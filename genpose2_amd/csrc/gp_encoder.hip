@@ -432,51 +432,68 @@ __device__ __forceinline__ Gather0Pre split_gather0_pre(const SplitArgs& a, int 
     return Gather0Pre{a.nbr[((size_t)b * a.m + m) * a.ns + s], cc[0], cc[1], cc[2]};
 }
 
-template <int CT, int KC0>
-__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, const f32x4* w0x, int b,
-                                              int ct, int lane, const Gather0Pre pre) {
+// GH > 1: the gather of a column tile is split over GH waves by chunk (all SPLIT_WV = CT * GH waves
+// gather); their partial column maxima meet in LDS (pm, free until layer 1's epilogue) behind one
+// barrier that every wave executes, and each wave splits its own chunks at the column's exponent.
+template <int CT, int KC0, int GH>
+__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* w0x,
+                                              int b, int ct, int gh, int lane, const Gather0Pre pre) {
 #pragma clang fp contract(off)
+    constexpr int KH = KC0 / GH;
+    static_assert(KC0 % GH == 0 && (GH == 1 || CT * GH == SPLIT_WV), "gather split");
     const int q = lane >> 4, n = lane & 15;
     const int col = ct * 16 + n;
     const int p = pre.p;
     const float cx = pre.cx, cy = pre.cy, cz = pre.cz;
-    const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
-    f32x4 v[KC0][2];
+    const int c0 = gh * KH;
+    const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q + 32 * c0;
+    f32x4 v[KH][2];
 #pragma unroll
-    for (int c = 0; c < KC0; ++c) {
+    for (int c = 0; c < KH; ++c) {
         v[c][0] = ld4(qrow + 32 * c);
         v[c][1] = ld4(qrow + 32 * c + 16);
     }
     float mx = 0.f;
 #pragma unroll
-    for (int c = 0; c < KC0; ++c)
+    for (int c = 0; c < KH; ++c)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             float r[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const f32x4 w = w0x[32 * c + 16 * h + 4 * q + j];
+                const f32x4 w = w0x[32 * (c0 + c) + 16 * h + 4 * q + j];
                 r[j] = fmaxf(v[c][h][j] - ((w.x * cx + w.y * cy) + w.z * cz), 0.f);
                 mx = fmaxf(mx, r[j]);
             }
             v[c][h] = f32x4{r[0], r[1], r[2], r[3]};
         }
-    const int E = col_exponent(rows_max(mx));
+    float M = rows_max(mx);
+    if constexpr (GH > 1) {
+        if (q == 0) pm[gh * 16 * CT + col] = M;
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < GH; ++g) M = fmaxf(M, pm[g * 16 * CT + col]);
+    }
+    const int E = col_exponent(M);
     const float sc = exp2i(14 - E);
 #pragma unroll
-    for (int c = 0; c < KC0; ++c) {
+    for (int c = 0; c < KH; ++c) {
         f16x8 hi, lo;
         split_pair(v[c][0], v[c][1], sc, hi, lo);
-        X[((c * CT + ct) * 2 + 0) * 64 + lane] = hi;
-        X[((c * CT + ct) * 2 + 1) * 64 + lane] = lo;
+        X[(((c0 + c) * CT + ct) * 2 + 0) * 64 + lane] = hi;
+        X[(((c0 + c) * CT + ct) * 2 + 1) * 64 + lane] = lo;
     }
-    if (q == 0) e0s[col] = E;
+    if (q == 0 && gh == 0) e0s[col] = E;
 }
+
+// Waves that gather layer 0 (all of them when the gather is split, GH > 1).
+template <int CT, int GH>
+__device__ __forceinline__ bool split_gathers(int wid) { return GH > 1 || wid < CT; }
 
 // Layer 1 for this wave's NC output chunks (wid, wid + 8, ...): primes its weight ring, gathers layer
 // 0 (waves < CT), streams, and leaves the planes of its outputs in X (over layer 0's) plus every
 // column's exponent in e1[ct] (for lane column n). Executes the same two barriers in every wave.
-template <int CT, int KC0, int NC, int D>
+template <int CT, int KC0, int NC, int D, int GH>
 __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* w0x,
                                              int b, int col0, int wid, int lane, int oc1, int (&e1)[CT],
                                              const Gather0Pre pre) {
@@ -486,7 +503,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) pmax[ct] = 0.f;
     if constexpr (NC == 0) {
-        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, wid, lane, pre);
+        if (split_gathers<CT, GH>(wid)) split_gather0<CT, KC0, GH>(a, X, e0s, pm, w0x, b, wid % CT, wid / CT, lane, pre);
         __syncthreads();
         if (q == 0)
 #pragma unroll
@@ -515,7 +532,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
         stream_hk_step<KC0, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
-        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, wid, lane, pre);
+        if (split_gathers<CT, GH>(wid)) split_gather0<CT, KC0, GH>(a, X, e0s, pm, w0x, b, wid % CT, wid / CT, lane, pre);
         __syncthreads();
         SPLIT_MARK(a, 2);
         stream_hk_step<KC0, D, KC0 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
@@ -615,7 +632,11 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.y, col0 = blockIdx.x * C;
     SPLIT_MARK(a, 0);
-    const Gather0Pre pre = wid < CT ? split_gather0_pre(a, b, col0, wid, lane) : Gather0Pre{0, 0.f, 0.f, 0.f};
+    // layer-0 gather split over GH waves per column tile when the waves divide evenly (level 2: 4 tiles
+    // on 8 waves); level 3's 6 tiles keep one wave each
+    constexpr int GH = (SPLIT_WV % CT == 0 && KC0 % (SPLIT_WV / CT) == 0) ? SPLIT_WV / CT : 1;
+    const Gather0Pre pre = split_gathers<CT, GH>(wid) ? split_gather0_pre(a, b, col0, wid % CT, lane)
+                                                      : Gather0Pre{0, 0.f, 0.f, 0.f};
     for (int ch = tid; ch < KC0 * 32; ch += SPLIT_WV * 64)   // packed layer-0 fragment of channel ch, q = 0
         w0x[ch] = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
     __syncthreads();
@@ -625,9 +646,10 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     constexpr int NC1_HI = (OC1 + SPLIT_WV - 1) / SPLIT_WV;
     const int nc1 = wid < OC1 % SPLIT_WV || OC1 % SPLIT_WV == 0 ? NC1_HI : NC1_HI - 1;
     if (nc1 == NC1_HI)
-        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
+        split_layer1<CT, KC0, NC1_HI, D, GH>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
     else
-        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
+        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D, GH>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1,
+                                                                     pre);
     static_assert(OC2 % SPLIT_WV == 0, "layer-2 chunks spread evenly over the waves");
     split_layer2<CT, OC1, OC2 / SPLIT_WV, D>(a, X, e1, b, col0, wid, lane, OC2);
     SPLIT_MARK(a, 7);
@@ -1378,19 +1400,25 @@ static int launch_pair(SAArgs a0, SAArgs a1, int B, hipStream_t st) {
 static inline const int64_t* enc_layer(const int64_t* tab, int l, int br, int i) { return tab + ((l * 2 + br) * 3 + i) * 4; }
 
 // Per-call view of the encoder workspace (enc_layout) and the packed layer table.
+// geo: the workspace that holds (or receives) the geometry -- FPS indices, centroids, ball lists -- which
+// depends only on the points; another encoder's workspace when two models encode the same points
+// (gp_encoder_forward_geom). geo_ready: the ball lists are already there (no ball query per level).
 struct EncCtx {
     const float* wbuf;
     const int64_t* tab;
     const float* pts;
     int B, N;
     char* ws;
+    char* geo;
+    bool geo_ready;
     EncLayout L;
     int* fidx[4];
     float* nxyz[4];
     int nin[4], mout[4];
 };
 
-static EncCtx enc_ctx(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N, void* workspace) {
+static EncCtx enc_ctx(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N, void* workspace,
+                      void* geometry = nullptr) {
     EncCtx c;
     c.wbuf = wbuf;
     c.tab = layer_off;
@@ -1398,10 +1426,12 @@ static EncCtx enc_ctx(const float* wbuf, const int64_t* layer_off, const float* 
     c.B = B;
     c.N = N;
     c.ws = static_cast<char*>(workspace);
+    c.geo = geometry ? static_cast<char*>(geometry) : c.ws;
+    c.geo_ready = geometry != nullptr;
     c.L = enc_layout(B, N);
     for (int l = 0; l < 4; ++l) {
-        c.fidx[l] = reinterpret_cast<int*>(c.ws + c.L.fps[l]);
-        c.nxyz[l] = reinterpret_cast<float*>(c.ws + c.L.nxyz[l]);
+        c.fidx[l] = reinterpret_cast<int*>(c.geo + c.L.fps[l]);
+        c.nxyz[l] = reinterpret_cast<float*>(c.geo + c.L.nxyz[l]);
         c.nin[l] = l == 0 ? N : kNpoint[l - 1];
         c.mout[l] = kNpoint[l];
     }
@@ -1528,11 +1558,13 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
     int* b0 = nullptr;
     int* b1 = nullptr;
     if (l < 4) {
-        b0 = reinterpret_cast<int*>(c.ws + c.L.ball[l][0]);
-        b1 = reinterpret_cast<int*>(c.ws + c.L.ball[l][1]);
-        rc = gp_launch_ball_query2(B, n_prev, kNpoint[l], kRadius[l][0], kRadius[l][1], kNs[0], kNs[1], c.nxyz[l],
-                                   xyz_prev, b0, b1, st);
-        if (rc) return rc;
+        b0 = reinterpret_cast<int*>(c.geo + c.L.ball[l][0]);
+        b1 = reinterpret_cast<int*>(c.geo + c.L.ball[l][1]);
+        if (!c.geo_ready) {
+            rc = gp_launch_ball_query2(B, n_prev, kNpoint[l], kRadius[l][0], kRadius[l][1], kNs[0], kNs[1], c.nxyz[l],
+                                       xyz_prev, b0, b1, st);
+            if (rc) return rc;
+        }
     }
     // layer 0 once per input point for both branches (levels 0-3)
     float* qbuf = l < 4 ? reinterpret_cast<float*>(c.ws + c.L.proj[l]) : nullptr;
@@ -1792,6 +1824,45 @@ extern "C" int gp_encoder_fps(const float* pts, int B, int N, void* workspace, s
     if (rc) return rc;
     const EncCtx c = enc_ctx(nullptr, nullptr, pts, B, N, workspace);
     return gp_launch_fps_chain(pts, B, 4, c.nin, c.mout, (int* const*)c.fidx, (float* const*)c.nxyz, st);
+}
+
+// The geometry of every level in one pass: the FPS chain of all four levels, then the ball lists of both
+// radii per level. Another encoder of the same points then skips all of it (gp_encoder_forward_geom).
+extern "C" int gp_encoder_geometry(const float* pts, int B, int N, void* workspace, size_t workspace_bytes,
+                                   hipStream_t st) {
+    const float dummy = 0.f;
+    const int64_t tab = 0;
+    int rc = enc_check(&dummy, &tab, pts, B, N, workspace, workspace_bytes);
+    if (rc) return rc;
+    const EncCtx c = enc_ctx(nullptr, nullptr, pts, B, N, workspace);
+    rc = gp_launch_fps_chain(pts, B, 4, c.nin, c.mout, (int* const*)c.fidx, (float* const*)c.nxyz, st);
+    if (rc) return rc;
+    for (int l = 0; l < 4; ++l) {
+        const float* xyz_prev = l == 0 ? pts : c.nxyz[l - 1];
+        rc = gp_launch_ball_query2(B, c.nin[l], kNpoint[l], kRadius[l][0], kRadius[l][1], kNs[0], kNs[1], c.nxyz[l],
+                                   xyz_prev, reinterpret_cast<int*>(c.ws + c.L.ball[l][0]),
+                                   reinterpret_cast<int*>(c.ws + c.L.ball[l][1]), st);
+        if (rc) return rc;
+    }
+    return GP_OK;
+}
+
+// gp_encoder_forward over geometry that gp_encoder_geometry left in `geometry` (a workspace of the same
+// (B, N) layout; it may be `workspace` itself): only the per-level MLPs run, their scratch in `workspace`.
+extern "C" int gp_encoder_forward_geom(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N,
+                                       const void* geometry, void* workspace, size_t workspace_bytes, float* feat,
+                                       hipStream_t st) {
+    int rc = enc_check(wbuf, layer_off, pts, B, N, workspace, workspace_bytes);
+    if (rc) return rc;
+    GP_REQUIRE(feat && geometry, "encoder_forward_geom: null feat or geometry");
+    const EncCtx c = enc_ctx(wbuf, layer_off, pts, B, N, workspace, const_cast<void*>(geometry));
+    for (int l = 0; l < 5; ++l) {
+        const float* fprev = l == 0 ? nullptr : reinterpret_cast<const float*>(c.ws + c.L.feat[l - 1]);
+        float* out = l < 4 ? reinterpret_cast<float*>(c.ws + c.L.feat[l]) : feat;
+        rc = run_sa_level(c, l, l == 0 ? 0 : kCout[l - 1], fprev, out, false, st);
+        if (rc) return rc;
+    }
+    return GP_OK;
 }
 
 extern "C" int gp_sa_level(const float* wbuf, const int64_t* layer_off, int level, int c_prev, const float* pts, int B,

@@ -40,6 +40,14 @@ class _Uploaded:
         return self.t[k].data_ptr()
 
 
+class EncoderGeometry:
+    """Geometry of one point batch in an encoder workspace (EncoderModel.geometry): valid until that
+    model's next encoder call; ``event`` marks its completion on the producing stream."""
+
+    def __init__(self, ws: torch.Tensor, event, key):
+        self.ws, self.event, self.key = ws, event, key   # key: (points tensor address, (B, N))
+
+
 class EncoderModel:
     """Pointnet2ClsMSG(0), Light cfg, on device (gp_encoder_forward)."""
 
@@ -81,19 +89,52 @@ class EncoderModel:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def forward(self, pts: torch.Tensor, return_workspace: bool = False):
+    @staticmethod
+    def _xyz(pts: torch.Tensor) -> torch.Tensor:
         pts = require_device_tensor(pts, "pts")
-        B, N, C = pts.shape
-        if C < 3:
+        if pts.dim() != 3 or pts.shape[2] < 3:
             raise ValueError("pts must be (B, N, 3+)")
-        if C != 3:
-            pts = pts[..., :3].contiguous()
+        return pts if pts.shape[2] == 3 else pts[..., :3].contiguous()
+
+    def geometry(self, pts: torch.Tensor) -> "EncoderGeometry":
+        """FPS indices, centroids and ball lists of every level (gp_encoder_geometry) into this model's
+        workspace, for this model and any other encoder of the same points (forward(geometry=...))."""
+        key = (require_device_tensor(pts, "pts").data_ptr(), tuple(pts.shape[:2]))
+        pts = self._xyz(pts)
+        B, N, _ = pts.shape
+        ws = self.workspace(B, N)
+        check(self.lib.gp_encoder_geometry(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()),
+                                           ws.numel(), ctypes.c_void_p(stream_handle(self.device))), "encoder_geometry")
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return EncoderGeometry(ws, ev, key)
+
+    def forward(self, pts: torch.Tensor, return_workspace: bool = False,
+                geometry: Optional["EncoderGeometry"] = None):
+        """geometry: from geometry() on the same points (this model's or another encoder's); the call then
+        runs only the per-level MLPs (gp_encoder_forward_geom), after the stream waits for it."""
+        key = (require_device_tensor(pts, "pts").data_ptr(), tuple(pts.shape[:2]))
+        pts = self._xyz(pts)
+        B, N, _ = pts.shape
         feat = torch.empty((B, arch.PTS_FEAT_DIM), dtype=torch.float32, device=self.device)
         ws = self.workspace(B, N)
-        check(self.lib.gp_encoder_forward(
-            ctypes.c_void_p(self.wbuf.data_ptr()), self.offsets.ctypes.data_as(_lib.c_int64_p),
-            ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
-            ctypes.c_void_p(feat.data_ptr()), ctypes.c_void_p(stream_handle(self.device))), "encoder_forward")
+        st = ctypes.c_void_p(stream_handle(self.device))
+        if geometry is None:
+            check(self.lib.gp_encoder_forward(
+                ctypes.c_void_p(self.wbuf.data_ptr()), self.offsets.ctypes.data_as(_lib.c_int64_p),
+                ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                ctypes.c_void_p(feat.data_ptr()), st), "encoder_forward")
+        else:
+            if geometry.key != key:
+                raise ValueError("encoder geometry was computed for other points")
+            torch.cuda.current_stream(self.device).wait_event(geometry.event)
+            check(self.lib.gp_encoder_forward_geom(
+                ctypes.c_void_p(self.wbuf.data_ptr()), self.offsets.ctypes.data_as(_lib.c_int64_p),
+                ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(geometry.ws.data_ptr()),
+                ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(feat.data_ptr()), st),
+                "encoder_forward_geom")
+            if geometry.ws is not ws:
+                geometry.ws.record_stream(torch.cuda.current_stream(self.device))
         return (feat, ws) if return_workspace else feat
 
     def levels(self, b: int, n: int, ws: torch.Tensor):

@@ -63,6 +63,11 @@ class EvaluationPipeline:
             edata = {k: batch[k] for k in ("pts", "pts_center", "roi_rgb", "roi_xs", "roi_ys", "dino_layers",
                                            "point_rgb_feat") if k in batch}
 
+            # one geometry pass (FPS, centroids, ball lists of every level) for both Light encoders
+            self.score_agent.encode_geometry(data)
+            if "enc_geometry" in data:
+                edata["enc_geometry"] = data["enc_geometry"]
+
             def start_energy_encoder():   # after the score encoder, beside the sampler
                 self._side.wait_stream(main)
                 with torch.cuda.stream(self._side):

@@ -75,6 +75,17 @@ int gp_encoder_workspace_layout(int b, int n, int64_t *offsets);
 /* pts (b,n,3) un-centred points -> feat (b,1024). */
 int gp_encoder_forward(const float *wbuf, const int64_t *layer_off, const float *pts, int b, int n,
                        void *workspace, size_t workspace_bytes, float *feat, hipStream_t stream);
+/* Two models over the same points (the ScoreNet and EnergyNet encoders of one batch) share the geometry
+ * -- FPS indices, centroids and ball lists depend only on the points. gp_encoder_geometry runs the FPS
+ * chain of all four levels and the ball lists of every level into `workspace`; gp_encoder_forward_geom
+ * is gp_encoder_forward with that geometry read from `geometry` (a workspace of the same (b, n) layout
+ * that gp_encoder_geometry filled, possibly `workspace` itself) and only the per-level MLPs run, their
+ * scratch in `workspace`. Same results as gp_encoder_forward, bit for bit. */
+int gp_encoder_geometry(const float *pts, int b, int n, void *workspace, size_t workspace_bytes,
+                        hipStream_t stream);
+int gp_encoder_forward_geom(const float *wbuf, const int64_t *layer_off, const float *pts, int b, int n,
+                            const void *geometry, void *workspace, size_t workspace_bytes, float *feat,
+                            hipStream_t stream);
 /* Level-by-level form (the fused encoders, whose levels take features computed between levels):
  * gp_encoder_fps runs the FPS chain of all four levels into the workspace (fps idx + new_xyz, as
  * gp_encoder_workspace_layout places them); gp_sa_level then runs SA level `level`

@@ -128,6 +128,43 @@ def test_encoder_split_matches_f32_full_size(n, B, score_agent):
     assert not np.array_equal(out["split_f16"][0], out["f32"][0])   # the two paths differ in arithmetic
 
 
+@pytest.mark.parametrize("N", [1024, 2048])
+def test_encoder_shared_geometry_bit_exact(N, score_agent):
+    """gp_encoder_geometry + gp_encoder_forward_geom: the EnergyNet encoder over the ScoreNet encoder's
+    geometry of the same points, and the ScoreNet encoder over its own, equal the self-contained
+    gp_encoder_forward bit for bit (split-f16 and exact fp32), and the geometry equals what a forward
+    pass leaves in the workspace."""
+    from genpose2_amd import synthetic
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    energy = PoseNet(GenPoseConfig(device=DEV, agent_type="energy")).eval()
+    pts, _ = synthetic.make_batch(21, 10, N, n_unique_every=5)
+    p = torch.from_numpy(pts).to(DEV)
+    for arith in ("split_f16", "f32"):
+        for a in (score_agent, energy):
+            a.encoder.set_arith(arith)
+        ref_s, ws_s = score_agent.encoder.forward(p, return_workspace=True)
+        lv_ref = [{k: (v.clone() if torch.is_tensor(v) else [x.clone() for x in v]) for k, v in d.items()
+                   if k != "features"} for d in score_agent.encoder.levels(10, N, ws_s)]
+        ref_e = energy.encoder.forward(p)
+        data = {"pts": p}
+        score_agent.encode_geometry(data)
+        got_e = energy.encoder.forward(p, geometry=data["enc_geometry"])
+        got_s = score_agent.encoder.forward(p, geometry=data["enc_geometry"])
+        torch.cuda.synchronize()
+        assert torch.equal(got_s, ref_s) and torch.equal(got_e, ref_e), arith
+        for d0, d1 in zip(lv_ref, score_agent.encoder.levels(10, N, data["enc_geometry"].ws)):
+            for k in d0:
+                if torch.is_tensor(d0[k]):
+                    assert torch.equal(d0[k], d1[k]), k
+                else:
+                    assert all(torch.equal(x, y) for x, y in zip(d0[k], d1[k])), k
+        with pytest.raises(ValueError):
+            energy.encoder.forward(p.clone(), geometry=data["enc_geometry"])   # other points
+    for a in (score_agent, energy):
+        a.encoder.set_arith("split_f16")
+
+
 def test_encoder_batch_independence(score_agent):
     from genpose2_amd import synthetic
     pts, _ = synthetic.make_batch(5, 6, 1024, n_unique_every=4)
