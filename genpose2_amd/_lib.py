@@ -60,6 +60,8 @@ _SIGS: Dict[str, tuple] = {
     "gp_relpe_bias_bytes": (c_size_t, [c_int, c_int]),
     "gp_relpe_bias": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "gp_mha_attention": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "gp_mha_relpe_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                       c_void_p]),
     "gp_interp_points": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "gp_fusion_attend_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "gp_fusion_attend": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -432,68 +432,51 @@ __device__ __forceinline__ Gather0Pre split_gather0_pre(const SplitArgs& a, int 
     return Gather0Pre{a.nbr[((size_t)b * a.m + m) * a.ns + s], cc[0], cc[1], cc[2]};
 }
 
-// GH > 1: the gather of a column tile is split over GH waves by chunk (all SPLIT_WV = CT * GH waves
-// gather); their partial column maxima meet in LDS (pm, free until layer 1's epilogue) behind one
-// barrier that every wave executes, and each wave splits its own chunks at the column's exponent.
-template <int CT, int KC0, int GH>
-__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* w0x,
-                                              int b, int ct, int gh, int lane, const Gather0Pre pre) {
+template <int CT, int KC0>
+__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, const f32x4* w0x, int b,
+                                              int ct, int lane, const Gather0Pre pre) {
 #pragma clang fp contract(off)
-    constexpr int KH = KC0 / GH;
-    static_assert(KC0 % GH == 0 && (GH == 1 || CT * GH == SPLIT_WV), "gather split");
     const int q = lane >> 4, n = lane & 15;
     const int col = ct * 16 + n;
     const int p = pre.p;
     const float cx = pre.cx, cy = pre.cy, cz = pre.cz;
-    const int c0 = gh * KH;
-    const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q + 32 * c0;
-    f32x4 v[KH][2];
+    const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
+    f32x4 v[KC0][2];
 #pragma unroll
-    for (int c = 0; c < KH; ++c) {
+    for (int c = 0; c < KC0; ++c) {
         v[c][0] = ld4(qrow + 32 * c);
         v[c][1] = ld4(qrow + 32 * c + 16);
     }
     float mx = 0.f;
 #pragma unroll
-    for (int c = 0; c < KH; ++c)
+    for (int c = 0; c < KC0; ++c)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             float r[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const f32x4 w = w0x[32 * (c0 + c) + 16 * h + 4 * q + j];
+                const f32x4 w = w0x[32 * c + 16 * h + 4 * q + j];
                 r[j] = fmaxf(v[c][h][j] - ((w.x * cx + w.y * cy) + w.z * cz), 0.f);
                 mx = fmaxf(mx, r[j]);
             }
             v[c][h] = f32x4{r[0], r[1], r[2], r[3]};
         }
-    float M = rows_max(mx);
-    if constexpr (GH > 1) {
-        if (q == 0) pm[gh * 16 * CT + col] = M;
-        __syncthreads();
-#pragma unroll
-        for (int g = 0; g < GH; ++g) M = fmaxf(M, pm[g * 16 * CT + col]);
-    }
-    const int E = col_exponent(M);
+    const int E = col_exponent(rows_max(mx));
     const float sc = exp2i(14 - E);
 #pragma unroll
-    for (int c = 0; c < KH; ++c) {
+    for (int c = 0; c < KC0; ++c) {
         f16x8 hi, lo;
         split_pair(v[c][0], v[c][1], sc, hi, lo);
-        X[(((c0 + c) * CT + ct) * 2 + 0) * 64 + lane] = hi;
-        X[(((c0 + c) * CT + ct) * 2 + 1) * 64 + lane] = lo;
+        X[((c * CT + ct) * 2 + 0) * 64 + lane] = hi;
+        X[((c * CT + ct) * 2 + 1) * 64 + lane] = lo;
     }
-    if (q == 0 && gh == 0) e0s[col] = E;
+    if (q == 0) e0s[col] = E;
 }
-
-// Waves that gather layer 0 (all of them when the gather is split, GH > 1).
-template <int CT, int GH>
-__device__ __forceinline__ bool split_gathers(int wid) { return GH > 1 || wid < CT; }
 
 // Layer 1 for this wave's NC output chunks (wid, wid + 8, ...): primes its weight ring, gathers layer
 // 0 (waves < CT), streams, and leaves the planes of its outputs in X (over layer 0's) plus every
 // column's exponent in e1[ct] (for lane column n). Executes the same two barriers in every wave.
-template <int CT, int KC0, int NC, int D, int GH>
+template <int CT, int KC0, int NC, int D>
 __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* w0x,
                                              int b, int col0, int wid, int lane, int oc1, int (&e1)[CT],
                                              const Gather0Pre pre) {
@@ -503,7 +486,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) pmax[ct] = 0.f;
     if constexpr (NC == 0) {
-        if (split_gathers<CT, GH>(wid)) split_gather0<CT, KC0, GH>(a, X, e0s, pm, w0x, b, wid % CT, wid / CT, lane, pre);
+        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, wid, lane, pre);
         __syncthreads();
         if (q == 0)
 #pragma unroll
@@ -532,7 +515,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
         stream_hk_step<KC0, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
-        if (split_gathers<CT, GH>(wid)) split_gather0<CT, KC0, GH>(a, X, e0s, pm, w0x, b, wid % CT, wid / CT, lane, pre);
+        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, wid, lane, pre);
         __syncthreads();
         SPLIT_MARK(a, 2);
         stream_hk_step<KC0, D, KC0 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
@@ -632,11 +615,7 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.y, col0 = blockIdx.x * C;
     SPLIT_MARK(a, 0);
-    // layer-0 gather split over GH waves per column tile when the waves divide evenly (level 2: 4 tiles
-    // on 8 waves); level 3's 6 tiles keep one wave each
-    constexpr int GH = (SPLIT_WV % CT == 0 && KC0 % (SPLIT_WV / CT) == 0) ? SPLIT_WV / CT : 1;
-    const Gather0Pre pre = split_gathers<CT, GH>(wid) ? split_gather0_pre(a, b, col0, wid % CT, lane)
-                                                      : Gather0Pre{0, 0.f, 0.f, 0.f};
+    const Gather0Pre pre = wid < CT ? split_gather0_pre(a, b, col0, wid, lane) : Gather0Pre{0, 0.f, 0.f, 0.f};
     for (int ch = tid; ch < KC0 * 32; ch += SPLIT_WV * 64)   // packed layer-0 fragment of channel ch, q = 0
         w0x[ch] = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
     __syncthreads();
@@ -646,10 +625,9 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     constexpr int NC1_HI = (OC1 + SPLIT_WV - 1) / SPLIT_WV;
     const int nc1 = wid < OC1 % SPLIT_WV || OC1 % SPLIT_WV == 0 ? NC1_HI : NC1_HI - 1;
     if (nc1 == NC1_HI)
-        split_layer1<CT, KC0, NC1_HI, D, GH>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
+        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
     else
-        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D, GH>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1,
-                                                                     pre);
+        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
     static_assert(OC2 % SPLIT_WV == 0, "layer-2 chunks spread evenly over the waves");
     split_layer2<CT, OC1, OC2 / SPLIT_WV, D>(a, X, e1, b, col0, wid, lane, OC2);
     SPLIT_MARK(a, 7);

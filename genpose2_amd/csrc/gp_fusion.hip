@@ -527,19 +527,13 @@ extern "C" int gp_add_layernorm(const float* x, const float* r, int m, int d, co
 // take consecutive keys j, so the stores are coalesced, and an attention lane reads its 4 consecutive
 // keys of a 16-key tile as one 16-byte load.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __restrict__ pe,
-                                                                 const float* __restrict__ xyz, int n,
-                                                                 float* __restrict__ bias) {
-    const int b = blockIdx.y;
-    const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
-    if (e >= (long long)n * n) return;
-    const int i = (int)(e / n), j = (int)(e - (long long)i * n);
-    const float* pi = xyz + ((size_t)b * n + i) * 3;
-    const float* pj = xyz + ((size_t)b * n + j) * 3;
+// The 8 heads' bias of one pair from rel = xyz[key] - xyz[query] (shared by relpe_bias_kernel and the
+// fused mha_relpe_kernel, so both produce the same bits).
+__device__ __forceinline__ void relpe_heads(const float* __restrict__ pe, float rx, float ry, float rz,
+                                            float (&out)[FUS_HEADS]) {
     float dist, dx, dy, dz;
     {
 #pragma clang fp contract(off)
-        const float rx = pj[0] - pi[0], ry = pj[1] - pi[1], rz = pj[2] - pi[2];   // xyz[j] - xyz[i]
         dist = sqrtf((rx * rx + ry * ry) + rz * rz);
         const float den = dist + 1e-7f;
         dx = rx / den;
@@ -565,8 +559,6 @@ __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __
     // composed second layers: head h accumulates the even / odd hidden units in the two halves
     const f32x2* A2 = reinterpret_cast<const f32x2*>(pe + 512);   // [h][u]
     const f32x2* B2 = reinterpret_cast<const f32x2*>(pe + 640);
-    const size_t hs = (size_t)n * n;
-    float* bp = bias + (size_t)b * FUS_HEADS * hs + (size_t)i * n + j;
 #pragma unroll
     for (int h = 0; h < FUS_HEADS; ++h) {
         f32x2 acc = {pe[768 + h], 0.f};
@@ -574,8 +566,32 @@ __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __
         for (int u2 = 0; u2 < 8; ++u2) acc = __builtin_elementwise_fma(hd[u2], A2[8 * h + u2], acc);
 #pragma unroll
         for (int u2 = 0; u2 < 8; ++u2) acc = __builtin_elementwise_fma(ho[u2], B2[8 * h + u2], acc);
-        bp[h * hs] = acc.x + acc.y;
+        out[h] = acc.x + acc.y;
     }
+}
+
+__global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __restrict__ pe,
+                                                                 const float* __restrict__ xyz, int n,
+                                                                 float* __restrict__ bias) {
+    const int b = blockIdx.y;
+    const long long e = (long long)blockIdx.x * FUS_THREADS + threadIdx.x;
+    if (e >= (long long)n * n) return;
+    const int i = (int)(e / n), j = (int)(e - (long long)i * n);
+    const float* pi = xyz + ((size_t)b * n + i) * 3;
+    const float* pj = xyz + ((size_t)b * n + j) * 3;
+    float rx, ry, rz;
+    {
+#pragma clang fp contract(off)
+        rx = pj[0] - pi[0];   // xyz[j] - xyz[i]
+        ry = pj[1] - pi[1];
+        rz = pj[2] - pi[2];
+    }
+    float hb[FUS_HEADS];
+    relpe_heads(pe, rx, ry, rz, hb);
+    const size_t hs = (size_t)n * n;
+    float* bp = bias + (size_t)b * FUS_HEADS * hs + (size_t)i * n + j;
+#pragma unroll
+    for (int h = 0; h < FUS_HEADS; ++h) bp[h * hs] = hb[h];
 }
 
 extern "C" size_t gp_relpe_bias_bytes(int b, int n) { return sizeof(float) * (size_t)b * FUS_HEADS * n * n; }
@@ -754,6 +770,169 @@ extern "C" int gp_mha_attention(const float* qkv, const float* bias, int b, int 
     else { gp_set_error("mha_attention: head dim %d > 128", hd); return GP_ERR_UNSUPPORTED; }
 #undef GP_MHA
     return gp_check_launch("mha_kernel");
+}
+
+// ============================================================================ attention with in-register bias
+// MultiheadAttentionWithRelativePE with its EfficientRelativePositionalEncoding bias evaluated where it is
+// used: a wave owns 16 queries and ALL 8 heads, so the relative-PE MLP of a (query, key) pair is evaluated
+// once (relpe_heads, the bits gp_relpe_bias writes) for the 8 heads' score tiles that hold that pair in the
+// same lane and register -- S^T = K Q^T puts keys 4q + r of query l & 15 in lane l, register r, for every
+// head. No (B, 8, n, n) bias buffer is written or read (2.1 GB at level 0, B = 256). K / V^T of all heads
+// and the keys' xyz are staged per chunk in LDS; per 16-key tile: the 8 heads' S^T on MFMA, the 4 pairs'
+// bias on VALU (their latency under those MFMAs), one online-softmax update per head, O^T += V^T P^T.
+// Head dims <= 32 (levels 0 and 1: the levels whose n^2 made the bias buffer large).
+template <int HDP>
+__global__ __launch_bounds__(FUS_THREADS) void mha_relpe_kernel(const float* __restrict__ qkv,
+                                                                const float* __restrict__ xyz,
+                                                                const float* __restrict__ pe, int n, int d, int hd,
+                                                                int nqb, float* __restrict__ out,
+                                                                float* __restrict__ ymax) {
+    constexpr int NG = HDP / 16;
+    constexpr int KC = HDP == 16 ? 64 : 32;   // keys per LDS chunk (69 / 68 KB: two workgroups per CU)
+    constexpr int DP = FUS_HEADS * HDP;       // all heads, each padded to HDP
+    constexpr int KS = DP + 4, VS = KC + 4;
+    __shared__ __attribute__((aligned(16))) float ks[KC * KS];
+    __shared__ __attribute__((aligned(16))) float vt[DP * VS];
+    __shared__ float kx[KC * 3];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int qg = lane >> 4, nl = lane & 15;
+    const int G = gridDim.x;   // XCD-aware: the query blocks of one object on one XCD when G % 8 == 0
+    const int t = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : (int)blockIdx.x;
+    const int qb = t % nqb, b = t / nqb;
+    const size_t ld = 3 * (size_t)d;
+    const float* base = qkv + (size_t)b * n * ld;
+    const int i = qb * 64 + wid * 16 + nl;
+    const int ii = i < n ? i : n - 1;
+    const float px = xyz[((size_t)b * n + ii) * 3], py = xyz[((size_t)b * n + ii) * 3 + 1],
+                pz = xyz[((size_t)b * n + ii) * 3 + 2];
+    f32x4 qf[FUS_HEADS][NG], o[FUS_HEADS][NG];
+    float m[FUS_HEADS], lsum[FUS_HEADS];
+#pragma unroll
+    for (int h = 0; h < FUS_HEADS; ++h) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int c = 16 * g + 4 * qg;
+            qf[h][g] = c < hd ? ld4(base + (size_t)ii * ld + h * hd + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+            o[h][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        m[h] = -INFINITY;
+        lsum[h] = 0.f;
+    }
+    const float inv = 1.0f / sqrtf((float)hd);
+    for (int c0 = 0; c0 < n; c0 += KC) {
+        const int kn = min(KC, n - c0), k16 = (kn + 15) & ~15;
+        __syncthreads();
+        for (int e = threadIdx.x; e < k16 * (DP / 4); e += FUS_THREADS) {
+            const int j = e / (DP / 4), cc = 4 * (e - j * (DP / 4));
+            const int h = cc / HDP, c = cc - h * HDP;
+            f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+            if (j < kn && c < hd) {
+                const float* row = base + (size_t)(c0 + j) * ld + h * hd + c;
+                kv = ld4(row + d);
+                vv = ld4(row + 2 * d);
+            }
+            st4(ks + j * KS + cc, kv);
+            vt[(cc + 0) * VS + j] = vv.x;
+            vt[(cc + 1) * VS + j] = vv.y;
+            vt[(cc + 2) * VS + j] = vv.z;
+            vt[(cc + 3) * VS + j] = vv.w;
+        }
+        for (int e = threadIdx.x; e < kn * 3; e += FUS_THREADS) kx[e] = xyz[((size_t)b * n + c0) * 3 + e];
+        __syncthreads();
+        for (int kt = 0; kt < k16; kt += 16) {
+            f32x4 s[FUS_HEADS];
+#pragma unroll
+            for (int h = 0; h < FUS_HEADS; ++h) {
+                s[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const float* kr = ks + (kt + nl) * KS + h * HDP + 4 * qg;
+#pragma unroll
+                for (int g = 0; g < NG; ++g) s[h] = mfma_kgroup(ld4(kr + 16 * g), qf[h][g], s[h]);
+            }
+            float bb[4][FUS_HEADS];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = kt + 4 * qg + r;
+                if (j < kn) {
+                    float rx, ry, rz;
+                    {
+#pragma clang fp contract(off)
+                        rx = kx[3 * j] - px;   // xyz[key] - xyz[query]
+                        ry = kx[3 * j + 1] - py;
+                        rz = kx[3 * j + 2] - pz;
+                    }
+                    relpe_heads(pe, rx, ry, rz, bb[r]);
+                } else {
+#pragma unroll
+                    for (int h = 0; h < FUS_HEADS; ++h) bb[r][h] = 0.f;
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < FUS_HEADS; ++h) {
+                float bm = -INFINITY;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v;
+                    {
+#pragma clang fp contract(off)
+                        v = s[h][r] * inv + bb[r][h];
+                    }
+                    s[h][r] = kt + 4 * qg + r < kn ? v : -INFINITY;
+                    bm = fmaxf(bm, s[h][r]);
+                }
+                const float mn = fmaxf(m[h], rows_max(bm));
+                const float alpha = __expf(m[h] - mn);
+                m[h] = mn;
+                float ps = 0.f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    s[h][r] = __expf(s[h][r] - mn);
+                    ps += s[h][r];
+                }
+                lsum[h] = lsum[h] * alpha + ps;
+                const float* vr = vt + (h * HDP + nl) * VS + kt + 4 * qg;
+#pragma unroll
+                for (int g = 0; g < NG; ++g) o[h][g] = mfma_kgroup(ld4(vr + 16 * g * VS), s[h], o[h][g] * alpha);
+            }
+        }
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int h = 0; h < FUS_HEADS; ++h) {
+        const float rl = 1.0f / rows_sum(lsum[h]);
+        if (i < n) {
+            float* op = out + ((size_t)b * n + i) * d + h * hd;
+#pragma unroll
+            for (int g = 0; g < NG; ++g)
+                if (16 * g + 4 * qg < hd) {
+                    const f32x4 v = o[h][g] * rl;
+                    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+                    st4(op + 16 * g + 4 * qg, v);
+                }
+        }
+    }
+    if (ymax) {   // this wave holds the query's whole row (all heads)
+        mx = rows_max(mx);
+        if (qg == 0 && i < n) ymax[(size_t)b * n + i] = mx;
+    }
+}
+
+extern "C" int gp_mha_relpe_attention(const float* qkv, const float* xyz, const float* pe, int b, int n, int d,
+                                      float* out, float* ymax, hipStream_t st) {
+    GP_REQUIRE(qkv && xyz && pe && out && b >= 0 && n >= 1, "mha_relpe_attention: bad arguments");
+    GP_REQUIRE(d % (4 * FUS_HEADS) == 0 && d / FUS_HEADS <= 32,
+               "mha_relpe_attention: d=%d (head dims that are multiples of 4, up to 32)", d);
+    GP_REQUIRE(((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)pe) % 16 == 0,
+               "mha_relpe_attention: pointers must be 16-byte aligned");
+    if (!b) return GP_OK;
+    const int hd = d / FUS_HEADS;
+    const int nqb = (n + 63) / 64;
+    GP_REQUIRE((long long)nqb * b < (1LL << 31), "mha_relpe_attention: grid too large");
+    const dim3 grid((unsigned)(nqb * b));
+    if (hd <= 16)
+        hipLaunchKernelGGL((mha_relpe_kernel<16>), grid, dim3(FUS_THREADS), 0, st, qkv, xyz, pe, n, d, hd, nqb, out, ymax);
+    else
+        hipLaunchKernelGGL((mha_relpe_kernel<32>), grid, dim3(FUS_THREADS), 0, st, qkv, xyz, pe, n, d, hd, nqb, out, ymax);
+    return gp_check_launch("mha_relpe_kernel");
 }
 
 // ============================================================================ gated fusion

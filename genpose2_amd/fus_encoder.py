@@ -123,6 +123,7 @@ class FusEncoderModel:
         self._bias: Optional[torch.Tensor] = None
         self._fws: Optional[torch.Tensor] = None
         self._rmax: Optional[torch.Tensor] = None
+        self.fused_bias = os.environ.get("GENPOSE2_FUSED_RELPE", "1") == "1"
         self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
 
     @property
@@ -217,6 +218,12 @@ class FusEncoderModel:
         att = torch.empty_like(x)
         if xyz is None:
             check(self.lib.gp_mha_attention(_vp(qkv), None, B, n, d, _vp(att), _vp(amax), self._s()), "mha_attention")
+        elif d // arch.FUS_HEADS <= 16 and self.fused_bias:
+            # level 0: the bias evaluated in the attention kernel's registers (no (B, 8, n, n) buffer, 2.1 GB
+            # at B=256); at level 1 (head dim 32) the kernel holds one wave per SIMD and the two-kernel path
+            # is faster (0.45 vs 0.73 ms)
+            check(self.lib.gp_mha_relpe_attention(_vp(qkv), _vp(xyz), _vp(self.t[f"pe{lv}"]), B, n, d, _vp(att),
+                                                  _vp(amax), self._s()), "mha_relpe_attention")
         else:
             need = int(self.lib.gp_relpe_bias_bytes(B, n)) // 4
             if self._bias is None or self._bias.numel() < need:

@@ -144,6 +144,11 @@ int gp_relpe_bias(const float *pe, const float *xyz, int b, int n, float *bias, 
  * receive max |out| per token. */
 int gp_mha_attention(const float *qkv, const float *bias, int b, int n, int d, float *out,
                      float *ymax, hipStream_t stream);
+/* gp_relpe_bias + gp_mha_attention in one kernel, the bias evaluated per (query, key) pair in registers
+ * (no (b, 8, n, n) buffer): qkv as gp_mha_attention, xyz (b, n, 3), pe as gp_relpe_bias. Head dims
+ * d / 8 <= 32 (the fused encoder's levels 0 and 1). ymax: NULL or b * n floats (max |out| per token). */
+int gp_mha_relpe_attention(const float *qkv, const float *xyz, const float *pe, int b, int n, int d,
+                           float *out, float *ymax, hipStream_t stream);
 /* F.interpolate(mode="linear", align_corners=False) along the point index: x (b, n_in, c) ->
  * y (b, n_out, c) (pointnet2.py:344-350); c % 4 == 0. ymax: NULL, or b * n_out floats (max |y| per row). */
 int gp_interp_points(const float *x, int b, int n_in, int c, int n_out, float *y, float *ymax,

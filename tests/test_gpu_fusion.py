@@ -180,6 +180,32 @@ def test_mha_attention_vs_torch(lib, n, d, with_bias):
     assert torch.equal(ymax, out.reshape(B * n, d).abs().max(1).values)
 
 
+@pytest.mark.parametrize("n,d", [(512, 96), (256, 256), (77, 96), (130, 256), (1, 96)])
+def test_mha_relpe_attention_matches_two_kernel_path(lib, fus_sd, n, d):
+    """gp_mha_relpe_attention (bias in registers) against gp_relpe_bias + gp_mha_attention on the same
+    inputs: the same bias bits, so only the softmax blocking differs (2e-6), and the row maxima."""
+    from genpose2_amd._lib import check
+    from genpose2_amd.fus_encoder import pack_relpe
+    B = 3
+    g = torch.Generator().manual_seed(n * 7 + d)
+    qkv = torch.randn(B, n, 3 * d, generator=g).to(DEV)
+    xyz = (torch.rand(B, n, 3, generator=g) * 0.2 - 0.1).to(DEV)
+    if n > 5:
+        xyz[1, 5] = xyz[1, 3]                          # a duplicate point
+    pe = torch.from_numpy(pack_relpe(fus_sd, "pts_encoder.relative_pos_encoders.0")).to(DEV)
+    bias = torch.empty(B, 8, n, n, device=DEV)
+    ref = torch.empty(B, n, d, device=DEV)
+    out = torch.empty(B, n, d, device=DEV)
+    ymax = torch.full((B * n,), -1.0, device=DEV)
+    check(lib.gp_relpe_bias(_vp(pe), _vp(xyz), B, n, _vp(bias), _s()), "relpe_bias")
+    check(lib.gp_mha_attention(_vp(qkv), _vp(bias), B, n, d, _vp(ref), None, _s()), "mha_attention")
+    check(lib.gp_mha_relpe_attention(_vp(qkv), _vp(xyz), _vp(pe), B, n, d, _vp(out), _vp(ymax), _s()),
+          "mha_relpe_attention")
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 2e-6
+    assert torch.equal(ymax, out.reshape(B * n, d).abs().max(1).values)
+
+
 @pytest.mark.parametrize("n_in,n_out,c", [(1024, 512, 384), (512, 256, 384), (300, 77, 40), (64, 64, 8)])
 def test_interp_points_vs_torch(lib, n_in, n_out, c):
     from genpose2_amd._lib import check
