@@ -42,9 +42,11 @@ __device__ __forceinline__ f32x4 mfma_kgroup(const f32x4 a, const f32x4 b, f32x4
     return c;
 }
 
-__device__ __forceinline__ f32x4 relu4(f32x4 v) {
-    return f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
-}
+// max(v, 0) as one instruction (v_maximum3_f32 v, 0, 0): fmaxf on a value the compiler cannot prove canonical (an MFMA or
+// load result) is preceded by a v_max_f32 v, v, v that quiets signalling NaNs, doubling every ReLU.
+// IEEE maximum needs no quieting; it propagates NaN as torch.relu does (fmaxf maps NaN to 0).
+__device__ __forceinline__ float relu1(float v) { return __builtin_elementwise_maximum(v, 0.f); }
+__device__ __forceinline__ f32x4 relu4(f32x4 v) { return f32x4{relu1(v.x), relu1(v.y), relu1(v.z), relu1(v.w)}; }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
@@ -118,8 +120,10 @@ __device__ __forceinline__ float wave_sum(float v) { return rows_sum(row16_sum(v
 // max over the 16 lanes of each row, DPP only (no ds_bpermute round trip through LDS)
 template <int CTRL>
 __device__ __forceinline__ float dpp_max(float v) {
-    // every source lane of these patterns exists, so bound_ctrl never applies; it lets the DPP fold into v_max
-    return fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true)));
+    // every source lane of these patterns exists, so bound_ctrl never applies. IEEE maximum: a DPP move
+    // plus one v_maximum3_f32; fmaxf folded the DPP into v_max but quieted both operands first (four
+    // instructions per level on MFMA outputs)
+    return __builtin_elementwise_maximum(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true)));
 }
 __device__ __forceinline__ float row16_max(float v) {
     v = dpp_max<0xB1>(v);

@@ -217,7 +217,8 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
 #pragma unroll
                     for (int u = 1; u < SPAN; ++u) {
                         const f32x4 w2 = relu4(acc[t][cb + u] + bias);
-                        v = f32x4{fmaxf(v.x, w2.x), fmaxf(v.y, w2.y), fmaxf(v.z, w2.z), fmaxf(v.w, w2.w)};
+                        v = f32x4{__builtin_elementwise_maximum(v.x, w2.x), __builtin_elementwise_maximum(v.y, w2.y),
+                                  __builtin_elementwise_maximum(v.z, w2.z), __builtin_elementwise_maximum(v.w, w2.w)};
                     }
                     v = row16_max4(v);
                     const int colc = col0 + (cbase + cb) * 16;
@@ -291,8 +292,7 @@ __device__ __forceinline__ void sa_gather0(const SAArgs& a, f32x4* lds, int b, i
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if (ok[ct]) {
                 const f32x4 c4 = ld4(cx + mcol[ct] * H0p + 16 * T + 4 * q);
-                v = f32x4{fmaxf(qv[u].x - c4.x, 0.f), fmaxf(qv[u].y - c4.y, 0.f), fmaxf(qv[u].z - c4.z, 0.f),
-                          fmaxf(qv[u].w - c4.w, 0.f)};
+                v = relu4(qv[u] - c4);
             }
             lds[(T * CT + ct) * 64 + lane] = v;
         }
@@ -404,9 +404,12 @@ struct SplitArgs {
     int tag;                          // level * 2 + branch (tuning traces)
 };
 
-__device__ __forceinline__ float max4(f32x4 v) { return fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)); }
+// IEEE maximum (v_maximum3_f32: no quieting of non-canonical MFMA outputs first, three operands per
+// instruction); equal to fmaxf for every non-NaN value
+__device__ __forceinline__ float fmax2(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float max4(f32x4 v) { return fmax2(fmax2(fmax2(v.x, v.y), v.z), v.w); }
 __device__ __forceinline__ f32x4 vmax4(f32x4 a, f32x4 b) {
-    return f32x4{fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)};
+    return f32x4{fmax2(a.x, b.x), fmax2(a.y, b.y), fmax2(a.z, b.z), fmax2(a.w, b.w)};
 }
 // Max-pooling before the bias and ReLU: x -> relu(x + b) is monotonic and rounding is monotonic, so
 // relu(max_n x_n + b) equals max_n relu(x_n + b) bit for bit -- the pools take the max of the unscaled
@@ -456,8 +459,8 @@ __device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int*
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const f32x4 w = w0x[32 * c + 16 * h + 4 * q + j];
-                r[j] = fmaxf(v[c][h][j] - ((w.x * cx + w.y * cy) + w.z * cz), 0.f);
-                mx = fmaxf(mx, r[j]);
+                r[j] = relu1(v[c][h][j] - ((w.x * cx + w.y * cy) + w.z * cz));
+                mx = fmax2(mx, r[j]);
             }
             v[c][h] = f32x4{r[0], r[1], r[2], r[3]};
         }
@@ -527,7 +530,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
             for (int t = 0; t < 2 * NC; ++t) {
                 acc[t][ct] = relu4(acc[t][ct] * u + ld4(a.bias[0] + 16 * T[t] + 4 * q));
-                pmax[ct] = fmaxf(pmax[ct], max4(acc[t][ct]));
+                pmax[ct] = fmax2(pmax[ct], max4(acc[t][ct]));
             }
         }
 #pragma unroll
@@ -789,7 +792,7 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
             for (int g = 0; g < KG1; ++g) {
                 float r[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) r[j] = fmaxf(fsub(cur.q[ct][g][j], cw[g][j]), 0.f);
+                for (int j = 0; j < 4; ++j) r[j] = relu1(fsub(cur.q[ct][g][j], cw[g][j]));
                 bf[g] = f32x4{r[0], r[1], r[2], r[3]};
             }
             f32x4 acc1[NT1];
@@ -890,8 +893,8 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
                 float r[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    r[j] = fmaxf(fsub(cur.q[ct][g][j], cw[g][j]), 0.f);
-                    mx = fmaxf(mx, r[j]);
+                    r[j] = relu1(fsub(cur.q[ct][g][j], cw[g][j]));
+                    mx = fmax2(mx, r[j]);
                 }
                 bf[g] = f32x4{r[0], r[1], r[2], r[3]};
             }
@@ -919,7 +922,7 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
 #pragma unroll
             for (int t = 0; t < NT1; ++t) {
                 acc1[t] = relu4(acc1[t] * u0 + ld4(&sB1[16 * t + 4 * q]));
-                m1 = fmaxf(m1, fmaxf(fmaxf(acc1[t].x, acc1[t].y), fmaxf(acc1[t].z, acc1[t].w)));
+                m1 = fmax2(m1, max4(acc1[t]));
             }
             const int E1 = col_exponent(rows_max(m1));
             f16x8 h1[KC1], l1[KC1];
@@ -1211,7 +1214,7 @@ __global__ __launch_bounds__(TG_THREADS) void tok_split_gemm_kernel(TokArgs a) {
                 f32x4 v = acc[i][j] * u + ld4(bias + o);
                 if constexpr (MODE == 0) {
                     v = relu4(v);
-                    cm = fmaxf(cm, max4(v));
+                    cm = fmax2(cm, max4(v));
                 }
                 if (r < a.M) st4(a.y + (size_t)r * a.ldy + a.ycol[br] + o, v);
             }

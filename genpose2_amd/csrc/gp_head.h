@@ -40,7 +40,12 @@ struct HeadSmem {
     float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
     f32x4 act1[KG_HID * NT * 64];      // pose_encoder.0 output, accumulator-native [g][ct][lane]
     f32x4 act2[kAliasAct ? 4 : KG_HID * NT * 64];   // pose_encoder.2 output (act1 when aliased)
-    float red[NT * 16][9][WV];         // per-wave head-layer-2 partials, wave-minor (head_out reads a row)
+    // per-wave head-layer-2 partials, wave-minor (head_out reads a row), indexed [v][n][wave] by the
+    // value v = (head * NT + column tile) * 3 + output and the column n within the tile: the order the
+    // split trunk's reduce-scatter leaves them in (row q of the wave holds values 4g + q); padded to
+    // whole groups of four values
+    static constexpr int kRedV = (9 * NT + 3) / 4 * 4;
+    float red[kRedV][16][WV];
     float xu[NT * 16 * 9];             // PC: last-step mean rows, gathered for the quaternion
     float scratch[WV * 64];
     // small per-launch weights staged once per workgroup (their loads overlap the PC update)
@@ -71,9 +76,11 @@ __device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, He
 // Head output o of column c (valid after head_trunk): bias + the per-wave partials in wave order.
 template <int NT, int WV>
 __device__ __forceinline__ float head_out(const HeadSmem<NT, WV>& sm, int c, int o) {
+    const int h = o / 3;
+    const int v = (h * NT + (c >> 4)) * 3 + (o - 3 * h);
     float acc = 0.f;
 #pragma unroll
-    for (int v = 0; v < WV; ++v) acc += sm.red[c][o][v];
+    for (int w = 0; w < WV; ++w) acc += sm.red[v][c & 15][w];
     return sm.h2b[o] + acc;
 }
 
@@ -241,9 +248,9 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
             p1 = rows_sum(p1);
             p2 = rows_sum(p2);
             if (q == 0) {
-                sm.red[ct * 16 + n][h * 3 + 0][wid] = p0;
-                sm.red[ct * 16 + n][h * 3 + 1][wid] = p1;
-                sm.red[ct * 16 + n][h * 3 + 2][wid] = p2;
+                sm.red[(h * NT + ct) * 3 + 0][n][wid] = p0;
+                sm.red[(h * NT + ct) * 3 + 1][n][wid] = p1;
+                sm.red[(h * NT + ct) * 3 + 2][n][wid] = p2;
             }
         }
     }
@@ -393,6 +400,72 @@ __device__ __forceinline__ SplitScalars load_split_scalars(const gp_head_weights
     return r;
 }
 
+// Sums of four values over the four 16-lane rows, scattered: on return row q of the wave holds the
+// total of value q (its column n's sum over lanes n, n+16, n+32, n+48). Three row swaps and three adds
+// for four values (a full row sum of each would take eight and eight); the pairs are summed in
+// rows_sum's order, (r0 + r1) + (r2 + r3), so each total has rows_sum's bits.
+// v_permlane16_swap exchanges the odd rows of its first operand with the even rows of its second;
+// v_permlane32_swap the upper half of the first with the lower half of the second.
+__device__ __forceinline__ float rows_sum_scatter4(float a, float b, float c, float d) {
+    const auto ab = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    const auto cd = __builtin_amdgcn_permlane16_swap(__float_as_uint(c), __float_as_uint(d), false, false);
+    const float s = __uint_as_float(ab[0]) + __uint_as_float(ab[1]);   // rows: a01, b01, a23, b23
+    const float t = __uint_as_float(cd[0]) + __uint_as_float(cd[1]);   // rows: c01, d01, c23, d23
+    const auto st = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(t), false, false);
+    return __uint_as_float(st[0]) + __uint_as_float(st[1]);            // rows: a, b, c, d
+}
+
+// ReLU -> head layer 2 (block diagonal 3 x (256 -> 3)) partials of the split trunk's head-layer-1
+// accumulators (scaled domain; uh[ct] undoes the scale, a power of two, so scaling each lane's chain
+// before the row sum is exact). Each (column, output) is one fp32 FMA chain over this wave's channels,
+// t-major then j, with separately rounded sums across rows and waves (head_out). Scalar FMAs: the
+// same chains as v_pk_fma_f32 over column-tile pairs (broadcast weights through op_sel, results in
+// place) summed wrong values into the even column tiles of a fraction of the workgroups.
+template <int NT, int WV>
+__device__ __forceinline__ void head_l2_split(const f32x4 (&acc)[3 * (16 / WV)][NT], HeadSmem<NT, WV>& sm,
+                                              const float (&uh)[NT], int wid, int lane) {
+    constexpr int TPW = 16 / WV;
+    constexpr int NV = 9 * NT, NG = HeadSmem<NT, WV>::kRedV / 4;
+    const int q = lane >> 4, n = lane & 15;
+    // nothing of this phase is scheduled into the head-layer-1 MFMA stream: interleaved there, the
+    // row swaps below reused registers the in-flight MFMAs still read (v_permlane*_swap writes both of
+    // its operands) and a fraction of the workgroups summed stale values
+    __builtin_amdgcn_sched_barrier(0);
+    float pv[4 * NG];
+#pragma unroll
+    for (int v = NV; v < 4 * NG; ++v) pv[v] = 0.f;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+        float p[NT][3];
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) p[ct][0] = p[ct][1] = p[ct][2] = 0.f;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const int ch = 16 * (wid * TPW + t) + 4 * q;
+            const f32x4 w0 = ld4(&sm.h2w[(h * 3 + 0) * HID + ch]);
+            const f32x4 w1 = ld4(&sm.h2w[(h * 3 + 1) * HID + ch]);
+            const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) {
+                const f32x4 u = relu4(acc[h * TPW + t][ct]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    p[ct][0] = __builtin_fmaf(u[j], w0[j], p[ct][0]);
+                    p[ct][1] = __builtin_fmaf(u[j], w1[j], p[ct][1]);
+                    p[ct][2] = __builtin_fmaf(u[j], w2[j], p[ct][2]);
+                }
+            }
+        }
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+            for (int o = 0; o < 3; ++o) pv[(h * NT + ct) * 3 + o] = p[ct][o] * uh[ct];
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+        sm.red[4 * g + q][n][wid] = rows_sum_scatter4(pv[4 * g], pv[4 * g + 1], pv[4 * g + 2], pv[4 * g + 3]);
+}
+
 // head_trunk with the split-f16 GEMMs (same contract and phases; pose_encoder.0 and layer 2 stay fp32).
 template <int NT, int WV>
 __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const float* __restrict__ pobj,
@@ -446,14 +519,22 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
         sh[ct] = exp2i(14 - e2 + ewh);   // head layer 1's fp32 init (pts + t blocks) in the scaled domain
     }
     // head layer 1's fp32 init (pts + t blocks): first touch of pobj / tproj after the kernel
-    // boundary, so issued here, a whole pose_encoder.0 + .2 ahead of its use
+    // boundary, so issued here, a whole pose_encoder.0 + .2 ahead of its use. Buffer loads: one
+    // 32-bit lane offset per column tile, the output tile's offset wave-uniform (SGPR), instead of a
+    // 64-bit address per load
     f32x4 tpv[3 * TPW], pov[3 * TPW][NT];
+    {
+        const __amdgpu_buffer_rsrc_t RP = make_rsrc(pobj, 0x7ffffff0u), RT = make_rsrc(tproj, 3 * HID * 4);
+        int vo[NT];
 #pragma unroll
-    for (int i = 0; i < 3 * TPW; ++i) {
-        const int T = TH[i];
-        tpv[i] = ld4(tproj + 16 * T + 4 * q);
+        for (int ct = 0; ct < NT; ++ct) vo[ct] = obj_of_col[ct * 16 + n] * (3 * HID * 4) + 16 * q;
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ld4(pobj + (size_t)obj_of_col[ct * 16 + n] * (3 * HID) + 16 * T + 4 * q);
+        for (int i = 0; i < 3 * TPW; ++i) {
+            const int T = TH[i];
+            tpv[i] = ldbuf4(RT, 16 * q, 64 * T);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ldbuf4(RP, vo[ct], 64 * T);
+        }
     }
     // ---- pose_encoder.0 (9 -> 256) in fp32, one k-group; ReLU, scale, split into the chunk planes
 #pragma unroll
@@ -502,45 +583,12 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     // ---- head layer 1 (pose block 256 -> 3x256)
     stream_h_step<DH, KC_HID + DH, 3 * TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc);
     PC_MARK(5);
-    // ---- ReLU -> head layer 2 partial dot products (fp32 VALU, one FMA chain per output: at 64
-    //      candidates this is the PC step's longest serial phase, ~1000 instructions per wave with
-    //      separately rounded products and sums; fp32 MFMAs for it measured slower, 10.1k vs 8.1k cycles)
-#pragma unroll
-    for (int h = 0; h < 3; ++h) {
-        float p[NT][3];
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) p[ct][0] = p[ct][1] = p[ct][2] = 0.f;
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {   // each weight fragment read once for all column tiles
-            const int ch = 16 * (wid * TPW + t) + 4 * q;
-            const f32x4 w0 = ld4(&sm.h2w[(h * 3 + 0) * HID + ch]);
-            const f32x4 w1 = ld4(&sm.h2w[(h * 3 + 1) * HID + ch]);
-            const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
-#pragma unroll
-            for (int ct = 0; ct < NT; ++ct) {
-                const f32x4 u = relu4(acc[h * TPW + t][ct]);   // still in the scaled domain
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    p[ct][0] = __builtin_fmaf(u[j], w0[j], p[ct][0]);
-                    p[ct][1] = __builtin_fmaf(u[j], w1[j], p[ct][1]);
-                    p[ct][2] = __builtin_fmaf(u[j], w2[j], p[ct][2]);
-                }
-            }
-        }
-        // uh[ct] is a power of two: relu, every product and every partial sum scale by it exactly,
-        // so undoing it once per row sum equals undoing it per accumulator element (12 multiplies
-        // per column tile instead of 16 per output tile)
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-            const float s0 = rows_sum(p[ct][0]) * uh[ct], s1 = rows_sum(p[ct][1]) * uh[ct],
-                        s2 = rows_sum(p[ct][2]) * uh[ct];
-            if (q == 0) {
-                sm.red[ct * 16 + n][h * 3 + 0][wid] = s0;
-                sm.red[ct * 16 + n][h * 3 + 1][wid] = s1;
-                sm.red[ct * 16 + n][h * 3 + 2][wid] = s2;
-            }
-        }
-    }
+    // ---- ReLU -> head layer 2 partial dot products: one fp32 FMA chain per (column, output) over
+    //      this wave's channels, two column tiles per packed FMA (v_pk_fma_f32), then the four
+    //      16-lane rows' chains summed by a reduce-scatter. This phase is VALU-issue bound (both
+    //      waves of a SIMD run it at once, 4 cycles per wave-instruction), so its instruction count is
+    //      its time: ~800 per wave with scalar FMAs and a full row sum per value, ~350 now.
+    head_l2_split<NT, WV>(acc, sm, uh, wid, lane);
     __syncthreads();
     PC_MARK(6);
 }
