@@ -168,6 +168,12 @@ class PoseNet:
         data["rgb_feat"] = None
 
     @staticmethod
+    def per_object_energy_t(bs: int) -> torch.Tensor:
+        """get_energy(T=None)'s per-object times: (randint(1e-5 * 1e5, 1e-4 * 1e5, (bs, 1)) as float32) / 1e5
+        from torch's default generator (posenet_agent.py:677-685), shape (bs,)."""
+        return (torch.randint(1, 10, (bs, 1)).to(torch.float32) / 1e5).view(bs)
+
+    @staticmethod
     def _time_row_and_sigma(heads: dev.HeadModel, t: float):
         t32 = torch.tensor([t], dtype=torch.float32)
         sig = float(sde.sigma(t32)[0])
@@ -298,12 +304,18 @@ class PoseNet:
         if T is not None:
             trow, sig = self._time_row_and_sigma(self.heads, float(np.float32(T)))
             energy = self.heads.energy(pobj, trow, sig, pose, K)
-        else:  # per-object t ~ randint([1e-5, 1e-4)) (posenet_agent.py:677-687)
-            ts = torch.randint(1, 10, (bs,), generator=torch.Generator().manual_seed(self._calls)).float() / 1e5
+        else:
+            # per-object t = randint(1, 10) / 1e5 drawn from torch's default CPU generator with the
+            # reference's call shape (posenet_agent.py:677-687), so torch.manual_seed reproduces its t's;
+            # one time row and one energy launch per distinct t (at most 9), not per object
+            ts = self.per_object_energy_t(bs)
             energy = torch.empty((R, 2), dtype=torch.float32, device=self.device)
-            for b in range(bs):
-                trow, sig = self._time_row_and_sigma(self.heads, float(ts[b]))
-                energy[b * K:(b + 1) * K] = self.heads.energy(pobj[b:b + 1], trow, sig, pose[b * K:(b + 1) * K], K)
+            kk = torch.arange(K, device=self.device)
+            for tv in torch.unique(ts).tolist():
+                objs = torch.nonzero(ts == tv).view(-1).to(self.device)
+                rows = (objs.view(-1, 1) * K + kk).view(-1)
+                trow, sig = self._time_row_and_sigma(self.heads, tv)
+                energy[rows] = self.heads.energy(pobj[objs].contiguous(), trow, sig, pose[rows].contiguous(), K)
         self._calls += 1
         return energy.view(bs, K, -1)
 

@@ -468,3 +468,16 @@ def test_c_pc_step_table_matches_sde_table():
     assert worst[1] <= 3 and worst[2] <= 3 and worst[4] <= 1, worst
     print(f"sigma/g/sqrt(dt) entries differing: {n_diff} of {n}, worst ulp {worst}")
     assert lib.gp_pc_step_table(1, ctypes.c_float(1e-5), None) != 0
+
+
+def test_energy_per_object_t_draws_like_reference():
+    """PoseNet.per_object_energy_t consumes torch's default generator exactly as posenet_agent.py:677-685
+    does (randint(int(T_min * 1e5), int(T_max * 1e5), (bs, 1)).type_as(float32 features) / 1e5)."""
+    import torch
+    from genpose2_amd.agent import PoseNet
+    for bs in (1, 7, 64):
+        torch.manual_seed(bs)
+        ref = torch.randint(int(1e-5 * 1e5), int(1e-4 * 1e5), (bs, 1)).type_as(torch.zeros(1)) / 1e5
+        torch.manual_seed(bs)
+        got = PoseNet.per_object_energy_t(bs)
+        assert got.dtype == torch.float32 and torch.equal(got, ref.view(bs))

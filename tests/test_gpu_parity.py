@@ -488,6 +488,27 @@ def test_energy_ranking_aggregate_scale_vs_golden():
     assert rel(length, g["scale_length"]) < 1e-5
 
 
+def test_energy_per_object_t_batched():
+    """get_energy(T=None) (posenet_agent.py:677-687): per-object t drawn from torch's default generator
+    with the reference's call shape, evaluated per distinct t; equal to get_energy at each object's fixed t."""
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("pipeline")
+    e_agent = PoseNet(GenPoseConfig(device=DEV, agent_type="energy")).eval()
+    pts, center = torch.from_numpy(g["pts"]).to(DEV), torch.from_numpy(g["pts_center"]).to(DEV)
+    pose = torch.from_numpy(g["pred_pose"]).to(DEV)
+    bs = pts.shape[0]
+    torch.manual_seed(11)
+    e = e_agent.get_energy({"pts": pts, "pts_center": center}, pose, T=None, mode="test").cpu()
+    torch.manual_seed(11)
+    ts = PoseNet.per_object_energy_t(bs)
+    assert len(torch.unique(ts)) > 1
+    for b in range(bs):
+        eb = e_agent.get_energy({"pts": pts[b:b + 1], "pts_center": center[b:b + 1]}, pose[b:b + 1], T=float(ts[b]),
+                                mode="test").cpu()
+        assert rel(e[b:b + 1], eb.numpy()) < 1e-6
+
+
 def test_runner_pipeline_smoke():
     from genpose2_amd import synthetic
     from genpose2_amd.config import GenPoseConfig
