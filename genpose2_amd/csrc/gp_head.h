@@ -53,37 +53,7 @@ struct HeadSmem {
     float pe0b[HID], pe2b[HID];
     float h2w[9 * HID];                // head layer 2, [head*3 + out][256]
     float h2b[12];
-    // split trunk: head layer 1's fp32 init rows -- the object rows (pobj) of the objects this tile's
-    // candidates belong to and the time row -- copied global -> LDS at kernel entry (stage_init_rows)
-    static constexpr int kInitObj = NT + 1;   // objects a tile of 16 NT candidates spans when K >= 16
-    float pinit[kInitObj][3 * HID];
-    float tinit[3 * HID];
 };
-
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-
-// Copies head layer 1's init rows for candidate rows [r0, r0 + 16 NT) into sm.pinit / sm.tinit by
-// LDS DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPR round trip; the copies retire
-// by the trunk's first barrier). Returns the first object's index, or -1 when the tile spans more than
-// kInitObj objects (K < 16): the trunk then gathers the rows from global memory per column.
-// The rows gathered per column from global memory were 30 16-byte loads per lane and wave (~240 KB
-// per 64-candidate workgroup through the CU's vector-memory pipe, ~3k cycles of it per PC step).
-template <int NT, int WV>
-__device__ __forceinline__ int stage_init_rows(HeadSmem<NT, WV>& sm, const float* pobj, const float* tproj_row,
-                                               int r0, int rows, int kper) {
-    const int last = min(r0 + 16 * NT, rows) - 1;
-    const int o0 = r0 / kper, nspan = last / kper - o0 + 1;
-    if (nspan > HeadSmem<NT, WV>::kInitObj) return -1;
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int k = wid; k < 3 * (nspan + 1); k += WV) {   // 3 KiB per row
-        const int row = k / 3, part = k - 3 * row;
-        const float* src = (row < nspan ? pobj + (size_t)(o0 + row) * (3 * HID) : tproj_row) + part * 256 + lane * 4;
-        float* dst = (row < nspan ? sm.pinit[row] : sm.tinit) + part * 256;
-        __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)dst, 16, 0, 0);
-    }
-    return o0;
-}
 
 // Threads [FIRST, WV*64) copy the small weights into LDS.
 // PE0 = false: pose_encoder.0's fragments and bias are not staged (the split trunk holds them in
@@ -500,8 +470,7 @@ __device__ __forceinline__ void head_l2_split(const f32x4 (&acc)[3 * (16 / WV)][
 template <int NT, int WV>
 __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const float* __restrict__ pobj,
                                                  const float* __restrict__ tproj, const int* obj_of_col,
-                                                 HeadSmem<NT, WV>& sm, int trace_slot, const SplitScalars hs,
-                                                 int init_o = -1) {
+                                                 HeadSmem<NT, WV>& sm, int trace_slot, const SplitScalars hs) {
     constexpr int TPW = 16 / WV;   // output tiles per wave; tiles (2c, 2c+1) form 32-deep chunk c
     static_assert(TPW % 2 == 0, "split trunk pairs a wave's output tiles into 32-deep chunks");
     static_assert(WV == HSPLIT_WV, "SplitScalars carries the pose_encoder.0 fragments of HSPLIT_WV waves");
@@ -549,11 +518,12 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
         uh[ct] = exp2i(e2 - 14 - ewh);   // undo both scales of head layer 1
         sh[ct] = exp2i(14 - e2 + ewh);   // head layer 1's fp32 init (pts + t blocks) in the scaled domain
     }
-    // head layer 1's fp32 init (pts + t blocks): from LDS when stage_init_rows staged them (init_o >= 0),
-    // else gathered from global memory here, a whole pose_encoder.0 + .2 ahead of their use (buffer
-    // loads: one 32-bit lane offset per column tile, the output tile's offset wave-uniform)
+    // head layer 1's fp32 init (pts + t blocks): first touch of pobj / tproj after the kernel
+    // boundary, so issued here, a whole pose_encoder.0 + .2 ahead of its use. Buffer loads: one
+    // 32-bit lane offset per column tile, the output tile's offset wave-uniform (SGPR), instead of a
+    // 64-bit address per load
     f32x4 tpv[3 * TPW], pov[3 * TPW][NT];
-    if (init_o < 0) {
+    {
         const __amdgpu_buffer_rsrc_t RP = make_rsrc(pobj, 0x7ffffff0u), RT = make_rsrc(tproj, 3 * HID * 4);
         int vo[NT];
 #pragma unroll
@@ -587,18 +557,6 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     // ---- pose_encoder.2 (256 -> 256)
     stream_h_step<D2, KC_HID + D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
     PC_MARK(3);
-    if (init_o >= 0) {   // staged rows: read where they are added (no registers held across pe0 / pe2)
-        int so[NT];
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) so[ct] = (obj_of_col[ct * 16 + n] - init_o) * (3 * HID) + 4 * q;
-#pragma unroll
-        for (int i = 0; i < 3 * TPW; ++i) {
-            const int T = TH[i];
-            tpv[i] = ld4(&sm.tinit[16 * T + 4 * q]);
-#pragma unroll
-            for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ld4(&sm.pinit[0][0] + so[ct] + 16 * T);
-        }
-    }
     f32x4 acc[3 * TPW][NT];
 #pragma unroll
     for (int i = 0; i < 3 * TPW; ++i)

@@ -96,8 +96,6 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         kout = a.kbuf[c->kidx[a.stage]];
         ynew = a.ybuf[c->yi ^ 1];
     }
-    int init_o = -1;
-    if constexpr (SPLIT) init_o = stage_init_rows(sm, a.pobj, tproj, r0, a.rows, a.kper);
     stage_small_weights<NT, EVAL_WV, 0, !SPLIT>(a.w, sm);
     for (int i = tid; i < ROWS * 16; i += NTH) {
         const int c = i >> 4, j = i & 15;
@@ -127,7 +125,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
     }
     if constexpr (SPLIT)
-        head_trunk_split<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm, 0, hs, init_o);
+        head_trunk_split<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm, 0, hs);
     else
         head_trunk<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
     double sq = 0.0;   // this thread's (err/scale)^2 terms, its elements in increasing order

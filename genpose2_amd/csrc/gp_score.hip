@@ -85,11 +85,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
     __shared__ int obj[16];
     const int r0 = blockIdx.x * 16;
     SplitScalars hs = {};
-    int init_o = -1;
-    if constexpr (SPLIT) {
-        init_o = stage_init_rows(sm, pobj, tproj, r0, rows, kper);
-        hs = load_split_scalars(w);
-    }
+    if constexpr (SPLIT) hs = load_split_scalars(w);
     stage_small_weights<1, EVAL_WV, 0, !SPLIT>(w, sm);
     for (int i = threadIdx.x; i < 256; i += EVAL_WV * 64) {
         const int c = i >> 4, j = i & 15;
@@ -101,7 +97,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
         obj[threadIdx.x] = (r < rows ? r : rows - 1) / kper;
     }
     if constexpr (SPLIT)
-        head_trunk_split<1, EVAL_WV>(w, pobj, tproj, obj, sm, 0, hs, init_o);
+        head_trunk_split<1, EVAL_WV>(w, pobj, tproj, obj, sm, 0, hs);
     else
         head_trunk<1, EVAL_WV>(w, pobj, tproj, obj, sm);
     if (MODE == 0) {
@@ -190,12 +186,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     const int r0 = blockIdx.x * ROWS;
     const int trace_slot = i & 1;
     SplitScalars hs = {};
-    int init_o = -1;
-    if constexpr (SPLIT) {
-        // in flight across the update: head layer 1's init rows (LDS DMA) and the split scalars
-        if (i < a.steps) init_o = stage_init_rows(sm, a.pobj, a.tproj + (size_t)i * 768, r0, a.rows, a.kper);
-        hs = load_split_scalars(a.w);
-    }
+    if constexpr (SPLIT) hs = load_split_scalars(a.w);   // in flight across the update
     PC_MARK(0);
     if (wid < NT) {
         // ---- every load first and unconditional (rows clamped: a guarded load becomes a branch,
@@ -337,7 +328,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     }
     stage_small_weights<NT, WV, 64 * NT, !SPLIT>(a.w, sm);
     if constexpr (SPLIT)
-        head_trunk_split<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs, init_o);
+        head_trunk_split<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
     else
         head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
     PC_MARK(7);

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Same-box A/B of library builds on the full bench step (bench.py, config 4 by default), alternating
+# ABAB... so that box-to-box clock spread does not decide it.
+# usage: bash scripts/ab_bench.sh TAG ROUNDS "BENCH ARGS" LIB1 LIB2 ...
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=$1; ROUNDS=$2; ARGS=$3; shift 3
+for r in $(seq 1 "$ROUNDS"); do
+  for L in "$@"; do
+    GENPOSE_HIP_LIB=$L timeout -k 10 300 python bench.py $ARGS > gpurun_out/${TAG}.json 2> gpurun_out/${TAG}.err || exit 1
+    echo "$r $L $(python -c "import json;d=json.loads(open('gpurun_out/${TAG}.json').read().strip().splitlines()[-1]);r=d['roofline'];print(f\"ms_per_step={d['ms_per_step']:.3f} sampler_ms={r.get('sampler_ms_per_step',0):.3f} pc_us={r['avg_launch_us']:.2f}\")")"
+  done
+done
