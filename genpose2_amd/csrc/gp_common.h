@@ -48,6 +48,8 @@ __device__ __forceinline__ f32x4 mfma_kgroup(const f32x4 a, const f32x4 b, f32x4
 __device__ __forceinline__ float relu1(float v) { return __builtin_elementwise_maximum(v, 0.f); }
 __device__ __forceinline__ f32x4 relu4(f32x4 v) { return f32x4{relu1(v.x), relu1(v.y), relu1(v.z), relu1(v.w)}; }
 
+typedef __attribute__((address_space(3))) void* lds_void_ptr;   // LDS-DMA destination
+
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
 // Buffer resource over `bytes` bytes at p (p must be wave-uniform: a kernel argument).
