@@ -53,6 +53,7 @@ struct HeadSmem {
     float pe0b[HID], pe2b[HID];
     float h2w[9 * HID];                // head layer 2, [head*3 + out][256]
     float h2b[12];
+    f32x4 cscl[NT * 16][2];            // split trunk: per-column scales {s1, s2, u2, uh}, {sh} (ColScales)
 };
 
 // Threads [FIRST, WV*64) copy the small weights into LDS.
@@ -466,8 +467,31 @@ __device__ __forceinline__ void head_l2_split(const f32x4 (&acc)[3 * (16 / WV)][
         sm.red[4 * g + q][n][wid] = rows_sum_scatter4(pv[4 * g], pv[4 * g + 1], pv[4 * g + 2], pv[4 * g + 3]);
 }
 
+// A candidate's power-of-two scales of the split trunk from m0 = max |pose entry| (rigorous bounds of
+// pose_encoder.0's and .2's outputs, hs): s1 / s2 scale the two activations into [2^14, 2^15) at their
+// bound, u2 / uh undo both scales of pose_encoder.2 / head layer 1, sh brings head layer 1's fp32 init
+// into the scaled domain. One definition for the trunk and the PC update waves that precompute it.
+struct ColScales {
+    float s1, s2, u2, uh, sh;
+};
+__device__ __forceinline__ ColScales split_col_scales(float m0, const SplitScalars& hs) {
+    const float b1 = fmaxf(__builtin_fmaf(hs.A0, m0, hs.B0) * 1.0009765625f, 1e-18f);
+    const float b2 = fmaxf(__builtin_fmaf(hs.A2, b1, hs.B2) * 1.0009765625f, 1e-18f);
+    const int e1 = ilog2f(b1), e2 = ilog2f(b2);
+    return ColScales{exp2i(14 - e1), exp2i(14 - e2), exp2i(e1 - 14 - hs.ew2), exp2i(e2 - 14 - hs.ewh),
+                     exp2i(14 - e2 + hs.ewh)};
+}
+// max |x| of a 16-wide xin row held four entries per lane over the four 16-lane rows (the trunk's
+// B-operand layout): the bound's m0
+__device__ __forceinline__ float xin_row_absmax(f32x4 b) {
+    return rows_max(fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)), fmaxf(fabsf(b.z), fabsf(b.w))));
+}
+
 // head_trunk with the split-f16 GEMMs (same contract and phases; pose_encoder.0 and layer 2 stay fp32).
-template <int NT, int WV>
+// PRE: the caller wrote every column's ColScales to sm.cscl before the trunk's first barrier (the PC
+// step's update waves, which hold the rows), so the trunk reads them instead of recomputing them in
+// every wave.
+template <int NT, int WV, bool PRE = false>
 __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const float* __restrict__ pobj,
                                                  const float* __restrict__ tproj, const int* obj_of_col,
                                                  HeadSmem<NT, WV>& sm, int trace_slot, const SplitScalars hs) {
@@ -501,22 +525,23 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
     __syncthreads();
     PC_MARK(1);
     // ---- per-candidate exponents: bound1 >= |pose_encoder.0 out|, bound2 >= |pose_encoder.2 out|
-    const float A0 = hs.A0, B0 = hs.B0, A2 = hs.A2, B2 = hs.B2;
-    const int ew2 = hs.ew2, ewh = hs.ewh;
     f32x4 bf[NT];
     float s1[NT], s2[NT], u2[NT], uh[NT], sh[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) {
         bf[ct] = ld4(&sm.xin[(ct * 16 + n) * 16 + 4 * q]);
-        const float m0 = rows_max(fmaxf(fmaxf(fabsf(bf[ct].x), fabsf(bf[ct].y)), fmaxf(fabsf(bf[ct].z), fabsf(bf[ct].w))));
-        const float b1 = fmaxf((A0 * m0 + B0) * 1.0009765625f, 1e-18f);
-        const float b2 = fmaxf((A2 * b1 + B2) * 1.0009765625f, 1e-18f);
-        const int e1 = ilog2f(b1), e2 = ilog2f(b2);
-        s1[ct] = exp2i(14 - e1);         // activations scaled into [2^14, 2^15) at their bound
-        s2[ct] = exp2i(14 - e2);
-        u2[ct] = exp2i(e1 - 14 - ew2);   // undo both scales of pose_encoder.2
-        uh[ct] = exp2i(e2 - 14 - ewh);   // undo both scales of head layer 1
-        sh[ct] = exp2i(14 - e2 + ewh);   // head layer 1's fp32 init (pts + t blocks) in the scaled domain
+        ColScales cs;
+        if constexpr (PRE) {
+            const f32x4 a = sm.cscl[ct * 16 + n][0];
+            cs = ColScales{a.x, a.y, a.z, a.w, sm.cscl[ct * 16 + n][1].x};
+        } else {
+            cs = split_col_scales(xin_row_absmax(bf[ct]), hs);
+        }
+        s1[ct] = cs.s1;
+        s2[ct] = cs.s2;
+        u2[ct] = cs.u2;
+        uh[ct] = cs.uh;
+        sh[ct] = cs.sh;
     }
     // head layer 1's fp32 init (pts + t blocks): first touch of pobj / tproj after the kernel
     // boundary, so issued here, a whole pose_encoder.0 + .2 ahead of its use. Buffer loads: one

@@ -306,6 +306,18 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
 #pragma unroll
                 for (int j = 9; j < 16; ++j) sm.xin[c * 16 + j] = 0.f;
             }
+            if constexpr (SPLIT) {
+                // this row's split-trunk scales, from the entries just written to xin (max |x| over the
+                // row's four lanes by DPP), once here instead of in all eight waves of the trunk
+                float m = (p < 3 && r < a.rows) ? fmaxf(fmaxf(fabsf(x3[0]), fabsf(x3[1])), fabsf(x3[2])) : 0.f;
+                m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, true)));
+                m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, true)));
+                if (p == 0) {
+                    const ColScales cs = split_col_scales(m, hs);
+                    sm.cscl[c][0] = f32x4{cs.s1, cs.s2, cs.u2, cs.uh};
+                    sm.cscl[c][1] = f32x4{cs.sh, 0.f, 0.f, 0.f};
+                }
+            }
         }
         PC_MARK(12);
     }
@@ -328,7 +340,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     }
     stage_small_weights<NT, WV, 64 * NT, !SPLIT>(a.w, sm);
     if constexpr (SPLIT)
-        head_trunk_split<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
+        head_trunk_split<NT, WV, true>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
     else
         head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
     PC_MARK(7);

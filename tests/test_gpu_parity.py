@@ -488,6 +488,28 @@ def test_energy_ranking_aggregate_scale_vs_golden():
     assert rel(length, g["scale_length"]) < 1e-5
 
 
+@pytest.mark.parametrize("B,K", [(4, 16), (96, 50), (256, 50)])
+def test_pc_step_score_equals_eval_score(B, K):
+    """The PC step's score (16, 32 or 64 candidates per workgroup: head_pick_nt by row count) equals the
+    score-evaluation kernel's (16 per workgroup) on the same states bit for bit: both run the same
+    trunk, and per-candidate arithmetic does not depend on the tile (scripts/head_nt_diff.py)."""
+    from genpose2_amd import sde
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    torch.manual_seed(B)
+    h = PoseNet(GenPoseConfig(device=DEV, sampling_steps=2)).eval().heads
+    R = B * K
+    tab = sde.pc_step_table(2)
+    tproj = h.time_proj(torch.from_numpy(tab[:, 0]).to(DEV))
+    pobj = h.object_proj(torch.rand(B, 1024, device=DEV))
+    x0 = torch.randn(R, 9, device=DEV)
+    z = torch.zeros(2, R, 9, device=DEV)
+    _, _, xs = h.pc_sample(pobj, tproj, tab, x0.clone(), K, torch.zeros(B, 3, device=DEV), z1=z, z2=z, want_xs=True)
+    s_pc = h._pc_ws[: R * 9 * 4].view(torch.float32).view(R, 9).clone()
+    s_ev = h.score(pobj, tproj[1:2].contiguous(), float(tab[1, 1]), xs[:, 0].contiguous(), K)
+    assert torch.equal(s_pc, s_ev)
+
+
 def test_energy_per_object_t_batched():
     """get_energy(T=None) (posenet_agent.py:677-687): per-object t drawn from torch's default generator
     with the reference's call shape, evaluated per distinct t; equal to get_energy at each object's fixed t."""
