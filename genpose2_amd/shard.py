@@ -73,6 +73,10 @@ def broadcast_agent(agent, src: int = 0) -> None:
     if len(tabs) > 1:
         agent.img_encoder.set_table(tabs[1])
     agent._pc_cache = {}
+    if dev_ is not None:
+        # one-time: every copy the collective made into (or out of) the weight buffers has landed
+        # before any kernel of any stream reads them (gloo moves CUDA tensors on its own streams)
+        torch.cuda.synchronize(dev_)
 
 
 def packed_host_tables(kind: str, sd) -> List[np.ndarray]:
