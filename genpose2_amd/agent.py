@@ -76,7 +76,7 @@ class PoseNet:
             sd = {k: v for k, v in sd.items() if not k.startswith("dino.")}
         weights.check_keys(sd, self.weights_kind)
         self.state_dict = sd
-        self._pc_cache = {}                        # T -> (step table, tproj) of these weights
+        self._pc_cache = {}                        # T -> (step table, tproj); energy t -> time row
         if self.cfg.agent_type in ("score", "energy"):
             if self.pointwise:
                 from .fus_encoder import FusEncoderModel
@@ -172,6 +172,16 @@ class PoseNet:
         """get_energy(T=None)'s per-object times: (randint(1e-5 * 1e5, 1e-4 * 1e5, (bs, 1)) as float32) / 1e5
         from torch's default generator (posenet_agent.py:677-685), shape (bs,)."""
         return (torch.randint(1, 10, (bs, 1)).to(torch.float32) / 1e5).view(bs)
+
+    def _energy_time_row(self, t: float):
+        """The head-1 time row and sigma of t, cached with the weights (_pc_cache is reset when they
+        change): evaluation calls get_energy with the same T = 1e-5 for every batch."""
+        key = ("energy_t", t)
+        c = self._pc_cache.get(key)
+        if c is None:
+            c = self._time_row_and_sigma(self.heads, t)
+            self._pc_cache[key] = c
+        return c
 
     @staticmethod
     def _time_row_and_sigma(heads: dev.HeadModel, t: float):
@@ -302,7 +312,7 @@ class PoseNet:
         center = dev.require_device_tensor(data["pts_center"], "pts_center")
         pose[:, -3:] -= center.unsqueeze(1).repeat(1, K, 1).view(R, -1)
         if T is not None:
-            trow, sig = self._time_row_and_sigma(self.heads, float(np.float32(T)))
+            trow, sig = self._energy_time_row(float(np.float32(T)))
             energy = self.heads.energy(pobj, trow, sig, pose, K)
         else:
             # per-object t = randint(1, 10) / 1e5 drawn from torch's default CPU generator with the
@@ -314,7 +324,7 @@ class PoseNet:
             for tv in torch.unique(ts).tolist():
                 objs = torch.nonzero(ts == tv).view(-1).to(self.device)
                 rows = (objs.view(-1, 1) * K + kk).view(-1)
-                trow, sig = self._time_row_and_sigma(self.heads, tv)
+                trow, sig = self._energy_time_row(tv)
                 energy[rows] = self.heads.energy(pobj[objs].contiguous(), trow, sig, pose[rows].contiguous(), K)
         self._calls += 1
         return energy.view(bs, K, -1)

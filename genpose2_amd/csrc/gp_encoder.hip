@@ -1088,18 +1088,36 @@ constexpr size_t tg_lds_bytes() {   // two stages of (4*WO weight + 4*(8/WO) poi
     return 2 * (size_t)(4 * WO + 4 * (8 / WO)) * 2048 + sizeof(int) * 64 * (8 / WO);
 }
 
-// max |x| over each point's input row [x0 | x1] (a wave per point)
+// max |x| over each point's input row [x0 | x1]: 16 lanes per point (16-byte loads when the rows
+// allow), 16 points per 256-thread workgroup, the max over the 16 lanes by DPP (fmaxf, as the
+// one-wave-per-point form this replaces: a wave per point spent its time in dispatch, 30-64 us per
+// call at B=256)
+template <int CTRL>
+__device__ __forceinline__ float dpp_fmax(float v) {
+    return fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true)));
+}
 __global__ __launch_bounds__(256) void tok_rowmax_kernel(const float* __restrict__ x0, int ld0, int k0,
                                                          const float* __restrict__ x1, int ld1, int k1, int M,
                                                          float* __restrict__ rmax) {
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (r >= M) return;
+    const int r = blockIdx.x * 16 + (threadIdx.x >> 4), sub = threadIdx.x & 15;
     float m = 0.f;
-    for (int k = lane; k < k0; k += 64) m = fmaxf(m, fabsf(x0[(size_t)r * ld0 + k]));
-    for (int k = lane; k < k1; k += 64) m = fmaxf(m, fabsf(x1[(size_t)r * ld1 + k]));
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-    if (lane == 0) rmax[r] = m;
+    if (r < M) {   // no early exit: every lane of a 16-lane row takes part in the DPP max below
+        const float* row = x0 + (size_t)r * ld0;
+        if (((k0 | ld0) & 3) == 0 && (reinterpret_cast<uintptr_t>(x0) & 15) == 0) {
+            for (int k = 4 * sub; k < k0; k += 64) {
+                const f32x4 v = ld4(row + k);
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            }
+        } else {
+            for (int k = sub; k < k0; k += 16) m = fmaxf(m, fabsf(row[k]));
+        }
+        for (int k = sub; k < k1; k += 16) m = fmaxf(m, fabsf(x1[(size_t)r * ld1 + k]));
+    }
+    m = dpp_fmax<0xB1>(m);    // quad_perm [1,0,3,2]
+    m = dpp_fmax<0x4E>(m);    // quad_perm [2,3,0,1]
+    m = dpp_fmax<0x141>(m);   // row_half_mirror
+    m = dpp_fmax<0x140>(m);   // row_mirror
+    if (sub == 0 && r < M) rmax[r] = m;
 }
 
 template <int MODE, int WO>
@@ -1428,7 +1446,7 @@ static int run_proj_split(const EncCtx& c, int l, int c_prev, const float* feat_
     GP_REQUIRE(w == kWidths[l][1][1] && (w == 64 || w == 128 || w == 256) && feat_prev && c_prev % 4 == 0,
                "encoder: level %d projection of width %d has no split tile", l, w);
     float* rmax = reinterpret_cast<float*>(c.ws + c.L.proj[l - 1]);
-    hipLaunchKernelGGL(tok_rowmax_kernel, dim3((M + 3) / 4), dim3(256), 0, st, feat_prev, c_prev, c_prev, xyz_prev, 3,
+    hipLaunchKernelGGL(tok_rowmax_kernel, dim3((M + 15) / 16), dim3(256), 0, st, feat_prev, c_prev, c_prev, xyz_prev, 3,
                        3, M, rmax);
     TokArgs a = {};
     a.M = M;
@@ -1475,7 +1493,7 @@ static int run_groupall_split(const EncCtx& c, const float* feat_prev, float* ou
     GP_REQUIRE((size_t)kNpoint[2] * proj_stride(3) >= (size_t)P * 1024 && (size_t)kNpoint[1] * proj_stride(2) >= 3u * P,
                "encoder: GroupAll scratch does not fit the projection buffers");
     const float* xyz = c.nxyz[3];
-    hipLaunchKernelGGL(tok_rowmax_kernel, dim3((M + 3) / 4), dim3(256), 0, st, feat_prev, k_in, k_in, xyz, 3, 3, M,
+    hipLaunchKernelGGL(tok_rowmax_kernel, dim3((M + 15) / 16), dim3(256), 0, st, feat_prev, k_in, k_in, xyz, 3, 3, M,
                        rmax0);
     if (hipMemsetAsync(ymax, 0, sizeof(unsigned) * 2 * (size_t)M, st) != hipSuccess)
         return gp_check_launch("groupall memset");
