@@ -41,52 +41,21 @@ extern "C" int gp_debug_pc_trace(unsigned long long* host) {
 #include "gp_head.h"
 
 // ============================================================================ hoist kernels
-// OPB objects per workgroup: every weight read from L2 feeds OPB objects' dot products (one
-// object per workgroup read the 3 MB pts block once per object: 768 MB at B = 256). Each output keeps
-// dot_chains<1024, 32>'s 32 interleaved chains and pairwise tree, so the bits do not change.
-constexpr int OPB = 4;
-__global__ __launch_bounds__(HT) void object_proj_kernel(gp_head_weights w, const float* __restrict__ feat, int nb,
+__global__ __launch_bounds__(HT) void object_proj_kernel(gp_head_weights w, const float* __restrict__ feat,
                                                          float* __restrict__ pobj) {
-    constexpr int N = 1024, CH = 32;
-    __shared__ float sf[OPB][N];
-    const int b0 = blockIdx.y * OPB;
-    for (int i = threadIdx.x; i < OPB * N; i += HT) {
-        const int j = i / N, b = min(b0 + j, nb - 1);
-        sf[j][i - j * N] = feat[(size_t)b * N + (i - j * N)];
-    }
+    __shared__ float sf[1024];
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < 1024; i += HT) sf[i] = feat[(size_t)b * 1024 + i];
     __syncthreads();
     const int o = blockIdx.x * HT + threadIdx.x;  // 0..767
-    const float* W = w.h1pts_t + o;
-    float p[OPB][CH];
-#pragma unroll
-    for (int j = 0; j < OPB; ++j)
-#pragma unroll
-        for (int c = 0; c < CH; ++c) p[j][c] = 0.f;
-#pragma unroll 1
-    for (int c0 = 0; c0 < N; c0 += CH) {
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            const float wv = W[(size_t)(c0 + c) * 768];
-#pragma unroll
-            for (int j = 0; j < OPB; ++j) p[j][c] = fmaf(wv, sf[j][c0 + c], p[j][c]);
-        }
-    }
-    const float bias = w.h1_b[o];
-#pragma unroll
-    for (int j = 0; j < OPB; ++j) {
-#pragma unroll
-        for (int s = CH / 2; s >= 1; s >>= 1)
-#pragma unroll
-            for (int c = 0; c < s; ++c) p[j][c] += p[j][c + s];
-        if (b0 + j < nb) pobj[(size_t)(b0 + j) * 768 + o] = p[j][0] + bias;
-    }
+    pobj[(size_t)b * 768 + o] = dot_chains<1024, 32>(w.h1pts_t + o, 768, sf) + w.h1_b[o];
 }
 
 extern "C" int gp_head_object_proj(const gp_head_weights* w, const float* pts_feat, int b, float* pobj,
                                    hipStream_t stream) {
     GP_REQUIRE(w && pts_feat && pobj && b >= 0, "head_object_proj: bad arguments");
     if (!b) return GP_OK;
-    hipLaunchKernelGGL(object_proj_kernel, dim3(3, (b + OPB - 1) / OPB), dim3(HT), 0, stream, *w, pts_feat, b, pobj);
+    hipLaunchKernelGGL(object_proj_kernel, dim3(3, b), dim3(HT), 0, stream, *w, pts_feat, pobj);
     return gp_check_launch("object_proj_kernel");
 }
 
