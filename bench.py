@@ -43,6 +43,46 @@ def dist_env():
     return ws, rank, local
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes/*/properties"
+
+
+def count_gpus(env=None):
+    """GPUs on this node, counted without any HIP call (the launcher must start its ranks before anything
+    touches the GPU): amdsmi's processor handles, else the KFD topology nodes whose gfx_target_version is
+    non-zero (CPU nodes report 0); capped by HIP/ROCR/CUDA_VISIBLE_DEVICES. None when neither source can
+    be read -- the caller then refuses to launch rather than fall back to torch.cuda.device_count(),
+    which calls hipGetDeviceCount in this process when amdsmi is unusable."""
+    env = os.environ if env is None else env
+    n = None
+    try:
+        import amdsmi
+        amdsmi.amdsmi_init()
+        try:
+            n = len(amdsmi.amdsmi_get_processor_handles())
+        finally:
+            amdsmi.amdsmi_shut_down()
+    except Exception:   # not importable, no driver, or no permission: try the KFD topology
+        n = None
+    if not n:
+        found = 0
+        for fn in glob.glob(KFD_NODES):
+            try:
+                with open(fn) as f:
+                    for line in f:
+                        k, _, v = line.partition(" ")
+                        if k == "gfx_target_version" and int(v) != 0:
+                            found += 1
+            except (OSError, ValueError):
+                continue
+        n = found if found else n
+    if n is None:
+        return None
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if env.get(var):
+            n = min(n, len([d for d in env[var].split(",") if d.strip()]))
+    return n
+
+
 def launch_command(argv, gpus, env, device_count, probe=False):
     """How `bench.py --gpus N` runs: None = in this process (N == 1, or already a rank of a launcher
     whose WORLD_SIZE equals N); otherwise the torchrun command that starts N ranks (one per GPU) as a
@@ -192,16 +232,31 @@ def cpu_baseline(cfg, config_id, threads, sample_objects, reps=3):
     return out
 
 
-def load_rocprof(kernel_prefix):
-    """Mean duration of the dominant kernel from the newest committed rocprofv3 --stats summary of a bench
-    run (profiles/r*/config4*_kernel_stats.csv), or None."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "config4*_kernel_stats.csv")),
-                   key=lambda f: (int(os.path.basename(os.path.dirname(f))[1:] or 0), os.path.getmtime(f)))
+def rocprof_files(config, dino="none"):
+    """Committed rocprofv3 --stats summaries of bench runs of `config` (profiles/r<round>/config<C>_*_kernel_stats.csv;
+    DINO-pointwise runs: config<C>_pointwise_*), newest round first, then reverse lexical order within a round:
+    deterministic on any checkout (no mtimes)."""
+    import re
+    out = []
+    for fn in glob.glob(os.path.join(REPO, "profiles", "r*", f"config{config}_*kernel_stats.csv")):
+        base = os.path.basename(fn)
+        if ("_pointwise_" in base) != (dino == "pointwise"):
+            continue
+        m = re.fullmatch(r"r(\d+)", os.path.basename(os.path.dirname(fn)))
+        if m:
+            out.append((int(m.group(1)), base, fn))
+    return [fn for _, _, fn in sorted(out, reverse=True)]
+
+
+def load_rocprof(kernel, config, dino="none"):
+    """Mean duration of `kernel` (its full instantiation name, e.g. "void pc_step_kernel<4, 8, true>(...") in the
+    newest committed rocprofv3 --stats summary of a bench run of the same config (so the same row count and
+    tile) that holds it, or None."""
     import csv
-    for fn in reversed(files):
+    for fn in rocprof_files(config, dino):
         with open(fn) as f:
             for row in csv.DictReader(f):
-                if row["Name"].startswith(kernel_prefix):
+                if row["Name"].startswith(kernel):
                     return {"avg_launch_us": float(row["AverageNs"]) / 1e3, "calls": int(row["Calls"]),
                             "source": os.path.relpath(fn, REPO)}
     return None
@@ -319,13 +374,17 @@ def main():
                     help="1: encode batch k+1 on a side stream while batch k samples (every timed step "
                          "still encodes and samples one batch; the first encode is not overlapped). "
                          "Off by default: no gain measured (profiles/r1/ab_encoder_pipeline.txt)")
-    ap.add_argument("--f32-steps", type=int, default=2,
+    ap.add_argument("--f32-steps", type=int, default=5,
                     help="PC runs: also time this many steps with every GEMM in exact fp32 (heads and encoders; "
                          "GENPOSE2_HEAD_ARITH=f32 / GENPOSE2_ENC_ARITH=f32) and report them under 'f32_exact' (0: off)")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
-    # device_count() does not initialise the GPU on this image, so starting a launcher after it is safe
-    ndev = 0 if args.launch_probe else torch.cuda.device_count()
+    ndev = 0
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.launch_probe:
+        ndev = count_gpus()
+        if ndev is None:
+            raise SystemExit(f"bench.py: --gpus {args.gpus}: cannot count the node's GPUs without a HIP call (amdsmi "
+                             f"unusable and no KFD topology at {KFD_NODES}); not starting the launcher")
     cmd = launch_command(sys.argv[1:], args.gpus, os.environ, ndev, probe=args.launch_probe)
     if cmd is not None:
         import subprocess
@@ -476,9 +535,9 @@ def main():
             dist.destroy_process_group()
         return
     ode_info = time_ode_calls(args, cfg, data0, B, K, ws, dev) if args.ode_calls > 0 else None
-    split = score.heads.arith == "split_f16"
+    fast = score.heads.arith == "f16x3"
     f32_info = None
-    if args.f32_steps > 0 and split:
+    if args.f32_steps > 0 and fast:
         # the same steps with every GEMM in exact fp32 (the arithmetic the reference runs)
         agents = [a for a in (score, energy) if a is not None]
         for a in agents:
@@ -504,28 +563,35 @@ def main():
         ms32 = float(np.mean([a.elapsed_time(b) for a, b in samp_ev[n_ev:]]))
         del samp_ev[n_ev:]
         for a in agents:
-            a.heads.set_arith("split_f16")
+            a.heads.set_arith("f16x3")
             if hasattr(a.encoder, "set_arith"):
                 a.encoder.set_arith("split_f16")
         us32 = ms32 / 1e3 / (T + 1) * 1e6
         fl = B * K * arch.score_flops_per_candidate_step()
+        k32 = f"void pc_step_kernel<{int(_tile_rows(B * K, False)) // 16}, 8, false>"
         f32_info = {"value": B * K * T * ws * args.f32_steps / el32, "unit": "pose-candidate-steps/s",
                     "steps": args.f32_steps, "ms_per_step": el32 / args.f32_steps * 1e3,
-                    "pc_step_avg_launch_us": us32, "achieved_tflops": fl / us32 / 1e6,
-                    "frac_of_fp32_mfma_peak": fl / us32 / 1e6 / FP32_PEAK_TFLOPS,
-                    "kernel": f"pc_step_kernel<{int(_tile_rows(B * K, False)) // 16}, ..., false>"}
+                    "dtype": "f32 (every GEMM exact fp32 MFMA, v_mfma_f32_16x16x4_f32)",
+                    "roofline": {"bound": "mfma", "achieved": fl / us32 / 1e6, "peak": FP32_PEAK_TFLOPS,
+                                 "unit": "TFLOP/s", "frac": fl / us32 / 1e6 / FP32_PEAK_TFLOPS,
+                                 "avg_launch_us": us32, "kernel": k32}}
+        rp32 = load_rocprof(k32, args.config, args.dino)
+        if rp32 is not None:
+            rp32["achieved"] = fl / (rp32["avg_launch_us"] * 1e-6) / 1e12
+            rp32["frac"] = rp32["achieved"] / FP32_PEAK_TFLOPS
+            f32_info["roofline"]["rocprof"] = rp32
     units = B * K * T * ws * args.steps
     samp_ms = float(np.mean([a.elapsed_time(b) for a, b in samp_ev]))
     per_launch_s = samp_ms / 1e3 / (T + 1)
     flop_launch = B * K * arch.score_flops_per_candidate_step()
     achieved = flop_launch / per_launch_s / 1e12
-    # split-f16: the two per-candidate GEMMs run 3 f16 MFMA products per fp32 MAC, so their MFMA
-    # ceiling in algorithmic (fp32) FLOP/s is the dense f16 peak / 3
-    peak = F16_PEAK_TFLOPS / 3 if split else FP32_PEAK_TFLOPS
+    # f16x3: the two per-candidate GEMMs run 6 f16 MFMA products per fp32 MAC (three planes per operand),
+    # so their MFMA ceiling in algorithmic (fp32) FLOP/s is the dense f16 peak / 6
+    peak = F16_PEAK_TFLOPS / 6 if fast else FP32_PEAK_TFLOPS
     up = score.heads.up.t
     wg_bytes = sum(up[k].numel() * up[k].element_size() for k in
-                   (("pe2_h", "h1p_h") if split else ("pe2_w", "h1p_w")))   # streamed per workgroup per step
-    tile = int(_tile_rows(B * K, split))   # the kernel's real tile width
+                   (("pe2_h", "h1p_h") if fast else ("pe2_w", "h1p_w")))   # streamed per workgroup per step
+    tile = int(_tile_rows(B * K, fast))   # the kernel's real tile width
     nwg = -(-B * K // tile)
     if rank == 0:
         out = {
@@ -539,7 +605,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (pose_encoder.2 / head-1 GEMMs: split-f16 MFMA, fp32 accumulate)" if split else "f32",
+            "dtype": ("f32 (pose_encoder.2 / head-1 GEMMs: f16x3 -- three f16 planes per fp32 operand, six MFMA "
+                      "products, products to 2^-33, fp32 accumulation; encoder SA levels 1-3: split-f16)") if fast else "f32",
             "data": "synthetic (seeded point clouds, seeded synthetic weights; no checkpoint exists for dino=none)",
             "config": {"workload": f"config{args.config}: B={B} objects/GPU, N={N} pts, K={K} candidates, T={T} PC "
                                    f"steps, {'ScoreNet+EnergyNet+ranking/aggregation' if cfgd['energy'] else 'ScoreNet'}"
@@ -552,17 +619,17 @@ def main():
                        "energy_encoder": (["after the sampler", "beside the sampler", "beside the score encoder"]
                                           [args.energy_overlap] if cfgd["energy"] else None)},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": load_traffic(B * K, split, tile),
+                         "frac": achieved / peak, "traffic": load_traffic(B * K, fast, tile),
                          "kernel": "pc_step_kernel", "arith": score.heads.arith, "flop_per_launch": flop_launch,
                          "avg_launch_us": per_launch_s * 1e6, "sampler_ms_per_step": samp_ms,
                          "fp32_mfma_equiv_frac": achieved / FP32_PEAK_TFLOPS,
-                         # what binds the split kernel: every workgroup streams the GEMM weights from L2
+                         # every workgroup streams the GEMM weights from L2
                          "l2_weight_stream": {"bytes_per_workgroup": wg_bytes, "workgroups": nwg,
                                               "candidates_per_workgroup": tile,
                                               "GBps_per_CU": wg_bytes / per_launch_s / 1e9,
                                               "TBps_chip": wg_bytes * nwg / per_launch_s / 1e12}},
         }
-        rp = load_rocprof(f"void pc_step_kernel<{tile // 16}, 8, {'true' if split else 'false'}>")
+        rp = load_rocprof(f"void pc_step_kernel<{tile // 16}, 8, {'true' if fast else 'false'}>", args.config, args.dino)
         if rp is not None:   # the committed rocprofv3 --stats of a bench run: its mean launch, same FLOPs
             rp["achieved"] = flop_launch / (rp["avg_launch_us"] * 1e-6) / 1e12
             rp["frac"] = rp["achieved"] / peak

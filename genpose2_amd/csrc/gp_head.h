@@ -31,15 +31,17 @@ constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
 
 
 // ============================================================================ shared head trunk
-// NT = column tiles (16 candidates each) per workgroup.
-template <int NT, int WV>
+// NT = column tiles (16 candidates each) per workgroup. PL = 0: the exact-fp32 trunk's activations
+// (fp32, accumulator-native); PL = 3: the f16x3 trunk's (three f16 planes per value, 6 B).
+template <int NT, int WV, int PL = 0>
 struct HeadSmem {
     // 64-candidate tiles (NT = 4) alias pose_encoder.2's output onto pose_encoder.0's (written after
     // a barrier that retires every read of act1), so one workgroup still fits the 160 KiB of a CU
     static constexpr bool kAliasAct = NT >= 4;
+    static constexpr int kAct = PL ? (HID / 32) * NT * PL * 64 : KG_HID * NT * 64;   // 16-byte entries
     float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
-    f32x4 act1[KG_HID * NT * 64];      // pose_encoder.0 output, accumulator-native [g][ct][lane]
-    f32x4 act2[kAliasAct ? 4 : KG_HID * NT * 64];   // pose_encoder.2 output (act1 when aliased)
+    f32x4 act1[kAct];                  // pose_encoder.0 output: [g][ct][lane] (fp32) / [chunk][ct][plane][lane]
+    f32x4 act2[kAliasAct ? 4 : kAct];  // pose_encoder.2 output (act1 when aliased)
     // per-wave head-layer-2 partials, wave-minor (head_out reads a row), indexed [v][n][wave] by the
     // value v = (head * NT + column tile) * 3 + output and the column n within the tile: the order the
     // split trunk's reduce-scatter leaves them in (row q of the wave holds values 4g + q); padded to
@@ -48,9 +50,10 @@ struct HeadSmem {
     float red[kRedV][16][WV];
     float xu[NT * 16 * 9];             // PC: last-step mean rows, gathered for the quaternion
     float scratch[WV * 64];
-    // small per-launch weights staged once per workgroup (their loads overlap the PC update)
-    f32x4 pe0w[16 * 64];               // pose_encoder.0 packed A fragments
-    float pe0b[HID], pe2b[HID];
+    // small per-launch weights staged once per workgroup (their loads overlap the PC update); the
+    // f16x3 trunk holds pose_encoder.0's fragments and bias in registers (SplitScalars)
+    f32x4 pe0w[PL ? 1 : 16 * 64];      // pose_encoder.0 packed A fragments
+    float pe0b[PL ? 1 : HID], pe2b[HID];
     float h2w[9 * HID];                // head layer 2, [head*3 + out][256]
     float h2b[12];
     f32x4 cscl[NT * 16][2];            // split trunk: per-column scales {s1, s2, u2, uh}, {sh} (ColScales)
@@ -59,8 +62,9 @@ struct HeadSmem {
 // Threads [FIRST, WV*64) copy the small weights into LDS.
 // PE0 = false: pose_encoder.0's fragments and bias are not staged (the split trunk holds them in
 // registers from kernel entry, SplitScalars).
-template <int NT, int WV, int FIRST = 0, bool PE0 = true>
-__device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, HeadSmem<NT, WV>& sm) {
+template <int NT, int WV, int FIRST = 0, bool PE0 = true, int PL>
+__device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, HeadSmem<NT, WV, PL>& sm) {
+    static_assert(PE0 || PL, "the fp32 trunk reads pose_encoder.0 from LDS");
     constexpr int NTH = WV * 64 - FIRST;
     const int t0 = (int)threadIdx.x - FIRST;
     if (t0 < 0) return;
@@ -75,8 +79,8 @@ __device__ __forceinline__ void stage_small_weights(const gp_head_weights& w, He
 }
 
 // Head output o of column c (valid after head_trunk): bias + the per-wave partials in wave order.
-template <int NT, int WV>
-__device__ __forceinline__ float head_out(const HeadSmem<NT, WV>& sm, int c, int o) {
+template <int NT, int WV, int PL>
+__device__ __forceinline__ float head_out(const HeadSmem<NT, WV, PL>& sm, int c, int o) {
     const int h = o / 3;
     const int v = (h * NT + (c >> 4)) * 3 + (o - 3 * h);
     float acc = 0.f;
@@ -259,28 +263,11 @@ __device__ __forceinline__ void head_trunk(const gp_head_weights& w, const float
     PC_MARK(6);
 }
 
-// ============================================================================ split-f16 trunk
-// The two per-candidate GEMMs (pose_encoder.2 and head layer 1's pose block) on
-// v_mfma_f32_16x16x32_f16. Both operands are scaled by exact powers of two and split x = hi + lo with
-// hi = f16(x), lo = f16(x - hi), so each keeps ~22 significant bits. Per 32-deep chunk, three MFMAs
-// (w_lo*a_hi, w_hi*a_lo, w_hi*a_hi) accumulate in fp32; the dropped w_lo*a_lo term is ~2^-22
-// relative. Weights: per-layer exponents and packed hi/lo planes from pack.py (4 B per weight, the
-// same bytes as fp32). Activations: a per-candidate exponent from a rigorous bound on the layer's
-// outputs (max|pose| times the layer's max row L1 norm plus max|bias|, chained), so no extra
-// barrier is needed and f16 cannot overflow. scripts/precision_study2.py (STUDY_F16=1): through
-// the sampler this is as close to the golden trajectories as fp32 (rotation 1.51e-5 vs 1.56e-5).
-#ifndef PC_D2H
-#define PC_D2H 2                 // 32-deep chunks of pose_encoder.2 weights kept in flight
-#endif
-#ifndef PC_NT2_D2H
-#define PC_NT2_D2H 2             // the same for 32-candidate (NT = 2) tiles
-#endif
-#ifndef PC_NT2_DH
-#define PC_NT2_DH 1              // NT = 2: one head-layer-1 chunk in flight leaves registers for 2 column tiles
-#endif
-#ifndef HEAD_PREFETCH_H
-#define HEAD_PREFETCH_H 2        // 32-deep chunks of head-layer-1 weights kept in flight
-#endif
+// ============================================================================ f16 MFMA helpers
+// Split-f16 arithmetic on v_mfma_f32_16x16x32_f16 (16x the fp32 MFMA rate on gfx950). An operand is
+// scaled by an exact power of two and split into f16 planes: x = hi + lo (hi = f16(x), lo = f16(x - hi),
+// ~22 significant bits; the encoder's SA levels 1-3 and token GEMMs, gp_encoder.hip) or x = hi + mid + lo
+// (every bit of an fp32 value: the head trunk below).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr int KC_HID = HID / 32;   // 32-deep chunks over a 256-wide activation
 
@@ -369,12 +356,6 @@ __device__ __forceinline__ void stream_hk_step(__amdgpu_buffer_rsrc_t W, const i
     }
 }
 
-// The 256-deep layers of the head trunk.
-template <int G, int GEND, int TT, int NT, int D>
-__device__ __forceinline__ void stream_h_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
-                                              int lane, int voff, f16x8 (&ring)[D + 1][TT][2], f32x4 (&acc)[TT][NT]) {
-    stream_hk_step<KC_HID, G, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc);
-}
 
 // The split trunk's activation bounds and weight exponents (gp_head_weights.hsc). Loaded at kernel entry by
 // the callers: read where they are used, their round trip (a cold L2 line after the kernel boundary) sat
@@ -421,51 +402,6 @@ __device__ __forceinline__ float rows_sum_scatter4(float a, float b, float c, fl
 // before the row sum is exact). Each (column, output) is one fp32 FMA chain over this wave's channels,
 // t-major then j, with separately rounded sums across rows and waves (head_out). Scalar FMAs: the
 // same chains as v_pk_fma_f32 over column-tile pairs (broadcast weights through op_sel, results in
-// place) summed wrong values into the even column tiles of a fraction of the workgroups.
-template <int NT, int WV>
-__device__ __forceinline__ void head_l2_split(const f32x4 (&acc)[3 * (16 / WV)][NT], HeadSmem<NT, WV>& sm,
-                                              const float (&uh)[NT], int wid, int lane) {
-    constexpr int TPW = 16 / WV;
-    constexpr int NV = 9 * NT, NG = HeadSmem<NT, WV>::kRedV / 4;
-    const int q = lane >> 4, n = lane & 15;
-    // nothing of this phase is scheduled into the head-layer-1 MFMA stream: interleaved there, the
-    // row swaps below reused registers the in-flight MFMAs still read (v_permlane*_swap writes both of
-    // its operands) and a fraction of the workgroups summed stale values
-    __builtin_amdgcn_sched_barrier(0);
-    float pv[4 * NG];
-#pragma unroll
-    for (int v = NV; v < 4 * NG; ++v) pv[v] = 0.f;
-#pragma unroll
-    for (int h = 0; h < 3; ++h) {
-        float p[NT][3];
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) p[ct][0] = p[ct][1] = p[ct][2] = 0.f;
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            const int ch = 16 * (wid * TPW + t) + 4 * q;
-            const f32x4 w0 = ld4(&sm.h2w[(h * 3 + 0) * HID + ch]);
-            const f32x4 w1 = ld4(&sm.h2w[(h * 3 + 1) * HID + ch]);
-            const f32x4 w2 = ld4(&sm.h2w[(h * 3 + 2) * HID + ch]);
-#pragma unroll
-            for (int ct = 0; ct < NT; ++ct) {
-                const f32x4 u = relu4(acc[h * TPW + t][ct]);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    p[ct][0] = __builtin_fmaf(u[j], w0[j], p[ct][0]);
-                    p[ct][1] = __builtin_fmaf(u[j], w1[j], p[ct][1]);
-                    p[ct][2] = __builtin_fmaf(u[j], w2[j], p[ct][2]);
-                }
-            }
-        }
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct)
-#pragma unroll
-            for (int o = 0; o < 3; ++o) pv[(h * NT + ct) * 3 + o] = p[ct][o] * uh[ct];
-    }
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-        sm.red[4 * g + q][n][wid] = rows_sum_scatter4(pv[4 * g], pv[4 * g + 1], pv[4 * g + 2], pv[4 * g + 3]);
-}
 
 // A candidate's power-of-two scales of the split trunk from m0 = max |pose entry| (rigorous bounds of
 // pose_encoder.0's and .2's outputs, hs): s1 / s2 scale the two activations into [2^14, 2^15) at their
@@ -487,53 +423,213 @@ __device__ __forceinline__ float xin_row_absmax(f32x4 b) {
     return rows_max(fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)), fmaxf(fabsf(b.z), fabsf(b.w))));
 }
 
-// head_trunk with the split-f16 GEMMs (same contract and phases; pose_encoder.0 and layer 2 stay fp32).
+// ============================================================================ f16x3 trunk
+// The two per-candidate GEMMs (pose_encoder.2 and head layer 1's pose block) on
+// v_mfma_f32_16x16x32_f16 with three f16 planes per operand: after an exact power-of-two scaling,
+// x = hi + mid + lo with hi = f16(x), mid = f16(x - hi), lo = f16(x - hi - mid) holds every bit of an
+// fp32 value (11 + 11 + 11 >= 24 significant bits; only values ~2^-7 below the operand's scale lose
+// lo bits to f16 subnormals, an absolute error <= 2^-39 of the scale). Per 32-deep chunk, the six
+// products whose plane orders sum to <= 2 (relative sizes 1, 2^-11, 2^-11, 2^-22 x3) are formed; the
+// three dropped ones are <= 2^-33 relative, so every product w*a enters the sum to ~2^-33, finer than
+// an fp32 FMA. hi*hi accumulates in one fp32 accumulator (one rounding per 32-deep chunk, as the
+// MFMA sums its 32 exact f16 products and rounds once), the five cross products in a second one (its
+// roundings are 2^-11 smaller), and the two are added once per layer: fewer roundings at full
+// magnitude than v_mfma_f32_16x16x4_f32's one per 4-deep step (scripts/precision_study3.py,
+// scripts/mfma_round_probe.hip). Six f16 MFMAs per 32x16x16 chunk-tile take 96 cycles against the
+// exact fp32 MFMA's 256.
+// Weights: per-layer exponents and packed hi/mid/lo planes (pack.pack_h16_fragments, 6 B per weight).
+// Activations: a per-candidate exponent from a rigorous bound on the layer's outputs (max|pose| times
+// the layer's max row L1 norm plus max|bias|, chained), so no extra barrier is needed and f16 cannot
+// overflow. pose_encoder.0 and head layer 2 stay fp32 (VALU / fp32 MFMA).
+#ifndef X3_D2
+#define X3_D2 2                  // 32-deep chunks of pose_encoder.2 weights kept in flight
+#endif
+#ifndef X3_DH
+#define X3_DH 2                  // 32-deep chunks of head-layer-1 weights kept in flight
+#endif
+constexpr int X3P = 3;           // planes per operand
+
+// x = h + m + l exactly (x finite, |x| < 65504; f16 subnormals aside)
+__device__ __forceinline__ void split3(float x, _Float16& h, _Float16& m, _Float16& l) {
+#pragma clang fp contract(off)
+    h = (_Float16)x;
+    const float r = x - (float)h;   // exact: x and h agree in sign and leading bits
+    m = (_Float16)r;
+    l = (_Float16)(r - (float)m);   // exact likewise; <= 3 significant bits remain
+}
+// The three planes of the 32-deep chunk made of two accumulator tiles (u: tile 2c, v: tile 2c+1),
+// times s, in the k order of pack_h16_fragments (as split_pair).
+__device__ __forceinline__ void split3_pair(f32x4 u, f32x4 v, float s, f16x8 (&p)[X3P]) {
+#pragma clang fp contract(off)
+    const float x[8] = {u.x * s, u.y * s, u.z * s, u.w * s, v.x * s, v.y * s, v.z * s, v.w * s};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        _Float16 h, m, l;
+        split3(x[j], h, m, l);
+        p[0][j] = h;
+        p[1][j] = m;
+        p[2][j] = l;
+    }
+}
+
+// One pipelined step of a 256-deep f16x3 layer: step G issues the loads of chunk G (tile T[t]'s three
+// weight planes, 3 KiB per tile: pack_h16_fragments' [T][c][plane][lane]) and computes chunk G - D from
+// the ring; B = activation planes in LDS, [chunk][ct][plane][lane]. acc += hi*hi, cor += the five cross
+// products, smallest first. One column tile's planes are live at a time. Steps 0..D-1 only prime the
+// ring (no B or accumulator access), so they can run before a barrier or under another phase.
+template <int G, int GEND, int TT, int NT, int D>
+__device__ __forceinline__ void stream_x3_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
+                                               int lane, int voff, f16x8 (&ring)[D + 1][TT][X3P],
+                                               f32x4 (&acc)[TT][NT], f32x4 (&cor)[TT][NT]) {
+    if constexpr (G < GEND) {
+        if constexpr (G < KC_HID) {
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int p = 0; p < X3P; ++p)
+                    ring[G % (D + 1)][t][p] =
+                        __builtin_bit_cast(f16x8, ldbuf4(W, voff, ((T[t] * KC_HID + G) * X3P + p) * 1024));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (G >= D) {
+            constexpr int GG = G - D, S = GG % (D + 1);
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) {
+                const f16x8 b0 = B[((GG * NT + ct) * X3P + 0) * 64 + lane];
+                const f16x8 b1 = B[((GG * NT + ct) * X3P + 1) * 64 + lane];
+                const f16x8 b2 = B[((GG * NT + ct) * X3P + 2) * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    f32x4 c = cor[t][ct];
+                    c = mfma_h(ring[S][t][2], b0, c);
+                    c = mfma_h(ring[S][t][0], b2, c);
+                    c = mfma_h(ring[S][t][1], b1, c);
+                    c = mfma_h(ring[S][t][1], b0, c);
+                    c = mfma_h(ring[S][t][0], b1, c);
+                    cor[t][ct] = c;
+                    acc[t][ct] = mfma_h(ring[S][t][0], b0, acc[t][ct]);
+                }
+            }
+        }
+        stream_x3_step<G + 1, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc, cor);
+    }
+}
+
+// head_trunk with the f16x3 GEMMs (same contract: head_out reads the outputs after it returns).
+// Head layer 1 runs one head at a time (2 output tiles per wave and head), each head's fp32 init rows
+// (hoisted pts + t blocks) loaded while its weights stream and added once with its two accumulators;
+// the next head's first weight chunks are in flight during this head's layer-2 partials.
 // PRE: the caller wrote every column's ColScales to sm.cscl before the trunk's first barrier (the PC
 // step's update waves, which hold the rows), so the trunk reads them instead of recomputing them in
 // every wave.
+template <int H, int NT, int WV, int TPW, int DH>
+__device__ __forceinline__ void head_x3_head(__amdgpu_buffer_rsrc_t WH, const f16x8* __restrict__ act2h,
+                                             __amdgpu_buffer_rsrc_t RP, __amdgpu_buffer_rsrc_t RT, const int (&vo)[NT],
+                                             HeadSmem<NT, WV, X3P>& sm, const float (&uh)[NT], int wid, int lane,
+                                             f16x8 (&ringh)[DH + 1][TPW][X3P], float (&pv)[HeadSmem<NT, WV, X3P>::kRedV]) {
+    const int q = lane >> 4, n = lane & 15;
+    const int voff = lane * 16;
+    int TH[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) TH[t] = H * 16 + wid * TPW + t;
+    // the init rows: first touch of pobj / tproj after the kernel boundary, consumed after the stream
+    f32x4 tpv[TPW], pov[TPW][NT];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        tpv[t] = ldbuf4(RT, 16 * q, 64 * TH[t]);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) pov[t][ct] = ldbuf4(RP, vo[ct], 64 * TH[t]);
+    }
+    f32x4 acc[TPW][NT], cor[TPW][NT];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) acc[t][ct] = cor[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    stream_x3_step<DH, KC_HID + DH, TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc, cor);
+    if constexpr (H < 2) {   // the next head's first chunks, in flight across this head's epilogue
+        int TN[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) TN[t] = TH[t] + 16;
+        stream_x3_step<0, DH, TPW, NT, DH>(WH, TN, act2h, lane, voff, ringh, acc, cor);
+    }
+    // nothing below is scheduled into the MFMA stream above: interleaved there, the row swaps of the
+    // reduce-scatter reused registers in-flight MFMAs still read (v_permlane*_swap writes both operands)
+    __builtin_amdgcn_sched_barrier(0);
+    // u = ReLU(scale-undone GEMM + init) -> head layer 2 (3 outputs) partials: one fp32 FMA chain per
+    // (column, output) over this wave's channels, t-major then j
+    float p[NT][3];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) p[ct][0] = p[ct][1] = p[ct][2] = 0.f;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int ch = 16 * (wid * TPW + t) + 4 * q;
+        const f32x4 w0 = ld4(&sm.h2w[(H * 3 + 0) * HID + ch]);
+        const f32x4 w1 = ld4(&sm.h2w[(H * 3 + 1) * HID + ch]);
+        const f32x4 w2 = ld4(&sm.h2w[(H * 3 + 2) * HID + ch]);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+            const f32x4 u = relu4((acc[t][ct] + cor[t][ct]) * uh[ct] + (pov[t][ct] + tpv[t]));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                p[ct][0] = __builtin_fmaf(u[j], w0[j], p[ct][0]);
+                p[ct][1] = __builtin_fmaf(u[j], w1[j], p[ct][1]);
+                p[ct][2] = __builtin_fmaf(u[j], w2[j], p[ct][2]);
+            }
+        }
+    }
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int o = 0; o < 3; ++o) pv[(H * NT + ct) * 3 + o] = p[ct][o];
+    // rows reduce-scatter (rows_sum_scatter4) of this head's values where they fill whole groups of four
+    if constexpr ((3 * NT) % 4 == 0) {
+#pragma unroll
+        for (int g = H * 3 * NT / 4; g < (H + 1) * 3 * NT / 4; ++g)
+            sm.red[4 * g + q][n][wid] = rows_sum_scatter4(pv[4 * g], pv[4 * g + 1], pv[4 * g + 2], pv[4 * g + 3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int NT, int WV, bool PRE = false>
-__device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const float* __restrict__ pobj,
-                                                 const float* __restrict__ tproj, const int* obj_of_col,
-                                                 HeadSmem<NT, WV>& sm, int trace_slot, const SplitScalars hs) {
-    constexpr int TPW = 16 / WV;   // output tiles per wave; tiles (2c, 2c+1) form 32-deep chunk c
-    static_assert(TPW % 2 == 0, "split trunk pairs a wave's output tiles into 32-deep chunks");
+__device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const float* __restrict__ pobj,
+                                              const float* __restrict__ tproj, const int* obj_of_col,
+                                              HeadSmem<NT, WV, X3P>& sm, int trace_slot, const SplitScalars hs) {
+    constexpr int TPW = 16 / WV;   // output tiles per wave and 256-wide layer; tiles (2c, 2c+1) form chunk c
+    static_assert(TPW % 2 == 0, "the f16x3 trunk pairs a wave's output tiles into 32-deep chunks");
     static_assert(WV == HSPLIT_WV, "SplitScalars carries the pose_encoder.0 fragments of HSPLIT_WV waves");
     constexpr int CPW = TPW / 2;
+    using SM = HeadSmem<NT, WV, X3P>;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4, n = lane & 15;
     const int voff = lane * 16;
-    const __amdgpu_buffer_rsrc_t W2 = make_rsrc(w.pe2_h, HID * HID * 4);
-    const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_h, 3 * HID * HID * 4);
-    f16x8* act1h = reinterpret_cast<f16x8*>(sm.act1);   // same 16 KiB per column tile as fp32
-    f16x8* act2h = reinterpret_cast<f16x8*>(HeadSmem<NT, WV>::kAliasAct ? sm.act1 : sm.act2);
-    constexpr int D2 = NT > 1 ? PC_NT2_D2H : PC_D2H, DH = NT > 1 ? PC_NT2_DH : HEAD_PREFETCH_H;
-    int T2[TPW], TH[3 * TPW];
+    const __amdgpu_buffer_rsrc_t W2 = make_rsrc(w.pe2_h, HID * HID * 2 * X3P);
+    const __amdgpu_buffer_rsrc_t WH = make_rsrc(w.h1p_h, 3 * HID * HID * 2 * X3P);
+    f16x8* act1h = reinterpret_cast<f16x8*>(sm.act1);
+    f16x8* act2h = reinterpret_cast<f16x8*>(SM::kAliasAct ? sm.act1 : sm.act2);
+    constexpr int D2 = X3_D2, DH = X3_DH;
+    int T2[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) T2[t] = wid * TPW + t;
-#pragma unroll
-    for (int h = 0; h < 3; ++h)
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) TH[h * TPW + t] = h * 16 + wid * TPW + t;
-    f32x4 acc2[TPW][NT];
+    f32x4 acc2[TPW][NT], cor2[TPW][NT];
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) acc2[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f16x8 ring2[D2 + 1][TPW][2];
-    stream_h_step<0, D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
+        for (int ct = 0; ct < NT; ++ct) acc2[t][ct] = cor2[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f16x8 ring2[D2 + 1][TPW][X3P];
+    stream_x3_step<0, D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2, cor2);
     __syncthreads();
     PC_MARK(1);
     // ---- per-candidate exponents: bound1 >= |pose_encoder.0 out|, bound2 >= |pose_encoder.2 out|
     f32x4 bf[NT];
-    float s1[NT], s2[NT], u2[NT], uh[NT], sh[NT];
+    float s1[NT], s2[NT], u2[NT], uh[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) {
         bf[ct] = ld4(&sm.xin[(ct * 16 + n) * 16 + 4 * q]);
         ColScales cs;
         if constexpr (PRE) {
             const f32x4 a = sm.cscl[ct * 16 + n][0];
-            cs = ColScales{a.x, a.y, a.z, a.w, sm.cscl[ct * 16 + n][1].x};
+            cs = ColScales{a.x, a.y, a.z, a.w, 0.f};
         } else {
             cs = split_col_scales(xin_row_absmax(bf[ct]), hs);
         }
@@ -541,25 +637,6 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
         s2[ct] = cs.s2;
         u2[ct] = cs.u2;
         uh[ct] = cs.uh;
-        sh[ct] = cs.sh;
-    }
-    // head layer 1's fp32 init (pts + t blocks): first touch of pobj / tproj after the kernel
-    // boundary, so issued here, a whole pose_encoder.0 + .2 ahead of its use. Buffer loads: one
-    // 32-bit lane offset per column tile, the output tile's offset wave-uniform (SGPR), instead of a
-    // 64-bit address per load
-    f32x4 tpv[3 * TPW], pov[3 * TPW][NT];
-    {
-        const __amdgpu_buffer_rsrc_t RP = make_rsrc(pobj, 0x7ffffff0u), RT = make_rsrc(tproj, 3 * HID * 4);
-        int vo[NT];
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) vo[ct] = obj_of_col[ct * 16 + n] * (3 * HID * 4) + 16 * q;
-#pragma unroll
-        for (int i = 0; i < 3 * TPW; ++i) {
-            const int T = TH[i];
-            tpv[i] = ldbuf4(RT, 16 * q, 64 * T);
-#pragma unroll
-            for (int ct = 0; ct < NT; ++ct) pov[i][ct] = ldbuf4(RP, vo[ct], 64 * T);
-        }
     }
     // ---- pose_encoder.0 (9 -> 256) in fp32, one k-group; ReLU, scale, split into the chunk planes
 #pragma unroll
@@ -570,50 +647,58 @@ __device__ __forceinline__ void head_trunk_split(const gp_head_weights& w, const
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
             const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-            f16x8 hi, lo;
-            split_pair(relu4(mfma_kgroup(a0, bf[ct], z) + bias0), relu4(mfma_kgroup(a1, bf[ct], z) + bias1), s1[ct],
-                       hi, lo);
-            act1h[(((Ta >> 1) * NT + ct) * 2 + 0) * 64 + lane] = hi;
-            act1h[(((Ta >> 1) * NT + ct) * 2 + 1) * 64 + lane] = lo;
+            f16x8 pl[X3P];
+            split3_pair(relu4(mfma_kgroup(a0, bf[ct], z) + bias0), relu4(mfma_kgroup(a1, bf[ct], z) + bias1), s1[ct], pl);
+#pragma unroll
+            for (int p = 0; p < X3P; ++p) act1h[(((Ta >> 1) * NT + ct) * X3P + p) * 64 + lane] = pl[p];
         }
     }
     __syncthreads();
     PC_MARK(2);
     // ---- pose_encoder.2 (256 -> 256)
-    stream_h_step<D2, KC_HID + D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2);
+    stream_x3_step<D2, KC_HID + D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2, cor2);
     PC_MARK(3);
-    f32x4 acc[3 * TPW][NT];
+    // head layer 1's first chunks (head 0), in flight across the pose_encoder.2 epilogue
+    f16x8 ringh[DH + 1][TPW][X3P];
+    {
+        int TH0[TPW];
 #pragma unroll
-    for (int i = 0; i < 3 * TPW; ++i)
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) acc[i][ct] = (pov[i][ct] + tpv[i]) * sh[ct];
-    f16x8 ringh[DH + 1][3 * TPW][2];
-    stream_h_step<0, DH, 3 * TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc);
-    if constexpr (HeadSmem<NT, WV>::kAliasAct) __syncthreads();   // act2 overwrites act1: all reads done
+        for (int t = 0; t < TPW; ++t) TH0[t] = wid * TPW + t;
+        stream_x3_step<0, DH, TPW, NT, DH>(WH, TH0, act2h, lane, voff, ringh, acc2, cor2);
+    }
+    if constexpr (SM::kAliasAct) __syncthreads();   // act2 overwrites act1: all reads done
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
         const int Ta = T2[2 * c];
         const f32x4 bias0 = ld4(&sm.pe2b[16 * Ta + 4 * q]), bias1 = ld4(&sm.pe2b[16 * (Ta + 1) + 4 * q]);
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-            f16x8 hi, lo;
-            split_pair(relu4(acc2[2 * c][ct] * u2[ct] + bias0), relu4(acc2[2 * c + 1][ct] * u2[ct] + bias1), s2[ct], hi,
-                       lo);
-            act2h[(((Ta >> 1) * NT + ct) * 2 + 0) * 64 + lane] = hi;
-            act2h[(((Ta >> 1) * NT + ct) * 2 + 1) * 64 + lane] = lo;
+            f16x8 pl[X3P];
+            split3_pair(relu4((acc2[2 * c][ct] + cor2[2 * c][ct]) * u2[ct] + bias0),
+                        relu4((acc2[2 * c + 1][ct] + cor2[2 * c + 1][ct]) * u2[ct] + bias1), s2[ct], pl);
+#pragma unroll
+            for (int p = 0; p < X3P; ++p) act2h[(((Ta >> 1) * NT + ct) * X3P + p) * 64 + lane] = pl[p];
         }
     }
     __syncthreads();
     PC_MARK(4);
-    // ---- head layer 1 (pose block 256 -> 3x256)
-    stream_h_step<DH, KC_HID + DH, 3 * TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc);
+    // ---- head layer 1 (pose block 256 -> 3x256) head by head, each followed by its layer-2 partials
+    const __amdgpu_buffer_rsrc_t RP = make_rsrc(pobj, 0x7ffffff0u), RT = make_rsrc(tproj, 3 * HID * 4);
+    int vo[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) vo[ct] = obj_of_col[ct * 16 + n] * (3 * HID * 4) + 16 * q;
+    float pv[SM::kRedV];
+#pragma unroll
+    for (int v = 9 * NT; v < SM::kRedV; ++v) pv[v] = 0.f;
+    head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    head_x3_head<1, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
     PC_MARK(5);
-    // ---- ReLU -> head layer 2 partial dot products: one fp32 FMA chain per (column, output) over
-    //      this wave's channels, two column tiles per packed FMA (v_pk_fma_f32), then the four
-    //      16-lane rows' chains summed by a reduce-scatter. This phase is VALU-issue bound (both
-    //      waves of a SIMD run it at once, 4 cycles per wave-instruction), so its instruction count is
-    //      its time: ~800 per wave with scalar FMAs and a full row sum per value, ~350 now.
-    head_l2_split<NT, WV>(acc, sm, uh, wid, lane);
+    if constexpr ((3 * NT) % 4 != 0) {
+#pragma unroll
+        for (int g = 0; g < SM::kRedV / 4; ++g)
+            sm.red[4 * g + q][n][wid] = rows_sum_scatter4(pv[4 * g], pv[4 * g + 1], pv[4 * g + 2], pv[4 * g + 3]);
+    }
     __syncthreads();
     PC_MARK(6);
 }

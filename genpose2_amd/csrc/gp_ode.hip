@@ -10,7 +10,9 @@
 // (_estimate_error_norm, rk.py); ode_norm_kernel reduces it in a fixed order. The step
 // controller's scalars stay on the host (genpose2_amd/ode.py): one 8-byte read per attempt.
 #include <cstddef>
+#include <mutex>
 #include <utility>
+#include <vector>
 
 #include "gp_head.h"
 
@@ -67,7 +69,7 @@ template <int MODE, bool SPLIT, int NT>
 __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a) {
     constexpr int ROWS = 16 * NT;
     constexpr int NTH = EVAL_WV * 64;
-    __shared__ HeadSmem<NT, EVAL_WV> sm;
+    __shared__ HeadSmem<NT, EVAL_WV, SPLIT ? X3P : 0> sm;
     __shared__ int obj[ROWS];
     __shared__ double y0s[ROWS * 9], y1s[ROWS * 9], esq[NTH];
     const int tid = threadIdx.x;
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
         obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
     }
     if constexpr (SPLIT)
-        head_trunk_split<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm, 0, hs);
+        head_trunk_x3<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm, 0, hs);
     else
         head_trunk<NT, EVAL_WV>(a.w, a.pobj, tproj, obj, sm);
     double sq = 0.0;   // this thread's (err/scale)^2 terms, its elements in increasing order
@@ -726,18 +728,50 @@ OdeSampleLayout ode_sample_layout(int rows) {
     return L;
 }
 
-// host resources of the status read, made once per thread (not per call)
+// Host resources of gp_ode_sample's status reads (a pinned int and an event on the stream's device),
+// leased from a per-device pool for one call and returned after it. A per-thread cache bound them to
+// the first device a thread used, which breaks a host that drives several GPUs from one thread (or a
+// cgo host, whose goroutines move between OS threads); creating them per call would cost a
+// device-synchronising hipHostFree. The pool holds at most as many readers per device as calls ever
+// ran on it at once.
 struct StatusReader {
-    int* pinned = nullptr;
-    hipEvent_t ev = nullptr;
-    int init() {
-        if (pinned) return 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&pinned), 64, hipHostMallocDefault) != hipSuccess) return -1;
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
-        return 0;
+    int* pinned;
+    hipEvent_t ev;
+    int dev;
+};
+std::mutex g_status_mu;
+std::vector<StatusReader> g_status_pool;
+
+struct StatusLease {
+    StatusReader r{nullptr, nullptr, -1};
+    int acquire(hipStream_t stream) {
+        int cur = 0, dev = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return -1;
+        dev = cur;
+        if (stream != nullptr && hipStreamGetDevice(stream, &dev) != hipSuccess) return -1;
+        {
+            std::lock_guard<std::mutex> lk(g_status_mu);
+            for (size_t i = 0; i < g_status_pool.size(); ++i)
+                if (g_status_pool[i].dev == dev) {
+                    r = g_status_pool[i];
+                    g_status_pool.erase(g_status_pool.begin() + (long)i);
+                    return 0;
+                }
+        }
+        if (dev != cur && hipSetDevice(dev) != hipSuccess) return -1;
+        r.dev = dev;
+        const bool ok = hipHostMalloc(reinterpret_cast<void**>(&r.pinned), 64, hipHostMallocDefault) == hipSuccess &&
+                        hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) == hipSuccess;
+        if (dev != cur) (void)hipSetDevice(cur);
+        return ok ? 0 : -1;
+    }
+    ~StatusLease() {
+        if (r.pinned != nullptr && r.ev != nullptr) {
+            std::lock_guard<std::mutex> lk(g_status_mu);
+            g_status_pool.push_back(r);
+        }
     }
 };
-thread_local StatusReader g_status;
 }  // namespace
 
 __global__ void f32_to_f64_kernel(const float* __restrict__ in, double* __restrict__ out, long long n) {
@@ -757,7 +791,8 @@ extern "C" int gp_ode_sample(const gp_head_weights* w, const float* pobj, const 
     GP_REQUIRE(steps != 1, "ode_sample: steps must be 0 (t_eval unset) or >= 2");
     const OdeSampleLayout L = ode_sample_layout(rows);
     GP_REQUIRE(workspace_bytes >= L.total, "ode_sample: workspace too small (gp_ode_sample_workspace_size)");
-    GP_REQUIRE(g_status.init() == 0, "ode_sample: pinned status word / event");
+    StatusLease status;
+    GP_REQUIRE(status.acquire(stream) == 0, "ode_sample: pinned status word / event");
     char* ws = static_cast<char*>(workspace);
     double* y[2] = {reinterpret_cast<double*>(ws + L.y[0]), reinterpret_cast<double*>(ws + L.y[1])};
     double* K[ODE_NK];
@@ -826,11 +861,11 @@ extern "C" int gp_ode_sample(const gp_head_weights* w, const float* pobj, const 
         GP_REQUIRE(a < 100000, "ode_sample: attempt limit reached");
         if ((rc = launch(a + 1, 1))) return rc;   // decides attempt a, prepares a + 1
         const char* src = static_cast<const char*>(aws) + ((a + 2) & 1) * rec + stat_off;
-        GP_REQUIRE(hipMemcpyAsync(g_status.pinned, src, 4, hipMemcpyDeviceToHost, stream) == hipSuccess &&
-                       hipEventRecord(g_status.ev, stream) == hipSuccess, "ode_sample: status read");
+        GP_REQUIRE(hipMemcpyAsync(status.r.pinned, src, 4, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                       hipEventRecord(status.r.ev, stream) == hipSuccess, "ode_sample: status read");
         if ((rc = launch(a + 1, 2))) return rc;   // attempt a + 1 (a no-op once the solve has ended)
-        GP_REQUIRE(hipEventSynchronize(g_status.ev) == hipSuccess, "ode_sample: status wait");
-        if (*g_status.pinned != 0) break;
+        GP_REQUIRE(hipEventSynchronize(status.r.ev) == hipSuccess, "ode_sample: status wait");
+        if (*status.r.pinned != 0) break;
     }
     OdeCtl c;
     GP_REQUIRE(hipMemcpyAsync(&c, static_cast<const char*>(aws) + ((a + 2) & 1) * rec, sizeof(OdeCtl),

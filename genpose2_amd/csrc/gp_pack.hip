@@ -76,26 +76,28 @@ int split_exponent(const std::vector<float>& w) {
     return m > 0.f ? 14 - (int)std::floor(std::log2((double)m)) : 0;
 }
 
-// bits of the f16 hi/lo planes of w * 2^e in the v_mfma_f32_16x16x32_f16 A order (pack_h16_fragments):
-// packed[T][c][plane][q][i][half][j4] = plane(W[16T + i][32c + 16 half + 4q + j4])
-std::vector<uint32_t> pack_h16(const std::vector<float>& w, int n_out, int k_in, int e) {
+// bits of the f16 planes of x = w * 2^e in the v_mfma_f32_16x16x32_f16 A order (pack_h16_fragments):
+// packed[T][c][plane][q][i][half][j4] = plane(W[16T + i][32c + 16 half + 4q + j4]); planes 2 (hi, lo) or
+// 3 (hi, mid, lo: plane p = f16 of x minus the planes before it)
+std::vector<uint32_t> pack_h16(const std::vector<float>& w, int n_out, int k_in, int e, int planes = 2) {
     const int NT = n_out / 16, KC = k_in / 32;
-    std::vector<uint16_t> h((size_t)n_out * k_in * 2);
+    std::vector<uint16_t> h((size_t)n_out * k_in * planes);
     const float s = std::ldexp(1.0f, e);
     for (int T = 0; T < NT; ++T)
         for (int c = 0; c < KC; ++c)
-            for (int plane = 0; plane < 2; ++plane)
-                for (int q = 0; q < 4; ++q)
-                    for (int i = 0; i < 16; ++i)
-                        for (int half = 0; half < 2; ++half)
-                            for (int j4 = 0; j4 < 4; ++j4) {
-                                const float x = w[(size_t)(16 * T + i) * k_in + 32 * c + 16 * half + 4 * q + j4] * s;
-                                const _Float16 hi = (_Float16)x;
-                                const _Float16 v = plane == 0 ? hi : (_Float16)(x - (float)hi);
+            for (int q = 0; q < 4; ++q)
+                for (int i = 0; i < 16; ++i)
+                    for (int half = 0; half < 2; ++half)
+                        for (int j4 = 0; j4 < 4; ++j4) {
+                            float r = w[(size_t)(16 * T + i) * k_in + 32 * c + 16 * half + 4 * q + j4] * s;
+                            for (int plane = 0; plane < planes; ++plane) {
+                                const _Float16 v = (_Float16)r;
+                                r = r - (float)v;
                                 uint16_t bits;
                                 std::memcpy(&bits, &v, 2);
-                                h[((((((size_t)T * KC + c) * 2 + plane) * 4 + q) * 16 + i) * 2 + half) * 4 + j4] = bits;
+                                h[((((((size_t)T * KC + c) * planes + plane) * 4 + q) * 16 + i) * 2 + half) * 4 + j4] = bits;
                             }
+                        }
     std::vector<uint32_t> out(h.size() / 2);
     std::memcpy(out.data(), h.data(), h.size() * 2);
     return out;
@@ -270,8 +272,8 @@ bool pack_heads(StateDict& sd, Packer& P, int64_t* f) {
     f[11] = P.add(te_b, 128);
     f[12] = P.add(h1t_t);
     const int e2 = split_exponent(w_pe2), eh = split_exponent(h1_pose);
-    f[13] = P.add_bits(pack_h16(w_pe2, 256, 256, e2));
-    f[14] = P.add_bits(pack_h16(h1_pose, 768, 256, eh));
+    f[13] = P.add_bits(pack_h16(w_pe2, 256, 256, e2, 3));      // pack.HEAD_PLANES
+    f[14] = P.add_bits(pack_h16(h1_pose, 768, 256, eh, 3));
     // split_constants: activation bounds, rounded to float32 then one step up
     float b0 = 0.f, b2 = 0.f;
     for (int i = 0; i < 256; ++i) {

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
                                                        const float* __restrict__ tproj, float sigma,
                                                        const float* __restrict__ x, int rows, int kper,
                                                        float* __restrict__ out) {
-    __shared__ HeadSmem<1, EVAL_WV> sm;
+    __shared__ HeadSmem<1, EVAL_WV, SPLIT ? X3P : 0> sm;
     __shared__ int obj[16];
     const int r0 = blockIdx.x * 16;
     SplitScalars hs = {};
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
         obj[threadIdx.x] = (r < rows ? r : rows - 1) / kper;
     }
     if constexpr (SPLIT)
-        head_trunk_split<1, EVAL_WV>(w, pobj, tproj, obj, sm, 0, hs);
+        head_trunk_x3<1, EVAL_WV>(w, pobj, tproj, obj, sm, 0, hs);
     else
         head_trunk<1, EVAL_WV>(w, pobj, tproj, obj, sm);
     if (MODE == 0) {
@@ -178,7 +178,7 @@ template <int NT, int WV, bool SPLIT>
 __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
     constexpr int ROWS = NT * 16;
     static_assert(NT < WV, "at least one wave besides the update waves");
-    __shared__ HeadSmem<NT, WV> sm;
+    __shared__ HeadSmem<NT, WV, SPLIT ? X3P : 0> sm;
     __shared__ int obj[ROWS];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     }
     stage_small_weights<NT, WV, 64 * NT, !SPLIT>(a.w, sm);
     if constexpr (SPLIT)
-        head_trunk_split<NT, WV, true>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
+        head_trunk_x3<NT, WV, true>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
     else
         head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
     PC_MARK(7);

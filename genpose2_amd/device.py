@@ -164,15 +164,16 @@ class HeadModel:
         self.lib = _lib.load()
         self.device = device
         self.up = _Uploaded(pack.pack_heads(sd), device)
-        self.set_arith(os.environ.get("GENPOSE2_HEAD_ARITH", "split_f16"))
+        self.set_arith(os.environ.get("GENPOSE2_HEAD_ARITH", "f16x3"))
         self._pc_ws: Optional[torch.Tensor] = None
 
     def set_arith(self, arith: str) -> None:
         """Per-candidate GEMM arithmetic of every head kernel (PC step, score/energy eval, ODE stages):
-        "split_f16" (pose_encoder.2 and head layer 1's pose block as f16 hi/lo MFMA products,
-        gp_head.h) or "f32" (exact fp32 MFMA)."""
-        if arith not in ("split_f16", "f32"):
-            raise ValueError(f"unknown head arithmetic {arith!r} (split_f16 | f32)")
+        "f16x3" (pose_encoder.2 and head layer 1's pose block on f16 MFMA with three planes per operand
+        and six products: every bit of the fp32 operands, products to ~2^-33, fp32 accumulation;
+        gp_head.h) or "f32" (exact fp32 MFMA, v_mfma_f32_16x16x4_f32)."""
+        if arith not in ("f16x3", "f32"):
+            raise ValueError(f"unknown head arithmetic {arith!r} (f16x3 | f32)")
         ptrs = {k: self.up.ptr(k) for k in pack.HEAD_FIELDS}
         if arith == "f32":
             ptrs.update(pe2_h=None, h1p_h=None, hsc=None)

@@ -132,9 +132,11 @@ def split_exponent(w: np.ndarray) -> int:
     return 14 - int(np.floor(np.log2(m))) if m > 0 else 0
 
 
-def pack_h16_fragments(w: np.ndarray, e: int) -> np.ndarray:
-    """(n_out, k_in) -> bits (int32 words) of the f16 hi/lo planes of w * 2**e (hi = f16(x), lo = f16(x - hi)) in
-    the A-operand order of v_mfma_f32_16x16x32_f16 used by gp_head.h's split trunk:
+def pack_h16_fragments(w: np.ndarray, e: int, planes: int = 2) -> np.ndarray:
+    """(n_out, k_in) -> bits (int32 words) of the f16 planes of x = w * 2**e in the A-operand order of
+    v_mfma_f32_16x16x32_f16. planes = 2: hi = f16(x), lo = f16(x - hi) (the encoder's split-f16
+    GEMMs); planes = 3: hi, mid = f16(x - hi), lo = f16(x - hi - mid), every bit of x (the head
+    trunk's f16x3 GEMMs, gp_head.h):
 
         packed[T][c][plane][lane][j] = plane(W[16T + (lane & 15)][32c + 16*(j // 4) + 4*(lane >> 4) + j % 4])
 
@@ -142,16 +144,23 @@ def pack_h16_fragments(w: np.ndarray, e: int) -> np.ndarray:
     feeds the B operand without moving data between lanes. One (T, c, plane) is 1 KiB."""
     n_out, k_in = w.shape
     assert n_out % 16 == 0 and k_in % 32 == 0, (n_out, k_in)
-    x = (np.asarray(w, np.float32) * np.float32(2.0 ** e)).astype(np.float32)
-    hi = x.astype(np.float16)
-    lo = (x - hi.astype(np.float32)).astype(np.float16)
+    assert planes in (2, 3), planes
+    r = (np.asarray(w, np.float32) * np.float32(2.0 ** e)).astype(np.float32)
+    ps = []
+    for _ in range(planes):
+        h = r.astype(np.float16)
+        ps.append(h)
+        r = (r - h.astype(np.float32)).astype(np.float32)   # exact: r and h agree in their leading bits
     NT, KC = n_out // 16, k_in // 32
 
     def frag(p):   # [T][i][c][half][q][j4] -> [T][c][q][i][half][j4]: lane = 16q + i, j = 4*half + j4
         return p.reshape(NT, 16, KC, 2, 4, 4).transpose(0, 2, 4, 1, 3, 5)
-    out = np.stack([frag(hi), frag(lo)], axis=2)
+    out = np.stack([frag(p) for p in ps], axis=2)
     # int32 words (two f16 each): every torch.distributed backend broadcasts int32
     return np.ascontiguousarray(out).reshape(-1).view(np.int32)
+
+
+HEAD_PLANES = 3   # f16 planes per weight of the head trunk's GEMMs (pe2_h, h1p_h)
 
 
 def split_constants(p: Dict[str, np.ndarray], e2: int, eh: int) -> np.ndarray:
@@ -185,8 +194,8 @@ def pack_heads(sd: weights.StateDict) -> Dict[str, np.ndarray]:
     out = {k: np.ascontiguousarray(v, np.float32) for k, v in out.items()}
     h1_pose = p["h1_pose"].reshape(3 * H, arch.POSE_HID)
     e2, eh = split_exponent(p["pe2_w"]), split_exponent(h1_pose)
-    out["pe2_h"] = pack_h16_fragments(p["pe2_w"], e2)
-    out["h1p_h"] = pack_h16_fragments(h1_pose, eh)
+    out["pe2_h"] = pack_h16_fragments(p["pe2_w"], e2, HEAD_PLANES)
+    out["h1p_h"] = pack_h16_fragments(h1_pose, eh, HEAD_PLANES)
     out["hsc"] = np.asarray(split_constants(p, e2, eh), np.float32)
     return out
 

@@ -7,6 +7,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench[:ARGS]     python bench.py ARGS (comma-separated, e.g. bench:--config,5,--steps,2)
 #   prof[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS (--steps 3 --warmup 1 by default)
+#   bin:PROGRAM[:ARGS] a built program (e.g. scripts/mfma_round_probe)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS
 #   kprof:SCRIPT[:ARGS] rocprofv3 --kernel-trace --stats of python3 SCRIPT ARGS
 #   pmc[:ARGS]       scripts/pmc_passes.sh over scripts/pmc_target.py ARGS
@@ -23,7 +24,7 @@ for step in "$@"; do
   case $name in
     tests)
       K=(); [ -n "$arg" ] && K=(-k "$arg")
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > $out.log 2>&1 ;;
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${K[@]}" > $out.log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out.log 2>&1 ;;
     bench)
@@ -32,6 +33,8 @@ for step in "$@"; do
       [ ${#A[@]} -eq 0 ] && A=(--steps 3 --warmup 1 --no-cpu-baseline)
       rm -rf $out
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o k -- python3 bench.py "${A[@]}" > $out.log 2>&1 ;;
+    bin)
+      s=${A[0]}; timeout -k 10 120 $s "${A[@]:1}" > $out.out 2> $out.err ;;
     py)
       s=${A[0]}; timeout -k 10 600 python -u $s "${A[@]:1}" > $out.out 2> $out.err ;;
     kprof)

@@ -1,0 +1,219 @@
+"""CPU study: which rounding dominates the PC trajectory's error against float64, and how the GEMM
+arithmetic of the HIP kernels compares with exact fp32 there.
+
+The hoisted sampler (pose_encoder.0 -> pose_encoder.2 -> head layer 1 pose block on top of the fp32
+object/time rows -> head layer 2 -> / (sigma + 1e-7) -> Langevin corrector, predictor, Gram-Schmidt)
+runs on the pc_r4800_t100 fixture's inputs in float64 (the baseline) and in fp32 with the two
+per-candidate GEMMs (pose_encoder.2, head layer 1's pose block) emulated as:
+
+  f64     float64 GEMM rounded once to fp32 (an ideal fp32 GEMM: isolates every other rounding)
+  torch   torch's CPU fp32 GEMM (the reference's arithmetic)
+  mfma4   v_mfma_f32_16x16x4_f32: each 4-deep step's exact sum added to the fp32 accumulator with one
+          rounding (the exact-fp32 kernel)
+  h3      split f16, 2 planes, 3 products per 32-deep chunk into one accumulator (the round-3 trunk)
+  h6      split f16, 3 planes, the 6 products of plane order <= 2 into one accumulator, smallest first
+  h6x2    as h6, but hi*hi into a main accumulator and the 5 cross products into a second one,
+          summed once at the end of the layer
+
+Each f16 MFMA is modelled as its 32 exact products summed exactly and added to the accumulator with
+one rounding. Prints the rotation error (max, p99.9, mean) against the float64 run.
+Usage: python scripts/precision_study3.py [variant ...]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+from genpose2_amd import arch, weights  # noqa: E402
+
+F32, F64 = torch.float32, torch.float64
+torch.set_num_threads(8)
+
+
+def f16(x):
+    return x.to(torch.float16).to(F64)
+
+
+def pow2(m):
+    e = torch.where(m > 0, 14 - torch.floor(torch.log2(torch.where(m > 0, m, torch.ones_like(m)))), torch.zeros_like(m))
+    return torch.exp2(e)
+
+
+def planes(x, n):
+    out, r = [], x.to(F64)
+    for _ in range(n):
+        h = f16(r)
+        out.append(h)
+        r = r - h
+    return out
+
+
+def gemm(x, w, mode):
+    """x (R,K) fp32, w (N,K) fp32 -> (R,N) fp32 under `mode`."""
+    if mode == "torch":
+        return x @ w.T
+    if mode == "f64":
+        return (x.to(F64) @ w.to(F64).T).to(F32)
+    R, K = x.shape
+    acc = torch.zeros((R, w.shape[0]), dtype=F64)
+    if mode == "mfma4":
+        xd, wd = x.to(F64), w.to(F64)
+        for k0 in range(0, K, 4):
+            acc = (acc + xd[:, k0:k0 + 4] @ wd[:, k0:k0 + 4].T).to(F32).to(F64)
+        return acc.to(F32)
+    sx = pow2(x.abs().amax(1)).to(F64)[:, None]
+    sw = pow2(w.abs().max()).to(F64)
+    n = 2 if mode == "h3" else 3
+    xs, ws = planes(x.to(F64) * sx, n), planes(w.to(F64) * sw, n)
+    pairs = [(i, j) for i in range(n) for j in range(n) if i + j < (2 if mode == "h3" else 3)]
+    pairs.sort(key=lambda p: -(p[0] + p[1]))          # smallest first
+    corr = torch.zeros_like(acc)
+    for k0 in range(0, K, 32):
+        sl = slice(k0, k0 + 32)
+        for i, j in pairs:
+            s = xs[i][:, sl] @ ws[j][:, sl].T
+            if mode == "h6x2" and (i, j) != (0, 0):
+                corr = (corr + s).to(F32).to(F64)
+            else:
+                acc = (acc + s).to(F32).to(F64)
+    if mode == "h6x2":
+        acc = (acc + corr).to(F32).to(F64)
+    return (acc / (sx * sw)).to(F32)
+
+
+class Model:
+    def __init__(self, sd, dt):
+        n = "pose_score_net"
+        g = lambda k: torch.from_numpy(np.asarray(sd[f"{n}.{k}"])).to(dt)  # noqa: E731
+        self.dt = dt
+        self.W0, self.b0 = g("pose_encoder.0.weight"), g("pose_encoder.0.bias")
+        self.W2, self.b2 = g("pose_encoder.2.weight"), g("pose_encoder.2.bias")
+        self.te_W, self.te1w, self.te1b = g("t_encoder.0.W"), g("t_encoder.1.weight"), g("t_encoder.1.bias")
+        self.h1w = [g(f"{h}.0.weight") for h in arch.HEAD_NAMES]
+        self.h1b = [g(f"{h}.0.bias") for h in arch.HEAD_NAMES]
+        self.h2w = [g(f"{h}.2.weight") for h in arch.HEAD_NAMES]
+        self.h2b = [g(f"{h}.2.bias") for h in arch.HEAD_NAMES]
+        self.W1p = torch.cat([w[:, 1024 + 128:] for w in self.h1w], 0)   # (768, 256) pose block
+
+    def obj_rows(self, feat):
+        return torch.cat([feat @ w[:, :1024].T + b for w, b in zip(self.h1w, self.h1b)], 1)   # (B,768)
+
+    def time_row(self, t):
+        x = t * self.te_W * 2 * np.pi
+        emb = torch.cat([torch.sin(x), torch.cos(x)])
+        tf = torch.relu(emb @ self.te1w.T + self.te1b)
+        return torch.cat([tf @ w[:, 1024:1024 + 128].T for w in self.h1w])
+
+    def f(self, x, init, mode, hi=None):
+        """hi: a Model in float64 whose parts named in HI64 run in float64 (rounded to fp32 after)."""
+        P = lambda part: hi is not None and part in HI64  # noqa: E731
+        if P("pe0"):
+            h = torch.relu(x.to(F64) @ hi.W0.T + hi.b0).to(F32)
+        else:
+            h = torch.relu(x @ self.W0.T + self.b0)
+        if self.dt == F64:
+            pf = torch.relu(h @ self.W2.T + self.b2)
+            u = torch.relu(init + pf @ self.W1p.T)
+        else:
+            pf = torch.relu(gemm(h, self.W2, mode) + self.b2)
+            u = torch.relu(init + gemm(pf, self.W1p, mode))
+        if P("h2"):
+            u = u.to(F64)
+            return torch.cat([u[:, 256 * i:256 * (i + 1)] @ hi.h2w[i].T + hi.h2b[i] for i in range(3)], 1).to(F32)
+        return torch.cat([u[:, 256 * i:256 * (i + 1)] @ self.h2w[i].T + self.h2b[i] for i in range(3)], 1)
+
+
+def gs(x):
+    a1, a2 = x[:, :3], x[:, 3:6]
+    b1 = a1 / torch.clamp(a1.norm(dim=-1, keepdim=True), min=1e-12)
+    b2 = a2 - (b1 * a2).sum(-1, keepdim=True) * b1
+    b2 = b2 / torch.clamp(b2.norm(dim=-1, keepdim=True), min=1e-12)
+    return torch.cat([b1, b2], -1)
+
+
+HI64 = set(os.environ.get("HI64", "").split(",")) - {""}
+
+
+def run(sd, feat, prior, z1, z2, K, T, dt, mode):
+    m = Model(sd, dt)
+    hi = Model(sd, F64) if HI64 and dt == F32 else None
+    feat = torch.from_numpy(feat).to(dt)
+    pobj = m.obj_rows(feat).repeat_interleave(K, 0)
+    if hi is not None and "init" in HI64:
+        pobj = hi.obj_rows(feat.to(F64)).repeat_interleave(K, 0)
+    ts = torch.linspace(1.0, arch.SAMPLING_EPS, T, dtype=dt)
+    step = ts[0] - ts[1]
+    x = torch.from_numpy(prior).to(dt)
+    R = x.shape[0]
+    coef = torch.tensor(arch.SNR * 3.0, dtype=dt)
+    for k in range(T):
+        t = ts[k]
+        sig = arch.SIGMA_MIN * (arch.SIGMA_MAX / arch.SIGMA_MIN) ** t
+        g = sig * torch.tensor(arch.DIFFUSION_SCALE, dtype=dt)
+        if hi is not None and "init" in HI64:
+            init = (pobj + hi.time_row(ts[k].to(F64))).to(F32)
+        else:
+            init = pobj + m.time_row(t)
+        grad = m.f(x, init, mode, hi) / (sig + 1e-7)
+        if hi is not None and "upd" in HI64:   # the update and state in float64 from here on
+            x, grad, t, dt_ = x.to(F64), grad.to(F64), ts[k].to(F64), F64
+            sig = arch.SIGMA_MIN * (arch.SIGMA_MAX / arch.SIGMA_MIN) ** t
+            g = sig * torch.tensor(arch.DIFFUSION_SCALE, dtype=F64)
+            step64 = (torch.linspace(1.0, arch.SAMPLING_EPS, T, dtype=F64)[0] -
+                      torch.linspace(1.0, arch.SAMPLING_EPS, T, dtype=F64)[1])
+            gn = grad.norm(dim=-1).mean()
+            ls = 2 * (torch.tensor(arch.SNR * 3.0, dtype=F64) / gn) ** 2
+            x = x + ls * grad + torch.sqrt(2 * ls) * torch.from_numpy(z1[k]).to(F64)
+            x[:, :3] /= x[:, :3].norm(dim=-1, keepdim=True)
+            x[:, 3:6] /= x[:, 3:6].norm(dim=-1, keepdim=True)
+            mean = x + (-(g ** 2) * grad) * step64
+            x = mean + g * torch.sqrt(step64) * torch.from_numpy(z2[k]).to(F64)
+            x[:, :6] = gs(x[:, :6])
+            if "state" not in HI64:
+                x = x.to(F32)
+            mean = mean.to(F32) if "state" not in HI64 else mean
+            continue
+        gn = grad.norm(dim=-1).mean()
+        ls = 2 * (coef / gn) ** 2
+        x = x + ls * grad + torch.sqrt(2 * ls) * torch.from_numpy(z1[k]).to(dt)
+        x[:, :3] /= x[:, :3].norm(dim=-1, keepdim=True)
+        x[:, 3:6] /= x[:, 3:6].norm(dim=-1, keepdim=True)
+        mean = x + (-(g ** 2) * grad) * step
+        x = mean + g * torch.sqrt(step) * torch.from_numpy(z2[k]).to(dt)
+        x[:, :6] = gs(x[:, :6])
+    mean[:, :6] = gs(mean[:, :6])
+    return mean.to(F64).numpy()
+
+
+def main():
+    import large_noise
+    from oracle import oracle
+    name = os.environ.get("CASE", "pc_r4800_t100")
+    _, _, B, K, T, _, _ = large_noise.CASES[name]
+    T = int(os.environ.get("STEPS", T))
+    pts, center, prior, z1, z2 = large_noise.inputs(name)
+    sd = weights.synthetic_state_dict("score")
+    cache = f"/tmp/feat_{name}.npy"
+    if os.path.exists(cache):
+        feat = np.load(cache)
+    else:
+        feat = oracle.encoder_forward(sd, pts).astype(np.float32)
+        np.save(cache, feat)
+    t0 = time.time()
+    ref = run(sd, feat, prior, z1, z2, K, T, F64, None)
+    print(f"{name} T={T}: float64 run {time.time() - t0:.1f}s", flush=True)
+    for mode in sys.argv[1:] or ["f64", "torch", "mfma4", "h3", "h6", "h6x2"]:
+        t0 = time.time()
+        p = run(sd, feat, prior, z1, z2, K, T, F32, mode)
+        e = np.abs(p[:, :6] - ref[:, :6])
+        print(f"{mode:6s} rot max {e.max():.3e} p99.9 {np.percentile(e, 99.9):.3e} mean {e.mean():.3e} "
+              f"({time.time() - t0:.0f}s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -16,6 +16,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
 
 
+# Arithmetic of the GPU kernels a parity test runs: "fast" = the defaults (head GEMMs in f16x3: three f16
+# planes and six MFMA products, fp32-faithful; encoder SA levels 1-3 / token GEMMs in split-f16), "f32" = exact
+# fp32 MFMA everywhere, "heads" = the f16x3 head GEMMs over the exact-fp32 encoder (isolates the head kernels'
+# arithmetic against "f32").
+ARITHS = ("fast", "f32")
+ARITHS3 = ("fast", "heads", "f32")
+
+
+def set_arith(agent, arith, encoder=None):
+    """Sets `agent`'s head arithmetic and its encoder's (or `encoder`: "fast" | "f32", default the same)."""
+    enc = ("f32" if arith == "heads" else arith) if encoder is None else encoder
+    agent.heads.set_arith("f32" if arith == "f32" else "f16x3")
+    if hasattr(agent.encoder, "set_arith"):
+        agent.encoder.set_arith("split_f16" if enc == "fast" else "f32")
+
+
 def golden(name):
     return np.load(os.path.join(GOLDEN, f"golden_{name}.npz"), allow_pickle=False)
 

@@ -79,6 +79,35 @@ def test_split_f16_packing_layout_and_bounds(score_sd):
     assert e2 == pack.split_exponent(p["pe2_w"]) and heads["pe2_h"].dtype == np.int32
 
 
+def test_f16x3_head_planes_hold_every_bit(score_sd):
+    """The head trunk's weight planes (pack.HEAD_PLANES = 3: hi, mid, lo): hi + mid + lo reproduces
+    x = W * 2^e (max |x| in [2^14, 2^15)) to within half an f16 subnormal step, 2^-25 -- exactly unless
+    the lo plane underflows, i.e. to 2^-39 of the layer's largest weight -- for every weight of
+    pose_encoder.2 and head layer 1's pose block, in the [T][c][plane][lane][j] order gp_head.h streams."""
+    from genpose2_amd import arch, pack, weights
+    heads = pack.pack_heads(score_sd)
+    p = weights.head_params(score_sd)
+    for key, W in (("pe2_h", p["pe2_w"]), ("h1p_h", p["h1_pose"].reshape(3 * arch.HEAD_HID, arch.POSE_HID))):
+        e = pack.split_exponent(W)
+        n_out, k_in = W.shape
+        pl = heads[key].view(np.float16).reshape(n_out // 16, k_in // 32, 3, 4, 16, 2, 4)
+        assert pl.size == 3 * W.size
+        full = pl.transpose(2, 0, 4, 1, 5, 3, 6).reshape(3, n_out, k_in).astype(np.float64)
+        x = W.astype(np.float64) * 2.0 ** e
+        err = np.abs(full[0] + full[1] + full[2] - x)
+        assert err.max() <= 2.0 ** -25, (key, err.max())
+        assert (err == 0).mean() > 0.999, key
+        assert np.array_equal(full[0], x.astype(np.float16))       # hi = f16(x)
+        assert (np.abs(full[2]) <= np.abs(x) * 2.0 ** -21).all()   # lo is ~2^-22 of the value
+    # the 2-plane encoder layout is the first two planes of the same rule
+    rng = np.random.default_rng(2)
+    w = (rng.normal(size=(32, 64)) * 0.05).astype(np.float32)
+    e = pack.split_exponent(w)
+    two = pack.pack_h16_fragments(w, e, 2).view(np.float16).reshape(2, 2, 2, -1)
+    three = pack.pack_h16_fragments(w, e, 3).view(np.float16).reshape(2, 2, 3, -1)
+    assert np.array_equal(two, three[:, :, :2])
+
+
 def test_encoder_packing_covers_every_layer(score_sd):
     from genpose2_amd import arch, pack, weights
     buf, off = pack.pack_encoder(score_sd)
@@ -430,7 +459,63 @@ def test_bench_gpus2_without_gpus_fails_loudly():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--no-cpu-baseline"],
                        capture_output=True, text=True, env=env, timeout=300)
-    assert p.returncode != 0 and "HIP device" in p.stderr and '"n_gpus"' not in p.stdout
+    assert p.returncode != 0 and ("HIP device" in p.stderr or "cannot count" in p.stderr), p.stderr[-2000:]
+    assert '"n_gpus"' not in p.stdout
+
+
+def test_bench_counts_gpus_without_hip(monkeypatch, tmp_path):
+    """bench.py --gpus N counts the node's GPUs before the launcher starts, without any HIP call: amdsmi,
+    else the KFD topology (nodes with a non-zero gfx_target_version); with neither it exits non-zero and
+    never falls back to torch.cuda.device_count() (hipGetDeviceCount in the parent of the ranks)."""
+    b = _bench_module()
+
+    def hip_touched(*a, **k):
+        raise AssertionError("HIP touched before the launcher")
+    for fn in ("device_count", "is_available", "init", "_lazy_init", "set_device", "current_device"):
+        monkeypatch.setattr(torch.cuda, fn, hip_touched)
+    monkeypatch.setitem(sys.modules, "amdsmi", None)          # import amdsmi -> ImportError
+    # a fake KFD topology: one CPU node, two GPU nodes
+    for i, ver in enumerate((0, 90500, 90500)):
+        d = tmp_path / "nodes" / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count 4\ngfx_target_version {ver}\nsimd_count 0\n")
+    monkeypatch.setattr(b, "KFD_NODES", str(tmp_path / "nodes" / "*" / "properties"))
+    assert b.count_gpus({}) == 2
+    assert b.count_gpus({"HIP_VISIBLE_DEVICES": "0"}) == 1
+    monkeypatch.setattr(b, "KFD_NODES", str(tmp_path / "absent" / "*" / "properties"))
+    assert b.count_gpus({}) is None
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit) as e:
+        b.main()
+    assert "cannot count" in str(e.value.code)
+
+
+def test_bench_rocprof_source_matches_config(tmp_path, monkeypatch):
+    """The roofline's rocprof figure comes from a summary of the same config (row count, tile) and kernel
+    instantiation, newest round first, then reverse lexical order -- never another config's file or an
+    mtime order."""
+    b = _bench_module()
+    monkeypatch.setattr(b, "REPO", str(tmp_path))
+    hdr = "Name,Calls,TotalDurationNs,AverageNs,Percentage,MinNs,MaxNs,StdDev\n"
+
+    def csv(path, kernel, avg):
+        path.parent.mkdir(parents=True, exist_ok=True)
+        path.write_text(hdr + f'"{kernel}(PCArgs, int, PCStep, PCStep)",501,1,{avg},50,1,1,0\n')
+    k4, k1 = "void pc_step_kernel<4, 8, true>", "void pc_step_kernel<1, 8, false>"
+    csv(tmp_path / "profiles" / "r3" / "config4_r3f_kernel_stats.csv", k4, 23890)
+    csv(tmp_path / "profiles" / "r4" / "config4_a_kernel_stats.csv", k4, 30000)
+    csv(tmp_path / "profiles" / "r4" / "config4_b_kernel_stats.csv", k4, 31000)
+    csv(tmp_path / "profiles" / "r4" / "config5_a_kernel_stats.csv", k4, 60000)
+    csv(tmp_path / "profiles" / "r4" / "config4_pointwise_a_kernel_stats.csv", k4, 32000)
+    csv(tmp_path / "profiles" / "r10" / "config4_z_kernel_stats.csv", k1, 70000)
+    assert b.load_rocprof(k4, 4)["avg_launch_us"] == 31.0           # r4 beats r3; b after a
+    assert b.load_rocprof(k4, 4)["source"].endswith("r4/config4_b_kernel_stats.csv")
+    assert b.load_rocprof(k1, 4)["avg_launch_us"] == 70.0           # r10 > r4 numerically
+    assert b.load_rocprof(k4, 5)["avg_launch_us"] == 60.0
+    assert b.load_rocprof(k4, 4, "pointwise")["avg_launch_us"] == 32.0
+    assert b.load_rocprof(k4, 2) is None
 
 
 def test_bench_launcher_starts_world2_gloo():

@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import ARITHS, ARITHS3, golden, set_arith
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -69,7 +69,7 @@ def _rank_mismatches(e, idx_ref, e64, tol):
     return int((order != idx_ref).sum()), bad
 
 
-@pytest.mark.parametrize("arith", ["split_f16", "f32"])
+@pytest.mark.parametrize("arith", ARITHS)
 def test_energy_rank_aggregate_r12800_vs_reference(arith):
     """Config 4's EnergyNet leg on the reference's own 12,800 PC candidates: energies within 1e-5 of
     max|ref| per object, the sort order identical, the aggregated 4x4 (with and without DBSCAN) within
@@ -85,8 +85,7 @@ def test_energy_rank_aggregate_r12800_vs_reference(arith):
     _, cid, B, K, _, _, _ = large_noise.CASES[src]
     pts, center = synthetic.make_batch(cid, B, 1024)
     agent = _agent(agent_type="energy")
-    agent.heads.set_arith(arith)
-    agent.encoder.set_arith(arith)
+    set_arith(agent, arith)
     data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
     keep = int(K * 0.4)
 
@@ -139,7 +138,7 @@ def test_energy_rank_aggregate_r12800_vs_reference(arith):
     _check_agg(got[same], g["cl_aggregated_c1"][same])
 
 
-@pytest.mark.parametrize("arith", ["split_f16", "f32"])
+@pytest.mark.parametrize("arith", ARITHS)
 def test_config5_shape_vs_reference(arith):
     """B=256, N=2048, K=100 (R=25,600: 400 PC workgroups, two passes), T=100, reference noise."""
     import large_noise
@@ -150,8 +149,7 @@ def test_config5_shape_vs_reference(arith):
     pts, center, prior, z1, z2 = large_noise.inputs(name)
     assert pts.shape == (256, 2048, 3) and B * K == 25600
     agent = _agent(sampling_steps=T)
-    agent.heads.set_arith(arith)
-    agent.encoder.set_arith(arith)
+    set_arith(agent, arith)
     agent.noise_feed = NoiseFeed(torch.from_numpy(prior), torch.from_numpy(np.ascontiguousarray(z1)),
                                  torch.from_numpy(np.ascontiguousarray(z2)))
     del z1, z2
@@ -171,7 +169,7 @@ def test_config5_shape_vs_reference(arith):
     assert _rel(length.cpu().numpy(), g["scale_length"]) < 1e-5
 
 
-@pytest.mark.parametrize("arith", ["split_f16", "f32"])
+@pytest.mark.parametrize("arith", ARITHS3)
 def test_pc_single_step_pins_r12800(arith):
     import large_noise
     g = golden("large_steps_r12800")
@@ -179,8 +177,7 @@ def test_pc_single_step_pins_r12800(arith):
     _, _, B, K, T, _, _ = large_noise.CASES[src]
     pts, center, prior, z1, z2 = large_noise.inputs(src)
     agent = _agent(sampling_steps=T)
-    agent.heads.set_arith(arith)
-    agent.encoder.set_arith(arith)
+    set_arith(agent, arith)
     cdev = torch.from_numpy(center).to(DEV)
     feat = agent.encoder.forward(torch.from_numpy(pts).to(DEV))
     pobj = agent.heads.object_proj(feat)
@@ -206,6 +203,62 @@ def test_pc_single_step_pins_r12800(arith):
         assert tr < 1e-5 and mine <= 2 * own, (j, rot, mine, own, tr)
         if own < 5e-6:   # a well-conditioned step: the north-star bar against the reference itself
             assert rot < 1e-5, (j, rot)
+
+
+def _score64(sd, feat, x, t32):
+    """PoseScoreNet.forward (scorenet.py:215-275) in float64 from fp32 features, poses and time value."""
+    from genpose2_amd import arch, weights
+    p = {k: v.astype(np.float64) for k, v in weights.head_params(sd).items()}
+    t = float(t32)
+    xp = t * p["gfp_w"] * 2.0 * np.pi
+    tf = np.maximum(p["te_w"] @ np.concatenate([np.sin(xp), np.cos(xp)]) + p["te_b"], 0.0)
+    h = np.maximum(x.astype(np.float64) @ p["pe0_w"].T + p["pe0_b"], 0.0)
+    pf = np.maximum(h @ p["pe2_w"].T + p["pe2_b"], 0.0)
+    out = []
+    for k in range(3):
+        u = np.maximum(feat @ p["h1_pts"][k].T + p["h1_t"][k] @ tf + pf @ p["h1_pose"][k].T + p["h1_b"][k], 0.0)
+        out.append(u @ p["h2_w"][k].T + p["h2_b"][k])
+    sig = arch.SIGMA_MIN * (arch.SIGMA_MAX / arch.SIGMA_MIN) ** t
+    return np.concatenate(out, 1) / (sig + 1e-7)
+
+
+def test_head_gemm_arith_vs_float64_r12800():
+    """The head kernels' arithmetic, free of trajectory chaos: one score evaluation of the 12,800 states the
+    reference's PC run entered steps 1 and 400 with (golden_large_steps_r12800), with the same fp32 features
+    (exact-fp32 encoder) and fp32 object/time rows, in the f16x3 GEMMs (default) and in exact fp32 MFMA,
+    against the same network in float64. The f16x3 GEMMs form every product of the fp32 operands to ~2^-33
+    and accumulate hi*hi with one MFMA rounding per 32-deep chunk (v_mfma_f32_16x16x32_f16 measured at
+    ~0.9 x 2^-24 of its largest term per 33 terms vs v_mfma_f32_16x16x4_f32's ~0.6 per 5,
+    scripts/mfma_round_probe.hip), so over the 256-deep GEMMs their error is below exact fp32's: the
+    mean and 99.9th percentile of the score error are asserted <= exact fp32's, max printed."""
+    import large_noise
+    from genpose2_amd import weights
+    g = golden("large_steps_r12800")
+    src = str(g["src"])
+    _, _, B, K, T, _, _ = large_noise.CASES[src]
+    pts, _, _, _, _ = large_noise.inputs(src)
+    agent = _agent(sampling_steps=T)
+    agent.encoder.set_arith("f32")
+    feat = agent.encoder.forward(torch.from_numpy(pts).to(DEV))
+    pobj = agent.heads.object_proj(feat)
+    tab, tproj = agent._pc_table(T)
+    feat_rows = np.repeat(feat.cpu().numpy().astype(np.float64), K, 0)
+    sd = weights.synthetic_state_dict("score")
+    for j in (int(s) for s in g["steps"]):
+        x = torch.from_numpy(g[f"x_{j}"]).to(DEV).contiguous()
+        ref = _score64(sd, feat_rows, g[f"x_{j}"], tab[j, 0])
+        scale = np.abs(ref).max(1, keepdims=True)
+        stats = {}
+        for arith in ("f16x3", "f32"):
+            agent.heads.set_arith(arith)
+            s = agent.heads.score(pobj, tproj[j], float(tab[j, 1]), x, K).cpu().numpy().astype(np.float64)
+            e = np.abs(s - ref) / scale
+            stats[arith] = {"max": float(e.max()), "p999": float(np.percentile(e, 99.9)), "mean": float(e.mean())}
+        print(f"step {j} score vs float64 (per-row relative): f16x3 {stats['f16x3']}  exact fp32 {stats['f32']}")
+        for arith in stats:
+            assert stats[arith]["max"] < 1e-5, (j, arith, stats)
+        assert stats["f16x3"]["mean"] <= stats["f32"]["mean"] and stats["f16x3"]["p999"] <= stats["f32"]["p999"], stats
+    agent.heads.set_arith("f16x3")
 
 
 def test_config5_full_t1000_properties():
