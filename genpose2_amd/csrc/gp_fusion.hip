@@ -880,12 +880,12 @@ __global__ __launch_bounds__(FUS_THREADS) void mha_relpe_kernel(const float* __r
                     bm = fmaxf(bm, s[h][r]);
                 }
                 const float mn = fmaxf(m[h], rows_max(bm));
-                const float alpha = __expf(m[h] - mn);
+                const float alpha = expf(m[h] - mn);
                 m[h] = mn;
                 float ps = 0.f;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    s[h][r] = __expf(s[h][r] - mn);
+                    s[h][r] = expf(s[h][r] - mn);
                     ps += s[h][r];
                 }
                 lsum[h] = lsum[h] * alpha + ps;

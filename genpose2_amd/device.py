@@ -41,11 +41,15 @@ class _Uploaded:
 
 
 class EncoderGeometry:
-    """Geometry of one point batch in an encoder workspace (EncoderModel.geometry): valid until that
-    model's next encoder call; ``event`` marks its completion on the producing stream."""
+    """Geometry of one point batch in an encoder workspace (EncoderModel.geometry): valid until the producing
+    model recomputes geometry in that workspace (its next geometry() or forward() without a geometry), which
+    forward(geometry=...) detects through the producer's generation counter; ``event`` marks its completion on
+    the producing stream. Refilling the points tensor in place also invalidates it (not detectable: the key is
+    the tensor's address and shape)."""
 
-    def __init__(self, ws: torch.Tensor, event, key):
+    def __init__(self, ws: torch.Tensor, event, key, producer=None, gen: int = 0):
         self.ws, self.event, self.key = ws, event, key   # key: (points tensor address, (B, N))
+        self.producer, self.gen = producer, gen
 
 
 class EncoderModel:
@@ -58,6 +62,7 @@ class EncoderModel:
         self.wbuf = torch.from_numpy(buf).to(device)
         self._table = np.ascontiguousarray(offs, np.int64)     # [5][2][3][4] (gp_encoder_forward)
         self._ws: Optional[torch.Tensor] = None
+        self._gen = 0   # bumped whenever this model writes geometry into its workspace
         self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
 
     @property
@@ -103,11 +108,12 @@ class EncoderModel:
         pts = self._xyz(pts)
         B, N, _ = pts.shape
         ws = self.workspace(B, N)
+        self._gen += 1
         check(self.lib.gp_encoder_geometry(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()),
                                            ws.numel(), ctypes.c_void_p(stream_handle(self.device))), "encoder_geometry")
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
-        return EncoderGeometry(ws, ev, key)
+        return EncoderGeometry(ws, ev, key, self, self._gen)
 
     def forward(self, pts: torch.Tensor, return_workspace: bool = False,
                 geometry: Optional["EncoderGeometry"] = None):
@@ -120,6 +126,7 @@ class EncoderModel:
         ws = self.workspace(B, N)
         st = ctypes.c_void_p(stream_handle(self.device))
         if geometry is None:
+            self._gen += 1   # the self-contained pass rewrites the geometry in this workspace
             check(self.lib.gp_encoder_forward(
                 ctypes.c_void_p(self.wbuf.data_ptr()), self.offsets.ctypes.data_as(_lib.c_int64_p),
                 ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
@@ -127,6 +134,8 @@ class EncoderModel:
         else:
             if geometry.key != key:
                 raise ValueError("encoder geometry was computed for other points")
+            if geometry.producer is not None and geometry.producer._gen != geometry.gen:
+                raise ValueError("encoder geometry is stale: its model encoded other points since")
             torch.cuda.current_stream(self.device).wait_event(geometry.event)
             check(self.lib.gp_encoder_forward_geom(
                 ctypes.c_void_p(self.wbuf.data_ptr()), self.offsets.ctypes.data_as(_lib.c_int64_p),

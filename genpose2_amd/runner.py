@@ -119,13 +119,21 @@ class ShardedEvaluationPipeline:
 
     def load_ckpt(self, score: Optional[str] = None, energy: Optional[str] = None, scale: Optional[str] = None) -> None:
         """Load reference checkpoints on ``src`` only (paths may not exist on the other ranks), then
-        broadcast them to every rank."""
+        broadcast them to every rank. A failure on ``src`` (missing file, key mismatch) is broadcast
+        first and raised on every rank, so no rank is left waiting in the weight broadcast."""
         import torch.distributed as dist
+        err = [None]
         if dist.get_rank() == self.src:
-            for a, p in ((self.local.score_agent, score), (self.local.energy_agent, energy),
-                         (self.local.scale_agent, scale)):
-                if a is not None and p:
-                    a.load_ckpt(model_dir=p, model_path=True, load_model_only=True)
+            try:
+                for a, p in ((self.local.score_agent, score), (self.local.energy_agent, energy),
+                             (self.local.scale_agent, scale)):
+                    if a is not None and p:
+                        a.load_ckpt(model_dir=p, model_path=True, load_model_only=True)
+            except Exception as e:   # noqa: BLE001 -- re-raised below, on every rank
+                err[0] = f"{type(e).__name__}: {e}"
+        dist.broadcast_object_list(err, src=self.src)
+        if err[0] is not None:
+            raise RuntimeError(f"load_ckpt failed on rank {self.src}: {err[0]}")
         self.sync_weights()
 
     def sync_weights(self) -> None:

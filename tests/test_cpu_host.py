@@ -566,3 +566,64 @@ def test_energy_per_object_t_draws_like_reference():
         torch.manual_seed(bs)
         got = PoseNet.per_object_energy_t(bs)
         assert got.dtype == torch.float32 and torch.equal(got, ref.view(bs))
+
+
+def _vregs(op):
+    """VGPR/AGPR indices named by one assembler operand (v7, v[4:7], a[0:3]); empty for others."""
+    m = re.fullmatch(r"([va])\[(\d+):(\d+)\]", op)
+    if m:
+        return {(m.group(1), i) for i in range(int(m.group(2)), int(m.group(3)) + 1)}
+    m = re.fullmatch(r"([va])(\d+)", op)
+    return {(m.group(1), int(m.group(2)))} if m else set()
+
+
+def test_no_permlane_swap_in_mfma_hazard_window():
+    """the head trunks' v_permlane16/32_swap row reductions once overwrote registers that in-flight
+    MFMAs still read (the swap writes BOTH of its operands), which only instruction scheduling kept apart.
+    Disassembles every head kernel (PC step, score/energy eval, ODE stages) of the built library and checks that
+    no swap's SOURCE operand -- the register the compiler's hazard recognizer may treat as read-only; its vdst
+    gets the ISA's wait states (s_nop) like any VALU def -- is the result (vdst, which is also SrcC for the trunks'
+    chained accumulators) of a v_mfma issued within the previous 11 wait states: a VALU write to an in-flight MFMA's
+    vdst needs NumPasses + 2 wait states (8 passes for 16x16x4 f32, fewer for 16x16x32 f16: the compiler's own
+    s_nop 8 + 1 before such writes; a separate SrcC, SrcA and SrcB are read at issue -- the compiler rewrites
+    them on the next cycle), s_nop N counting N+1. Validated with the ROCm 7.2 clang that builds the library (hipcc --version)."""
+    llvm = "/opt/rocm/lib/llvm/bin"
+    build = os.path.join(REPO, "genpose2_amd", "csrc", "build")
+    if not all(os.path.exists(os.path.join(build, f)) for f in ("gp_score.o", "gp_ode.o")):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "genpose2_amd", "csrc")], check=True)
+    window, checked = 11, 0
+    for src in ("gp_score.o", "gp_ode.o"):
+        tmp = os.path.join(build, src + ".fatbin")
+        co = os.path.join(build, src + ".gfx950.co")
+        subprocess.run([f"{llvm}/llvm-objcopy", "--dump-section", f".hip_fatbin={tmp}", os.path.join(build, src),
+                        os.devnull], check=True)
+        subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={tmp}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        asm = subprocess.run([f"{llvm}/llvm-objdump", "-d", "--mcpu=gfx950", co], capture_output=True, text=True,
+                             check=True).stdout
+        os.remove(tmp)
+        os.remove(co)
+        kernel, recent = None, []   # recent: (wait states since issue, regs) of MFMAs
+        for line in asm.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(.+)>:", line)
+            if m:
+                kernel, recent = m.group(1), []
+                continue
+            code = line.split("//")[0].strip()
+            if not code or kernel is None:
+                continue
+            parts = code.replace(",", " ").split()
+            op, args = parts[0], parts[1:]
+            if not re.search(r"head_eval|pc_step|ode_stage", kernel):
+                continue
+            step = int(args[0]) + 1 if op == "s_nop" and args else 1
+            if op.startswith("v_permlane") and "swap" in op:
+                written = _vregs(args[1])
+                for _, regs in recent:
+                    assert not (written & regs), (kernel, code)
+                checked += 1
+            recent = [(w + step, r) for w, r in recent if w + step < window]
+            if op.startswith("v_mfma"):
+                regs = _vregs(args[0])   # vdst
+                recent.append((0, regs))
+    assert checked > 50, checked   # the trunks' row reductions were found

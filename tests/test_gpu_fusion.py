@@ -405,3 +405,92 @@ def test_pointwise_pred_func_end_to_end_vs_reference():
     agent.dino = None
     with pytest.raises(KeyError):
         agent.pred_func(dict(base), repeat_num=K)
+
+
+def _pointwise_case(case):
+    import make_golden_img as mi
+    from genpose2_amd import synthetic
+    B, N = case["B"], case["N"]
+    pts, _ = synthetic.make_batch(case["cid"], B, N)
+    xs, ys = mi.roi_pixels(B, N, case["seed"])
+    layers = [torch.from_numpy(v).to(DEV) for v in mi.dino_layers(B, case["scale"], case["seed"])]
+    return pts, xs, ys, layers
+
+
+def test_pointwise_b16_end_to_end_and_levels_vs_reference():
+    """The larger pointwise case (golden_img_b16.npz: B=16, N=1024, K=50, T=20, R=800 rows; make_golden_img.py
+    b16): the reference's pred_func end to end against PoseNet(dino='pointwise'), injected noise -- pts_feat
+    within 1e-5 of max|ref| per object, rotation 1e-4, translation 1e-5 relative -- and the fused encoder's
+    per-level outputs (SA output, transformer output, fused input of levels 1-4) of two objects at 1e-5."""
+    import make_golden_img as mi
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("img_b16")
+    e = mi.E2E16
+    B, N, K, T = e["B"], e["N"], e["K"], e["T"]
+    pts, xs, ys, layers = _pointwise_case(e)
+    agent = PoseNet(GenPoseConfig(device=DEV, sampling_steps=T, dino="pointwise")).eval()
+    prior, z1, z2 = mi.e2e_noise(e)
+    agent.noise_feed = NoiseFeed(torch.from_numpy(prior), torch.from_numpy(z1), torch.from_numpy(z2))
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(g["e2e_pts_center"]).to(DEV),
+            "roi_xs": torch.from_numpy(xs), "roi_ys": torch.from_numpy(ys), "dino_layers": layers}
+    pose, q = agent.pred_func(data, repeat_num=K)
+    feat, p = data["pts_feat"].cpu().numpy(), pose.cpu().numpy()
+    ref = g["e2e_pred_pose"]
+    fe = np.abs(feat - g["e2e_pts_feat"]).max(1) / np.abs(g["e2e_pts_feat"]).max(1)
+    rot = np.abs(p[..., :6] - ref[..., :6]).max()
+    print(f"b16 e2e: pts_feat per-object max rel {fe.max():.2e}, rotation {rot:.2e}, translation rel "
+          f"{rel(p[..., 6:], ref[..., 6:]):.2e}")
+    assert fe.max() < 1e-5 and rot < 1e-4 and rel(p[..., 6:], ref[..., 6:]) < 1e-5
+    # per-level outputs of the recorded objects, from the same per-point image features
+    feat_img = agent.img_encoder.forward(layers)
+    rgb = agent.img_encoder.gather(feat_img, torch.from_numpy(xs), torch.from_numpy(ys))
+    out, levels = agent.encoder.forward(data["pts"], rgb, return_levels=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out, data["pts_feat"])
+    errs = {}
+    for i, b in enumerate(g["level_objs"]):
+        for lv in range(5):
+            for k in ("sa", "tf", "fused"):
+                if f"l{lv}_{k}" in g:
+                    errs[(int(b), lv, k)] = rel(levels[lv][k][int(b)].cpu().numpy().T, g[f"l{lv}_{k}"][i])
+    print("b16 per-level max rel", max(errs.values()))
+    assert max(errs.values()) < 1e-5, {k: v for k, v in errs.items() if v >= 1e-5}
+
+
+def test_pointwise_b256_batch_independence_and_properties():
+    """The pointwise pipeline at the bench's full shape (B=256, N=1024, K=50; T=20 to keep the test short):
+    the first 16 objects of the B=256 batch are the golden_img_b16 case itself, and their features equal the
+    B=16 run's bit for bit (objects are independent; no kernel's per-object arithmetic depends on the batch),
+    so the B=16 reference pin carries to the full batch; poses finite, rotations orthonormal, deterministic."""
+    import make_golden_img as mi
+    from genpose2_amd import synthetic
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    e = mi.E2E16
+    B, N, K, T = 256, e["N"], 50, 20
+    pts16, xs16, ys16, layers16 = _pointwise_case(e)
+    # objects 16..255: other clouds, pixels and layers
+    pts_r, _ = synthetic.make_batch(e["cid"] + 1000, B - 16, N)
+    rng = np.random.Generator(np.random.PCG64(e["seed"] + 77))
+    xs = np.concatenate([xs16, rng.integers(-30, 250, size=(B - 16, N))])
+    ys = np.concatenate([ys16, rng.integers(-30, 250, size=(B - 16, N))])
+    layers = [torch.cat([l16, torch.from_numpy(rng.standard_normal((B - 16, 256, 384), dtype=np.float32) * 0.3).to(DEV)])
+              for l16 in layers16]
+    pts = np.concatenate([pts16, pts_r])
+    agent = PoseNet(GenPoseConfig(device=DEV, sampling_steps=T, dino="pointwise", noise_seed=5)).eval()
+
+    def run(sl, npts, nx, ny, lay):
+        d = {"pts": torch.from_numpy(npts[sl]).to(DEV), "pts_center": torch.from_numpy(npts[sl].mean(1)).to(DEV),
+             "roi_xs": torch.from_numpy(nx[sl]), "roi_ys": torch.from_numpy(ny[sl]), "dino_layers": [v[sl] for v in lay]}
+        pose, q = agent.pred_func(d, repeat_num=K)
+        return d["pts_feat"], pose, q
+    f_all, p_all, q_all = run(slice(0, B), pts, xs, ys, layers)
+    f16, _, _ = run(slice(0, 16), pts, xs, ys, layers)
+    assert torch.equal(f_all[:16], f16)
+    assert torch.isfinite(p_all).all() and torch.isfinite(q_all).all()
+    r = p_all.reshape(-1, 9).double()
+    assert (r[:, :3].norm(dim=1) - 1).abs().max() < 1e-5 and (r[:, 3:6].norm(dim=1) - 1).abs().max() < 1e-5
+    assert (r[:, :3] * r[:, 3:6]).sum(1).abs().max() < 1e-5
+    f_again, _, _ = run(slice(0, B), pts, xs, ys, layers)
+    assert torch.equal(f_again, f_all)

@@ -76,8 +76,10 @@ def test_energy_rank_aggregate_r12800_vs_reference(arith):
     1e-5. A clustered candidate set (every object re-averaged by DBSCAN) has energies whose pose . score
     sums cancel ~100x: there the reference's own fp32 energies sit up to 9.6e-6 from its float64 run,
     so the bar is calibrated on it (max over objects within 2x the reference's own error), the order
-    may differ only at near-ties inside that error, and the aggregation is held at 1e-5 from the
-    reference's energies (the aggregation alone) and from ours where the kept set is the same."""
+    may differ only at near-ties inside that error, the kept top-20 sets must equal the reference's at every
+    (object, column) pair except where the fixture itself holds a boundary near-tie (one pair), and the
+    aggregation is held at 1e-5 from the reference's energies (the aggregation alone) and from ours on every
+    object whose kept sets are the reference's."""
     import large_noise
     from genpose2_amd import aggregate, synthetic
     g = golden("large_energy_r12800")
@@ -130,12 +132,32 @@ def test_energy_rank_aggregate_r12800_vs_reference(arith):
     got = aggregate.aggregate_pose(pose, torch.from_numpy(g["cl_energy"]).to(DEV), 0.4, 1, 0.05, 0.1667,
                                    retain_num=keep)
     _check_agg(got.cpu().numpy(), g["cl_aggregated_c1"])
-    same = [b for b in range(B) if set(np.argsort(-e_np[b, :, 0], kind="stable")[:keep]) == set(idx[b, :keep, 0])
-            and set(np.argsort(-e_np[b, :, 1], kind="stable")[:keep]) == set(idx[b, :keep, 1])]
+    # kept sets (top `keep` per object and energy column, evaluation_single.py:181-182): ours may differ from
+    # the reference's only at (object, column) pairs whose float64 energies of the reference's rank-keep and
+    # rank-keep+1 candidates are a near-tie within the reference's own fp32 error (the fixture holds 1 such pair)
+    ties = _kept_set_boundary_ties(idx, g["cl_energy64"], keep, 2 * own)
+    diff = [(b, j) for b in range(B) for j in range(2)
+            if set(np.argsort(-e_np[b, :, j], kind="stable")[:keep]) != set(idx[b, :keep, j])]
+    print(arith, f"clustered: kept sets differing from the reference at {len(diff)} of {2 * B} (object, column) "
+          f"pairs {diff}; boundary near-ties in the reference fixture: {sorted(ties)}")
+    assert set(diff) <= ties, sorted(set(diff) - ties)
+    same = sorted({b for b in range(B)} - {b for b, _ in diff})
     got = aggregate.aggregate_pose(pose, e, 0.4, 1, 0.05, 0.1667, retain_num=keep).cpu().numpy()
-    print(arith, "clustered: objects with the reference's kept set", len(same), "of", B)
-    assert len(same) >= B - 8
     _check_agg(got[same], g["cl_aggregated_c1"][same])
+
+
+def _kept_set_boundary_ties(idx_ref, e64, keep, tol):
+    """(object, column) pairs whose reference order places candidates at ranks keep-1 and keep (0-based) with
+    float64 energies within tol[b] x the object's max |energy| (tol: per object, twice the reference fp32's own
+    error there): the kept set may flip there under fp32 rounding."""
+    out = set()
+    for b in range(idx_ref.shape[0]):
+        scale = np.abs(e64[b]).max()
+        for j in range(2):
+            a, c = idx_ref[b, keep - 1, j], idx_ref[b, keep, j]
+            if abs(e64[b, a, j] - e64[b, c, j]) <= tol[b] * scale:
+                out.add((b, j))
+    return out
 
 
 @pytest.mark.parametrize("arith", ARITHS)

@@ -161,6 +161,9 @@ def test_encoder_shared_geometry_bit_exact(N, score_agent):
                     assert all(torch.equal(x, y) for x, y in zip(d0[k], d1[k])), k
         with pytest.raises(ValueError):
             energy.encoder.forward(p.clone(), geometry=data["enc_geometry"])   # other points
+        score_agent.encoder.forward(p[:5].contiguous())                        # the producer re-encodes
+        with pytest.raises(ValueError, match="stale"):
+            energy.encoder.forward(p, geometry=data["enc_geometry"])
     for a in (score_agent, energy):
         a.encoder.set_arith("split_f16")
 
