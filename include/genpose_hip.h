@@ -30,7 +30,7 @@ enum { GP_OK = 0, GP_ERR_INVALID = -1, GP_ERR_LAUNCH = -2, GP_ERR_UNSUPPORTED = 
 const char *gp_last_error(void);
 /* ABI version of this header. */
 int gp_abi_version(void);
-#define GP_ABI_VERSION 6
+#define GP_ABI_VERSION 7
 
 /* ===================================================================== operator level
  * Drop-in forward ops of `pointnet2_cuda` (same argument meaning and layouts). */
@@ -185,11 +185,12 @@ typedef struct {
     const float *te_w_t;  /* t_encoder.1.weight transposed (128,128) */
     const float *te_b;    /* (128) */
     const float *h1t_t;   /* head layer 1, t columns, transposed (128, 768) */
-    /* Split-f16 form of pe2_w / h1p_w for the PC sampler (pack.py pack_h16_fragments): f16 hi/lo
-     * planes of W * 2^e. hsc = {A0, B0, A2, B2, e_pe2, e_h1p, 0, 0}: max row L1 norm and max |bias|
-     * of pose_encoder.0 / .2 (activation bounds) and the two weight exponents. Used by every
-     * per-candidate head kernel (PC step, score/energy eval, ODE stages). All three NULL: those
-     * GEMMs run in exact fp32 instead. */
+    /* f16x3 form of pe2_w / h1p_w (pack.py pack_h16_fragments(w, e, 3), ABI 7): three f16 planes
+     * hi, mid, lo of W * 2^e (6 bytes per weight). hsc = {A0, B0, A2, B2, e_pe2, e_h1p, 0, 0}: max row
+     * L1 norm and max |bias| of pose_encoder.0 / .2 (activation bounds) and the two weight exponents.
+     * Used by every per-candidate head kernel (PC step, score/energy eval, ODE stages): six f16 MFMA
+     * products per 32-deep chunk over three planes of each operand, fp32 accumulation. All three NULL:
+     * those GEMMs run in exact fp32 MFMA instead. */
     const void *pe2_h;
     const void *h1p_h;
     const float *hsc;
@@ -224,7 +225,7 @@ int gp_energy_eval(const gp_head_weights *w, const float *pobj, const float *tpr
  * (posenet_agent.py:554-556), xs (R,T,9) trajectory or NULL. */
 size_t gp_pc_workspace_size(int rows);
 /* Candidates per PC-step workgroup gp_pc_sample uses for `rows` (split != 0: head weights carry the
- * split-f16 planes). For accounting only (the per-workgroup weight stream). */
+ * f16x3 planes). For accounting only (the per-workgroup weight stream). */
 int gp_pc_tile_rows(int rows, int split);
 int gp_pc_sample(const gp_head_weights *w, const float *pobj, const float *tproj,
                  const float *step_tab, int steps, float *x, int rows, int k,

@@ -8,6 +8,8 @@
 #   bench[:ARGS]     python bench.py ARGS (comma-separated, e.g. bench:--config,5,--steps,2)
 #   prof[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS (--steps 3 --warmup 1 by default)
 #   bin:PROGRAM[:ARGS] a built program (e.g. scripts/mfma_round_probe)
+#   env:NAME=VALUE   export NAME=VALUE for the steps after it (env:NAME= unsets it)
+#   ab:MODE,ROUNDS,LIB1,LIB2,...  scripts/ab.sh (same-box A/B of library variants)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS
 #   kprof:SCRIPT[:ARGS] rocprofv3 --kernel-trace --stats of python3 SCRIPT ARGS
 #   pmc[:ARGS]       scripts/pmc_passes.sh over scripts/pmc_target.py ARGS
@@ -35,6 +37,12 @@ for step in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o k -- python3 bench.py "${A[@]}" > $out.log 2>&1 ;;
     bin)
       s=${A[0]}; timeout -k 10 120 $s "${A[@]:1}" > $out.out 2> $out.err ;;
+    env)
+      k=${arg%%=*}; v=${arg#*=}
+      if [ -n "$v" ]; then export "$k=$v"; else unset "$k"; fi
+      true ;;
+    ab)
+      timeout -k 10 900 bash scripts/ab.sh "${A[@]}" > $out.log 2>&1 ;;
     py)
       s=${A[0]}; timeout -k 10 600 python -u $s "${A[@]:1}" > $out.out 2> $out.err ;;
     kprof)

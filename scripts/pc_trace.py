@@ -41,7 +41,7 @@ def main():
     torch.cuda.synchronize()
     buf = np.zeros(2 * 256 * 8 * 16, np.uint64)
     assert fn(buf.ctypes.data) == 0
-    tile = int(lib.gp_pc_tile_rows(B * K, int(agent.heads.arith == "split_f16")))
+    tile = int(lib.gp_pc_tile_rows(B * K, int(agent.heads.arith == "f16x3")))
     nwg = min((B * K + tile - 1) // tile, 256)
     tr = buf.reshape(2, 256, 8, 16)[(T - 1) & 1, :nwg, :, :9].astype(np.int64)
     t0 = tr[:, :, 0].min()

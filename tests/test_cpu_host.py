@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     from genpose2_amd import _lib
     assert set(_lib.EXPORTED) == declared   # the ctypes binding covers exactly the header
     lib = _lib.load()
-    assert lib.gp_abi_version() == 6
+    assert lib.gp_abi_version() == 7
     assert lib.gp_encoder_workspace_size(64, 1024) > 0 and lib.gp_pc_workspace_size(3200) >= 3200 * 36
 
 
