@@ -389,13 +389,15 @@ def test_ode_pred_func_vs_golden(tag, rot_tol, tr_rel):
         x = xs.cpu().numpy()
         # t_eval unset (T0=1): xs are the states at solve_ivp's own accepted step times, which move with the
         # last bits of every error norm even at equal nfev, so the intermediate states are compared to the
-        # reference's at slightly different t (measured 1.1e-3 with the f16x3 head GEMMs, 3.6e-4 with the
-        # round-3 split-f16 ones); the final state is held to the golden bar
-        mid_tol = rot_tol if tag == "t055_s20" else 3e-3
+        # reference's at slightly different t (measured 1.1e-3 rotation / 3.1e-4 relative translation with the
+        # f16x3 head GEMMs, 3.6e-4 rotation with the round-3 split-f16 ones); the final state is held to the
+        # golden bar
+        mid_tol, mid_rel = (rot_tol, tr_rel) if tag == "t055_s20" else (3e-3, 1e-3)
         err = np.abs(x[..., :6] - xr[..., :6])
-        print(f"{tag}: xs rotation max {err.max():.2e} (final state {err[..., -1, :].max():.2e})")
+        print(f"{tag}: xs rotation max {err.max():.2e} (final state {err[..., -1, :].max():.2e}), translation rel "
+              f"{rel(x[..., 6:], xr[..., 6:]):.2e} (final state {rel(x[..., -1, 6:], xr[..., -1, 6:]):.2e})")
         assert err.max() < mid_tol and err[..., -1, :].max() < rot_tol
-        assert rel(x[..., 6:], xr[..., 6:]) < tr_rel
+        assert rel(x[..., 6:], xr[..., 6:]) < mid_rel and rel(x[..., -1, 6:], xr[..., -1, 6:]) < tr_rel
 
 
 @pytest.mark.parametrize("tag", ["t055_s20", "t1_none"])
