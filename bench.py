@@ -249,7 +249,8 @@ def rocprof_files(config, dino="none"):
 
 
 def load_rocprof(kernel, config, dino="none"):
-    """Mean duration of `kernel` (its full instantiation name, e.g. "void pc_step_kernel<4, 8, true>(...") in the
+    """Mean duration of `kernel` (its full instantiation name, e.g. "void pc_step_kernel<4, 8, 3>(...": 64-candidate
+    tiles, 8 waves, f16x3 -- the plane count keeps it apart from the round-3 2-plane "<4, 8, true>") in the
     newest committed rocprofv3 --stats summary of a bench run of the same config (so the same row count and
     tile) that holds it, or None."""
     import csv
@@ -266,7 +267,12 @@ def load_traffic(rows, split, tile):
     """HBM(+Infinity Cache) bytes per pc_step launch from the newest committed PMC pass of the same
     kernel instantiation (tile width, arithmetic) and row count (profiles/**/pmc_pc_step*.json,
     scripts/pmc_passes.sh), or None."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "**", "pmc_pc_step*.json"), recursive=True))
+    import re
+
+    def key(fn):   # newest round first, then reverse lexical order (deterministic, no mtimes)
+        m = re.search(r"profiles/r(\d+)/", fn.replace(os.sep, "/"))
+        return (int(m.group(1)) if m else -1, fn)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "**", "pmc_pc_step*.json"), recursive=True), key=key)
     for fn in reversed(files):
         try:
             with open(fn) as f:
@@ -274,7 +280,7 @@ def load_traffic(rows, split, tile):
         except (OSError, ValueError):
             continue
         k = d.get("kernel", "")
-        if d.get("rows") == rows and (", true>" in k) == bool(split) and k.startswith(f"void pc_step_kernel<{tile // 16},"):
+        if d.get("rows") == rows and k.startswith(f"void pc_step_kernel<{tile // 16}, 8, {3 if split else 0}>"):
             return d.get("hbm_bytes_per_launch")
     return None
 
@@ -568,7 +574,7 @@ def main():
                 a.encoder.set_arith("split_f16")
         us32 = ms32 / 1e3 / (T + 1) * 1e6
         fl = B * K * arch.score_flops_per_candidate_step()
-        k32 = f"void pc_step_kernel<{int(_tile_rows(B * K, False)) // 16}, 8, false>"
+        k32 = f"void pc_step_kernel<{int(_tile_rows(B * K, False)) // 16}, 8, 0>"
         f32_info = {"value": B * K * T * ws * args.f32_steps / el32, "unit": "pose-candidate-steps/s",
                     "steps": args.f32_steps, "ms_per_step": el32 / args.f32_steps * 1e3,
                     "dtype": "f32 (every GEMM exact fp32 MFMA, v_mfma_f32_16x16x4_f32)",
@@ -629,7 +635,7 @@ def main():
                                               "GBps_per_CU": wg_bytes / per_launch_s / 1e9,
                                               "TBps_chip": wg_bytes * nwg / per_launch_s / 1e12}},
         }
-        rp = load_rocprof(f"void pc_step_kernel<{tile // 16}, 8, {'true' if fast else 'false'}>", args.config, args.dino)
+        rp = load_rocprof(f"void pc_step_kernel<{tile // 16}, 8, {3 if fast else 0}>", args.config, args.dino)
         if rp is not None:   # the committed rocprofv3 --stats of a bench run: its mean launch, same FLOPs
             rp["achieved"] = flop_launch / (rp["avg_launch_us"] * 1e-6) / 1e12
             rp["frac"] = rp["achieved"] / peak

@@ -691,7 +691,9 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
 #pragma unroll
     for (int v = 9 * NT; v < SM::kRedV; ++v) pv[v] = 0.f;
     head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    PC_MARK(13);
     head_x3_head<1, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    PC_MARK(14);
     head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
     PC_MARK(5);
     if constexpr ((3 * NT) % 4 != 0) {

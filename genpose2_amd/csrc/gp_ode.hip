@@ -65,11 +65,12 @@ struct OdeStageArgs {
 // MODE 0: stage derivative. MODE 1: last stage of an attempt (y_new, K_6, error partials).
 // NT column tiles of 16 candidates per workgroup (head_pick_nt: 32 / 64 candidates from 4097 / 8193 rows
 // with the split-f16 trunk, as the PC step).
-template <int MODE, bool SPLIT, int NT>
+template <int MODE, int PL, int NT>   // PL 0: exact fp32 GEMMs, X3P: f16x3
 __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a) {
     constexpr int ROWS = 16 * NT;
     constexpr int NTH = EVAL_WV * 64;
-    __shared__ HeadSmem<NT, EVAL_WV, SPLIT ? X3P : 0> sm;
+    __shared__ HeadSmem<NT, EVAL_WV, PL> sm;
+    constexpr bool SPLIT = PL != 0;
     __shared__ int obj[ROWS];
     __shared__ double y0s[ROWS * 9], y1s[ROWS * 9], esq[NTH];
     const int tid = threadIdx.x;
@@ -172,13 +173,13 @@ static void ode_launch_stage(const OdeStageArgs& a, int nt, hipStream_t st) {
     const int nwg = (a.rows + 16 * nt - 1) / (16 * nt);
     const dim3 grid(nwg), blk(EVAL_WV * 64);
     if (!a.w.pe2_h)
-        hipLaunchKernelGGL((ode_stage_kernel<MODE, false, 1>), grid, blk, 0, st, a);
+        hipLaunchKernelGGL((ode_stage_kernel<MODE, 0, 1>), grid, blk, 0, st, a);
     else if (nt == 4)
-        hipLaunchKernelGGL((ode_stage_kernel<MODE, true, 4>), grid, blk, 0, st, a);
+        hipLaunchKernelGGL((ode_stage_kernel<MODE, X3P, 4>), grid, blk, 0, st, a);
     else if (nt == 2)
-        hipLaunchKernelGGL((ode_stage_kernel<MODE, true, 2>), grid, blk, 0, st, a);
+        hipLaunchKernelGGL((ode_stage_kernel<MODE, X3P, 2>), grid, blk, 0, st, a);
     else
-        hipLaunchKernelGGL((ode_stage_kernel<MODE, true, 1>), grid, blk, 0, st, a);
+        hipLaunchKernelGGL((ode_stage_kernel<MODE, X3P, 1>), grid, blk, 0, st, a);
 }
 
 static int ode_nt(const gp_head_weights* w, int rows) { return head_pick_nt(rows, w->pe2_h != nullptr); }

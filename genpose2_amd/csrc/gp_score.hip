@@ -76,12 +76,13 @@ extern "C" int gp_head_time_proj(const gp_head_weights* w, const float* t, int n
 }
 
 // ============================================================================ score / energy eval
-template <int MODE, bool SPLIT>  // MODE 0: score f/(sigma+1e-7), 1: energy (IP, decoupled)
+template <int MODE, int PL>  // MODE 0: score f/(sigma+1e-7), 1: energy (IP, decoupled); PL 0: exact fp32, X3P: f16x3
 __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights w, const float* __restrict__ pobj,
                                                        const float* __restrict__ tproj, float sigma,
                                                        const float* __restrict__ x, int rows, int kper,
                                                        float* __restrict__ out) {
-    __shared__ HeadSmem<1, EVAL_WV, SPLIT ? X3P : 0> sm;
+    __shared__ HeadSmem<1, EVAL_WV, PL> sm;
+    constexpr bool SPLIT = PL != 0;
     __shared__ int obj[16];
     const int r0 = blockIdx.x * 16;
     SplitScalars hs = {};
@@ -123,10 +124,10 @@ extern "C" int gp_score_eval(const gp_head_weights* w, const float* pobj, const 
     GP_REQUIRE(w && pobj && tproj_row && x && score && rows >= 0 && k >= 1, "score_eval: bad arguments");
     if (!rows) return GP_OK;
     if (w->pe2_h)
-        hipLaunchKernelGGL((head_eval_kernel<0, true>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
+        hipLaunchKernelGGL((head_eval_kernel<0, X3P>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
                        sigma, x, rows, k, score);
     else
-        hipLaunchKernelGGL((head_eval_kernel<0, false>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
+        hipLaunchKernelGGL((head_eval_kernel<0, 0>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
                        sigma, x, rows, k, score);
     return gp_check_launch("head_eval_kernel<score>");
 }
@@ -136,10 +137,10 @@ extern "C" int gp_energy_eval(const gp_head_weights* w, const float* pobj, const
     GP_REQUIRE(w && pobj && tproj_row && pose && energy && rows >= 0 && k >= 1, "energy_eval: bad arguments");
     if (!rows) return GP_OK;
     if (w->pe2_h)
-        hipLaunchKernelGGL((head_eval_kernel<1, true>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
+        hipLaunchKernelGGL((head_eval_kernel<1, X3P>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
                        sigma, pose, rows, k, energy);
     else
-        hipLaunchKernelGGL((head_eval_kernel<1, false>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
+        hipLaunchKernelGGL((head_eval_kernel<1, 0>), dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, *w, pobj, tproj_row,
                        sigma, pose, rows, k, energy);
     return gp_check_launch("head_eval_kernel<energy>");
 }
@@ -174,11 +175,12 @@ struct PCArgs {
 // Waves 0..NT-1 run the update, one 16-row column tile each (their global loads, the draws and the
 // grad-norm reduction overlap), while the other waves make the next step's draws, stage the small
 // weights and issue their first weight-stream loads; one barrier (inside the trunk) joins them.
-template <int NT, int WV, bool SPLIT>
+template <int NT, int WV, int PL>   // PL 0: exact fp32 GEMMs, X3P: f16x3
 __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
     constexpr int ROWS = NT * 16;
     static_assert(NT < WV, "at least one wave besides the update waves");
-    __shared__ HeadSmem<NT, WV, SPLIT ? X3P : 0> sm;
+    __shared__ HeadSmem<NT, WV, PL> sm;
+    constexpr bool SPLIT = PL != 0;
     __shared__ int obj[ROWS];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -481,15 +483,15 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
         if (i > 0) prev = PCStep{step_tab[5 * (i - 1)], step_tab[5 * (i - 1) + 1], step_tab[5 * (i - 1) + 2],
                                  step_tab[5 * (i - 1) + 3], step_tab[5 * (i - 1) + 4]};
         if (nt == 4)
-            hipLaunchKernelGGL((pc_step_kernel<4, PC_WV1, true>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+            hipLaunchKernelGGL((pc_step_kernel<4, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else if (nt == 2 && split)
-            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV1, true>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else if (nt == 2)
-            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV2, false>), grid, dim3(PC_WV2 * 64), 0, stream, a, i, cur, prev);
+            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV2, 0>), grid, dim3(PC_WV2 * 64), 0, stream, a, i, cur, prev);
         else if (split)
-            hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, true>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+            hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else
-            hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, false>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+            hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, 0>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
     }
     return gp_check_launch("pc_step_kernel");
 }

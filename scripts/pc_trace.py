@@ -71,10 +71,17 @@ def main():
     out["gap_per_xcd"] = [float(tr[x::8, :, 0].min() - prev[x::8, :, 8].max()) for x in range(8)]
     out["launch_span_cycles"] = float(tr[:, :, 8].max() - tr[:, :, 0].min())
     full = buf.reshape(2, 256, 8, 16)[(T - 1) & 1, :nwg, :, :].astype(np.int64)
-    for nm, (a, b) in {"pe0: exponents": (1, 13), "pe0: init loads issued": (13, 14), "pe0: compute+lds": (14, 15),
-                       "pe0: barrier": (15, 2)}.items():
+    # head layer 1 head by head (marks 4 -> 13 -> 14 -> 5): per wave index (mean over workgroups) and the
+    # spread between a workgroup's fastest and slowest wave
+    for nm, (a, b) in {"head0": (4, 13), "head1": (13, 14), "head2": (14, 5)}.items():
         if full[..., b].any():
-            out.setdefault("pe0_sub_cycles_mean", {})[nm] = float((full[..., b] - full[..., a]).mean())
+            dd = full[..., b] - full[..., a]                  # (wg, wave)
+            out.setdefault("h1_heads_per_wave_mean", {})[nm] = [round(float(v)) for v in dd.mean(0)]
+            out.setdefault("h1_heads_spread_mean", {})[nm] = float((dd.max(1) - dd.min(1)).mean())
+    h1 = full[..., 5] - full[..., 4]
+    out["h1_per_wave_mean"] = [round(float(v)) for v in h1.mean(0)]
+    out["h1_end_spread_mean"] = float((full[..., 5].max(1) - full[..., 5].min(1)).mean())
+    out["h1_start_spread_mean"] = float((full[..., 4].max(1) - full[..., 4].min(1)).mean())
     print(json.dumps(out, indent=1))
 
 

@@ -503,7 +503,7 @@ def test_bench_rocprof_source_matches_config(tmp_path, monkeypatch):
     def csv(path, kernel, avg):
         path.parent.mkdir(parents=True, exist_ok=True)
         path.write_text(hdr + f'"{kernel}(PCArgs, int, PCStep, PCStep)",501,1,{avg},50,1,1,0\n')
-    k4, k1 = "void pc_step_kernel<4, 8, true>", "void pc_step_kernel<1, 8, false>"
+    k4, k1 = "void pc_step_kernel<4, 8, 3>", "void pc_step_kernel<1, 8, 0>"
     csv(tmp_path / "profiles" / "r3" / "config4_r3f_kernel_stats.csv", k4, 23890)
     csv(tmp_path / "profiles" / "r4" / "config4_a_kernel_stats.csv", k4, 30000)
     csv(tmp_path / "profiles" / "r4" / "config4_b_kernel_stats.csv", k4, 31000)
