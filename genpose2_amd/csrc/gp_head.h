@@ -447,6 +447,9 @@ __device__ __forceinline__ float xin_row_absmax(f32x4 b) {
 #ifndef X3_DH
 #define X3_DH 2                  // 32-deep chunks of head-layer-1 weights kept in flight
 #endif
+#ifndef X3_HEAD_BARRIER
+#define X3_HEAD_BARRIER 0        // 1: a workgroup barrier after each head of head layer 1 (tuning)
+#endif
 constexpr int X3P = 3;           // planes per operand
 
 // x = h + m + l exactly (x finite, |x| < 65504; f16 subnormals aside)
@@ -691,8 +694,10 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
 #pragma unroll
     for (int v = 9 * NT; v < SM::kRedV; ++v) pv[v] = 0.f;
     head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    if constexpr (X3_HEAD_BARRIER) __syncthreads();
     PC_MARK(13);
     head_x3_head<1, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    if constexpr (X3_HEAD_BARRIER) __syncthreads();
     PC_MARK(14);
     head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
     PC_MARK(5);

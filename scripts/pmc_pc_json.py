@@ -29,7 +29,7 @@ out = {"kernel": name, "rows": rows,
        "fetch_size_kb": m.get("FETCH_SIZE"), "write_size_kb": m.get("WRITE_SIZE"),
        "hbm_bytes_per_launch": (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024,
        "algorithmic_bytes_per_launch": rows * 72,
-       "note": "fabric reads are dominated by each XCD's L2 re-fetching the ~1 MB of streamed head weights once "
+       "note": "fabric reads are dominated by each XCD's L2 re-fetching the streamed head weights (1.57 MB of f16x3 planes) once "
                "per launch (the kernel boundary invalidates L2); served from the 256 MB Infinity Cache"}
 if "TCC_HIT_sum" in m:
     out["tcc_hit_rate"] = m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
