@@ -447,6 +447,12 @@ __device__ __forceinline__ float xin_row_absmax(f32x4 b) {
 #ifndef X3_DH
 #define X3_DH 2                  // 32-deep chunks of head-layer-1 weights kept in flight
 #endif
+#ifndef X3_PRIO
+#define X3_PRIO 0                // 1: alternate the issue priority of a SIMD's two waves per chunk (tuning)
+#endif
+#ifndef X3_BPRE
+#define X3_BPRE 0                // 1: a chunk's B planes of every column tile loaded before its MFMAs (tuning)
+#endif
 #ifndef X3_HEAD_BARRIER
 #define X3_HEAD_BARRIER 0        // 1: a workgroup barrier after each head of head layer 1 (tuning)
 #endif
@@ -496,11 +502,30 @@ __device__ __forceinline__ void stream_x3_step(__amdgpu_buffer_rsrc_t W, const i
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (G >= D) {
             constexpr int GG = G - D, S = GG % (D + 1);
+#if X3_PRIO
+            // the two waves of a SIMD (w, w + 4) take turns at issue priority chunk by chunk, so neither runs
+            // a whole stream ahead and leaves the other to finish it alone (tuning variant)
+            if ((__builtin_amdgcn_readfirstlane(threadIdx.x >> 8) ^ GG) & 1)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+#endif
+#if X3_BPRE
+            f16x8 bp[NT][X3P];   // every column tile's planes of this chunk up front (tuning variant)
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+                for (int p = 0; p < X3P; ++p) bp[ct][p] = B[((GG * NT + ct) * X3P + p) * 64 + lane];
+#endif
 #pragma unroll
             for (int ct = 0; ct < NT; ++ct) {
+#if X3_BPRE
+                const f16x8 b0 = bp[ct][0], b1 = bp[ct][1], b2 = bp[ct][2];
+#else
                 const f16x8 b0 = B[((GG * NT + ct) * X3P + 0) * 64 + lane];
                 const f16x8 b1 = B[((GG * NT + ct) * X3P + 1) * 64 + lane];
                 const f16x8 b2 = B[((GG * NT + ct) * X3P + 2) * 64 + lane];
+#endif
 #pragma unroll
                 for (int t = 0; t < TT; ++t) {
                     f32x4 c = cor[t][ct];
@@ -518,47 +543,63 @@ __device__ __forceinline__ void stream_x3_step(__amdgpu_buffer_rsrc_t W, const i
     }
 }
 
+// The fp32 init rows of head layer 1 (hoisted pts + t blocks: pobj of each column's object, tproj) for this
+// wave's output tiles of head H: loads issued where their latency hides (under the previous head's epilogue,
+// or the pose_encoder.2 epilogue for head 0) and folded into the accumulator at the head's start, so they are
+// not live across the MFMA stream.
+template <int H, int NT, int TPW>
+__device__ __forceinline__ void head_x3_init_load(__amdgpu_buffer_rsrc_t RP, __amdgpu_buffer_rsrc_t RT, const int (&vo)[NT],
+                                                  int wid, int lane, f32x4 (&tpv)[TPW], f32x4 (&pov)[TPW][NT]) {
+    const int q = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int T = H * 16 + wid * TPW + t;
+        tpv[t] = ldbuf4(RT, 16 * q, 64 * T);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) pov[t][ct] = ldbuf4(RP, vo[ct], 64 * T);
+    }
+}
+
 // head_trunk with the f16x3 GEMMs (same contract: head_out reads the outputs after it returns).
-// Head layer 1 runs one head at a time (2 output tiles per wave and head), each head's fp32 init rows
-// (hoisted pts + t blocks) loaded while its weights stream and added once with its two accumulators;
-// the next head's first weight chunks are in flight during this head's layer-2 partials.
+// Head layer 1 runs one head at a time (2 output tiles per wave and head): the head's fp32 init rows
+// enter its main accumulator in the scaled domain (x sh, a power of two: exact), hi*hi accumulates on top
+// and the cross products beside it; the next head's first weight chunks and init rows are in flight during
+// this head's layer-2 partials.
 // PRE: the caller wrote every column's ColScales to sm.cscl before the trunk's first barrier (the PC
 // step's update waves, which hold the rows), so the trunk reads them instead of recomputing them in
 // every wave.
 template <int H, int NT, int WV, int TPW, int DH>
 __device__ __forceinline__ void head_x3_head(__amdgpu_buffer_rsrc_t WH, const f16x8* __restrict__ act2h,
                                              __amdgpu_buffer_rsrc_t RP, __amdgpu_buffer_rsrc_t RT, const int (&vo)[NT],
-                                             HeadSmem<NT, WV, X3P>& sm, const float (&uh)[NT], int wid, int lane,
-                                             f16x8 (&ringh)[DH + 1][TPW][X3P], float (&pv)[HeadSmem<NT, WV, X3P>::kRedV]) {
+                                             HeadSmem<NT, WV, X3P>& sm, const float (&uh)[NT], const float (&sh)[NT],
+                                             int wid, int lane, f16x8 (&ringh)[DH + 1][TPW][X3P],
+                                             f32x4 (&tpv)[TPW], f32x4 (&pov)[TPW][NT],
+                                             float (&pv)[HeadSmem<NT, WV, X3P>::kRedV]) {
     const int q = lane >> 4, n = lane & 15;
     const int voff = lane * 16;
     int TH[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) TH[t] = H * 16 + wid * TPW + t;
-    // the init rows: first touch of pobj / tproj after the kernel boundary, consumed after the stream
-    f32x4 tpv[TPW], pov[TPW][NT];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        tpv[t] = ldbuf4(RT, 16 * q, 64 * TH[t]);
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) pov[t][ct] = ldbuf4(RP, vo[ct], 64 * TH[t]);
-    }
     f32x4 acc[TPW][NT], cor[TPW][NT];
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) acc[t][ct] = cor[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int ct = 0; ct < NT; ++ct) {
+            acc[t][ct] = (pov[t][ct] + tpv[t]) * sh[ct];
+            cor[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
     stream_x3_step<DH, KC_HID + DH, TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc, cor);
-    if constexpr (H < 2) {   // the next head's first chunks, in flight across this head's epilogue
+    if constexpr (H < 2) {   // the next head's first chunks and init rows, in flight across this epilogue
         int TN[TPW];
 #pragma unroll
         for (int t = 0; t < TPW; ++t) TN[t] = TH[t] + 16;
         stream_x3_step<0, DH, TPW, NT, DH>(WH, TN, act2h, lane, voff, ringh, acc, cor);
+        head_x3_init_load<H + 1, NT, TPW>(RP, RT, vo, wid, lane, tpv, pov);
     }
     // nothing below is scheduled into the MFMA stream above: interleaved there, the row swaps of the
     // reduce-scatter reused registers in-flight MFMAs still read (v_permlane*_swap writes both operands)
     __builtin_amdgcn_sched_barrier(0);
-    // u = ReLU(scale-undone GEMM + init) -> head layer 2 (3 outputs) partials: one fp32 FMA chain per
+    // u = ReLU(scale-undone accumulators) -> head layer 2 (3 outputs) partials: one fp32 FMA chain per
     // (column, output) over this wave's channels, t-major then j
     float p[NT][3];
 #pragma unroll
@@ -571,7 +612,7 @@ __device__ __forceinline__ void head_x3_head(__amdgpu_buffer_rsrc_t WH, const f1
         const f32x4 w2 = ld4(&sm.h2w[(H * 3 + 2) * HID + ch]);
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-            const f32x4 u = relu4((acc[t][ct] + cor[t][ct]) * uh[ct] + (pov[t][ct] + tpv[t]));
+            const f32x4 u = relu4((acc[t][ct] + cor[t][ct]) * uh[ct]);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 p[ct][0] = __builtin_fmaf(u[j], w0[j], p[ct][0]);
@@ -625,14 +666,14 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
     PC_MARK(1);
     // ---- per-candidate exponents: bound1 >= |pose_encoder.0 out|, bound2 >= |pose_encoder.2 out|
     f32x4 bf[NT];
-    float s1[NT], s2[NT], u2[NT], uh[NT];
+    float s1[NT], s2[NT], u2[NT], uh[NT], sh[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) {
         bf[ct] = ld4(&sm.xin[(ct * 16 + n) * 16 + 4 * q]);
         ColScales cs;
         if constexpr (PRE) {
             const f32x4 a = sm.cscl[ct * 16 + n][0];
-            cs = ColScales{a.x, a.y, a.z, a.w, 0.f};
+            cs = ColScales{a.x, a.y, a.z, a.w, sm.cscl[ct * 16 + n][1].x};
         } else {
             cs = split_col_scales(xin_row_absmax(bf[ct]), hs);
         }
@@ -640,6 +681,7 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
         s2[ct] = cs.s2;
         u2[ct] = cs.u2;
         uh[ct] = cs.uh;
+        sh[ct] = cs.sh;
     }
     // ---- pose_encoder.0 (9 -> 256) in fp32, one k-group; ReLU, scale, split into the chunk planes
 #pragma unroll
@@ -661,7 +703,7 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
     // ---- pose_encoder.2 (256 -> 256)
     stream_x3_step<D2, KC_HID + D2, TPW, NT, D2>(W2, T2, act1h, lane, voff, ring2, acc2, cor2);
     PC_MARK(3);
-    // head layer 1's first chunks (head 0), in flight across the pose_encoder.2 epilogue
+    // head layer 1's first chunks and init rows (head 0), in flight across the pose_encoder.2 epilogue
     f16x8 ringh[DH + 1][TPW][X3P];
     {
         int TH0[TPW];
@@ -669,6 +711,12 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
         for (int t = 0; t < TPW; ++t) TH0[t] = wid * TPW + t;
         stream_x3_step<0, DH, TPW, NT, DH>(WH, TH0, act2h, lane, voff, ringh, acc2, cor2);
     }
+    const __amdgpu_buffer_rsrc_t RP = make_rsrc(pobj, 0x7ffffff0u), RT = make_rsrc(tproj, 3 * HID * 4);
+    int vo[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) vo[ct] = obj_of_col[ct * 16 + n] * (3 * HID * 4) + 16 * q;
+    f32x4 tpv[TPW], pov[TPW][NT];
+    head_x3_init_load<0, NT, TPW>(RP, RT, vo, wid, lane, tpv, pov);
     if constexpr (SM::kAliasAct) __syncthreads();   // act2 overwrites act1: all reads done
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
@@ -686,20 +734,17 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
     __syncthreads();
     PC_MARK(4);
     // ---- head layer 1 (pose block 256 -> 3x256) head by head, each followed by its layer-2 partials
-    const __amdgpu_buffer_rsrc_t RP = make_rsrc(pobj, 0x7ffffff0u), RT = make_rsrc(tproj, 3 * HID * 4);
-    int vo[NT];
-#pragma unroll
-    for (int ct = 0; ct < NT; ++ct) vo[ct] = obj_of_col[ct * 16 + n] * (3 * HID * 4) + 16 * q;
     float pv[SM::kRedV];
 #pragma unroll
     for (int v = 9 * NT; v < SM::kRedV; ++v) pv[v] = 0.f;
-    head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
     if constexpr (X3_HEAD_BARRIER) __syncthreads();
     PC_MARK(13);
-    head_x3_head<1, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    head_x3_head<1, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
     if constexpr (X3_HEAD_BARRIER) __syncthreads();
     PC_MARK(14);
-    head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, wid, lane, ringh, pv);
+    head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
+    if constexpr (X3_PRIO) __builtin_amdgcn_s_setprio(0);
     PC_MARK(5);
     if constexpr ((3 * NT) % 4 != 0) {
 #pragma unroll
