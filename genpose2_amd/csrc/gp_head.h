@@ -445,7 +445,7 @@ __device__ __forceinline__ float xin_row_absmax(f32x4 b) {
 #define X3_D2 2                  // 32-deep chunks of pose_encoder.2 weights kept in flight
 #endif
 #ifndef X3_DH
-#define X3_DH 2                  // 32-deep chunks of head-layer-1 weights kept in flight
+#define X3_DH 1                  // 32-deep chunks of head-layer-1 weights kept in flight (2: ab_prio_dh1.json)
 #endif
 #ifndef X3_PRIO
 #define X3_PRIO 0                // 1: alternate the issue priority of a SIMD's two waves per chunk (tuning)
