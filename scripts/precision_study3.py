@@ -15,6 +15,11 @@ per-candidate GEMMs (pose_encoder.2, head layer 1's pose block) emulated as:
   h6x2    as h6, but hi*hi into a main accumulator and the 5 cross products into a second one,
           summed once at the end of the layer
 
+HI64 (comma list) runs parts in float64, rounded to fp32 after: pe0, h2, upd (update + state), init
+(object + time rows summed, rounded once), init1 (each rounded once, summed in fp32), init1e (as init1
+with the Fourier time embedding in fp32 as the reference computes it), init2 (hi/lo pairs of both rows,
+the lo parts in the second accumulator; TWOSUM=1 adds the two-sum error of the hi parts).
+
 Each f16 MFMA is modelled as its 32 exact products summed exactly and added to the accumulator with
 one rounding. Prints the rotation error (max, p99.9, mean) against the float64 run.
 Usage: python scripts/precision_study3.py [variant ...]
@@ -53,8 +58,10 @@ def planes(x, n):
     return out
 
 
-def gemm(x, w, mode):
-    """x (R,K) fp32, w (N,K) fp32 -> (R,N) fp32 under `mode`."""
+def gemm(x, w, mode, init=None):
+    """x (R,K) fp32, w (N,K) fp32 -> (R,N) fp32 under `mode`. init: None, or the head-layer-1 init rows as
+    (ph, pl, th, tl) fp32 hi/lo pairs of the object and time rows, entering the accumulators as the
+    kernel does (main: fp32(ph + th), second: pl + tl [+ the two-sum error of ph + th if TWOSUM])."""
     if mode == "torch":
         return x @ w.T
     if mode == "f64":
@@ -73,6 +80,14 @@ def gemm(x, w, mode):
     pairs = [(i, j) for i in range(n) for j in range(n) if i + j < (2 if mode == "h3" else 3)]
     pairs.sort(key=lambda p: -(p[0] + p[1]))          # smallest first
     corr = torch.zeros_like(acc)
+    if init is not None:
+        ph, pl, th, tl = (v.to(F64) for v in init)
+        ss = (ph + th).to(F32).to(F64)
+        lo = (pl + tl).to(F32).to(F64)
+        if os.environ.get("TWOSUM"):
+            lo = (lo + ((ph - ss) + th)).to(F32).to(F64)   # ph + th - ss is exact in float64
+        acc = (ss * sx * sw).to(F32).to(F64)
+        corr = (lo * sx * sw).to(F32).to(F64)
     for k0 in range(0, K, 32):
         sl = slice(k0, k0 + 32)
         for i, j in pairs:
@@ -100,6 +115,14 @@ class Model:
         self.h2b = [g(f"{h}.2.bias") for h in arch.HEAD_NAMES]
         self.W1p = torch.cat([w[:, 1024 + 128:] for w in self.h1w], 0)   # (768, 256) pose block
 
+    def time_row_e32(self, t32):
+        """The time row with the Fourier embedding in fp32 as the reference computes it (x_proj and sin/cos),
+        the two Linear layers after it in this model's dtype."""
+        x = ((t32 * self.te_W.to(F32)) * 2) * np.float32(np.pi)
+        emb = torch.cat([torch.sin(x), torch.cos(x)]).to(self.dt)
+        tf = torch.relu(emb @ self.te1w.T + self.te1b)
+        return torch.cat([tf @ w[:, 1024:1024 + 128].T for w in self.h1w])
+
     def obj_rows(self, feat):
         return torch.cat([feat @ w[:, :1024].T + b for w, b in zip(self.h1w, self.h1b)], 1)   # (B,768)
 
@@ -119,6 +142,9 @@ class Model:
         if self.dt == F64:
             pf = torch.relu(h @ self.W2.T + self.b2)
             u = torch.relu(init + pf @ self.W1p.T)
+        elif isinstance(init, tuple):
+            pf = torch.relu(gemm(h, self.W2, mode) + self.b2)
+            u = torch.relu(gemm(pf, self.W1p, mode, init))
         else:
             pf = torch.relu(gemm(h, self.W2, mode) + self.b2)
             u = torch.relu(init + gemm(pf, self.W1p, mode))
@@ -144,8 +170,10 @@ def run(sd, feat, prior, z1, z2, K, T, dt, mode):
     hi = Model(sd, F64) if HI64 and dt == F32 else None
     feat = torch.from_numpy(feat).to(dt)
     pobj = m.obj_rows(feat).repeat_interleave(K, 0)
-    if hi is not None and "init" in HI64:
+    if hi is not None and HI64 & {"init", "init1", "init1e", "init2"}:
         pobj = hi.obj_rows(feat.to(F64)).repeat_interleave(K, 0)
+        p_h = pobj.to(F32)
+        p_l = (pobj - p_h.to(F64)).to(F32)
     ts = torch.linspace(1.0, arch.SAMPLING_EPS, T, dtype=dt)
     step = ts[0] - ts[1]
     x = torch.from_numpy(prior).to(dt)
@@ -155,7 +183,15 @@ def run(sd, feat, prior, z1, z2, K, T, dt, mode):
         t = ts[k]
         sig = arch.SIGMA_MIN * (arch.SIGMA_MAX / arch.SIGMA_MIN) ** t
         g = sig * torch.tensor(arch.DIFFUSION_SCALE, dtype=dt)
-        if hi is not None and "init" in HI64:
+        if hi is not None and "init2" in HI64:
+            tr = hi.time_row(ts[k].to(F64))
+            th = tr.to(F32)
+            init = (p_h, p_l, th.expand_as(p_h), (tr - th.to(F64)).to(F32).expand_as(p_h))
+        elif hi is not None and "init1e" in HI64:   # as init1, the Fourier embedding in fp32
+            init = p_h + hi.time_row_e32(ts[k]).to(F32)
+        elif hi is not None and "init1" in HI64:   # hoisted rows each rounded once, summed in fp32
+            init = p_h + hi.time_row(ts[k].to(F64)).to(F32)
+        elif hi is not None and "init" in HI64:
             init = (pobj + hi.time_row(ts[k].to(F64))).to(F32)
         else:
             init = pobj + m.time_row(t)
