@@ -450,8 +450,9 @@ __device__ __forceinline__ float xin_row_absmax(f32x4 b) {
 #ifndef X3_PRIO
 #define X3_PRIO 0                // 1: alternate the issue priority of a SIMD's two waves per chunk (tuning)
 #endif
-#ifndef X3_BPRE
-#define X3_BPRE 0                // 1: a chunk's B planes of every column tile loaded before its MFMAs (tuning)
+#ifndef X3_BPIPE
+#define X3_BPIPE 1               // B planes read one column tile ahead of their MFMAs (0: just in time;
+                                 // profiles/r4/ab_bpipe.json)
 #endif
 #ifndef X3_HEAD_BARRIER
 #define X3_HEAD_BARRIER 0        // 1: a workgroup barrier after each head of head layer 1 (tuning)
@@ -484,12 +485,14 @@ __device__ __forceinline__ void split3_pair(f32x4 u, f32x4 v, float s, f16x8 (&p
 // One pipelined step of a 256-deep f16x3 layer: step G issues the loads of chunk G (tile T[t]'s three
 // weight planes, 3 KiB per tile: pack_h16_fragments' [T][c][plane][lane]) and computes chunk G - D from
 // the ring; B = activation planes in LDS, [chunk][ct][plane][lane]. acc += hi*hi, cor += the five cross
-// products, smallest first. One column tile's planes are live at a time. Steps 0..D-1 only prime the
-// ring (no B or accumulator access), so they can run before a barrier or under another phase.
+// products, smallest first. The B planes of column tile ct + 1 are read while column tile ct's MFMAs
+// run (X3_BPIPE; sched barriers keep the compiler from sinking the reads to their first use, where
+// each became an lgkmcnt(0) stall). Steps 0..D-1 only prime the ring (no B or accumulator access), so
+// they can run before a barrier or under another phase.
 template <int G, int GEND, int TT, int NT, int D>
-__device__ __forceinline__ void stream_x3_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
-                                               int lane, int voff, f16x8 (&ring)[D + 1][TT][X3P],
-                                               f32x4 (&acc)[TT][NT], f32x4 (&cor)[TT][NT]) {
+__device__ __forceinline__ void stream_x3_rec(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
+                                              int lane, int voff, f16x8 (&ring)[D + 1][TT][X3P],
+                                              f32x4 (&acc)[TT][NT], f32x4 (&cor)[TT][NT], f16x8 (&bc)[X3P]) {
     if constexpr (G < GEND) {
         if constexpr (G < KC_HID) {
 #pragma unroll
@@ -510,22 +513,46 @@ __device__ __forceinline__ void stream_x3_step(__amdgpu_buffer_rsrc_t W, const i
             else
                 __builtin_amdgcn_s_setprio(0);
 #endif
-#if X3_BPRE
-            f16x8 bp[NT][X3P];   // every column tile's planes of this chunk up front (tuning variant)
+#if X3_BPIPE
+            // B planes one column tile ahead: column tile ct + 1's (or the next chunk's first) reads are in
+            // flight during column tile ct's MFMAs
+            if constexpr (GG == 0) {
 #pragma unroll
-            for (int ct = 0; ct < NT; ++ct)
-#pragma unroll
-                for (int p = 0; p < X3P; ++p) bp[ct][p] = B[((GG * NT + ct) * X3P + p) * 64 + lane];
-#endif
+                for (int p = 0; p < X3P; ++p) bc[p] = B[p * 64 + lane];
+            }
 #pragma unroll
             for (int ct = 0; ct < NT; ++ct) {
-#if X3_BPRE
-                const f16x8 b0 = bp[ct][0], b1 = bp[ct][1], b2 = bp[ct][2];
+                f16x8 bn[X3P];
+                const int nx = ct + 1 < NT ? (GG * NT + ct + 1) : ((GG + 1) * NT);
+                if (ct + 1 < NT || GG + 1 < KC_HID) {
+#pragma unroll
+                    for (int p = 0; p < X3P; ++p) bn[p] = B[(nx * X3P + p) * 64 + lane];
+                }
+                __builtin_amdgcn_sched_barrier(0);   // the reads stay ahead of this column tile's MFMAs
+                const f16x8 b0 = bc[0], b1 = bc[1], b2 = bc[2];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    f32x4 c = cor[t][ct];
+                    c = mfma_h(ring[S][t][2], b0, c);
+                    c = mfma_h(ring[S][t][0], b2, c);
+                    c = mfma_h(ring[S][t][1], b1, c);
+                    c = mfma_h(ring[S][t][1], b0, c);
+                    c = mfma_h(ring[S][t][0], b1, c);
+                    cor[t][ct] = c;
+                    acc[t][ct] = mfma_h(ring[S][t][0], b0, acc[t][ct]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (ct + 1 < NT || GG + 1 < KC_HID) {
+#pragma unroll
+                    for (int p = 0; p < X3P; ++p) bc[p] = bn[p];
+                }
+            }
 #else
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) {
                 const f16x8 b0 = B[((GG * NT + ct) * X3P + 0) * 64 + lane];
                 const f16x8 b1 = B[((GG * NT + ct) * X3P + 1) * 64 + lane];
                 const f16x8 b2 = B[((GG * NT + ct) * X3P + 2) * 64 + lane];
-#endif
 #pragma unroll
                 for (int t = 0; t < TT; ++t) {
                     f32x4 c = cor[t][ct];
@@ -538,9 +565,17 @@ __device__ __forceinline__ void stream_x3_step(__amdgpu_buffer_rsrc_t W, const i
                     acc[t][ct] = mfma_h(ring[S][t][0], b0, acc[t][ct]);
                 }
             }
+#endif
         }
-        stream_x3_step<G + 1, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc, cor);
+        stream_x3_rec<G + 1, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc, cor, bc);
     }
+}
+template <int G, int GEND, int TT, int NT, int D>
+__device__ __forceinline__ void stream_x3_step(__amdgpu_buffer_rsrc_t W, const int (&T)[TT], const f16x8* __restrict__ B,
+                                               int lane, int voff, f16x8 (&ring)[D + 1][TT][X3P],
+                                               f32x4 (&acc)[TT][NT], f32x4 (&cor)[TT][NT]) {
+    f16x8 bc[X3P];   // X3_BPIPE: the B planes of the next column tile, carried from step to step
+    stream_x3_rec<G, GEND, TT, NT, D>(W, T, B, lane, voff, ring, acc, cor, bc);
 }
 
 // The fp32 init rows of head layer 1 (hoisted pts + t blocks: pobj of each column's object, tproj) for this
