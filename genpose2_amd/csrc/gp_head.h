@@ -454,6 +454,14 @@ __device__ __forceinline__ float xin_row_absmax(f32x4 b) {
 #define X3_BPIPE 1               // B planes read one column tile ahead of their MFMAs (0: just in time;
                                  // profiles/r4/ab_bpipe.json)
 #endif
+#ifndef X3_CHAIN
+#define X3_CHAIN 1               // each tile's correction products back to back (R=25,600 -3 %, R=12,800 even;
+                                 // profiles/r4/ab_chain.json)
+#endif
+#ifndef X3_DIAG
+#define X3_DIAG 0                // timing diagnostics only (wrong results), bits: 1 no B-plane LDS reads after
+                                 // the first, 2 no weight loads after the ring's priming
+#endif
 #ifndef X3_HEAD_BARRIER
 #define X3_HEAD_BARRIER 0        // 1: a workgroup barrier after each head of head layer 1 (tuning)
 #endif
@@ -494,7 +502,7 @@ __device__ __forceinline__ void stream_x3_rec(__amdgpu_buffer_rsrc_t W, const in
                                               int lane, int voff, f16x8 (&ring)[D + 1][TT][X3P],
                                               f32x4 (&acc)[TT][NT], f32x4 (&cor)[TT][NT], f16x8 (&bc)[X3P]) {
     if constexpr (G < GEND) {
-        if constexpr (G < KC_HID) {
+        if constexpr (G < KC_HID && ((X3_DIAG & 2) == 0 || G < D + 1)) {
 #pragma unroll
             for (int t = 0; t < TT; ++t)
 #pragma unroll
@@ -524,12 +532,37 @@ __device__ __forceinline__ void stream_x3_rec(__amdgpu_buffer_rsrc_t W, const in
             for (int ct = 0; ct < NT; ++ct) {
                 f16x8 bn[X3P];
                 const int nx = ct + 1 < NT ? (GG * NT + ct + 1) : ((GG + 1) * NT);
-                if (ct + 1 < NT || GG + 1 < KC_HID) {
+                if ((X3_DIAG & 1) == 0 && (ct + 1 < NT || GG + 1 < KC_HID)) {
 #pragma unroll
                     for (int p = 0; p < X3P; ++p) bn[p] = B[(nx * X3P + p) * 64 + lane];
                 }
+#if X3_DIAG & 1
+#pragma unroll
+                for (int p = 0; p < X3P; ++p) {   // distinct operands per tile, so the MFMAs stay distinct
+                    using u4 = __attribute__((ext_vector_type(4))) unsigned;
+                    bn[p] = __builtin_bit_cast(f16x8, __builtin_bit_cast(u4, bc[p]) ^ (unsigned)(nx + 1));
+                }
+#endif
                 __builtin_amdgcn_sched_barrier(0);   // the reads stay ahead of this column tile's MFMAs
                 const f16x8 b0 = bc[0], b1 = bc[1], b2 = bc[2];
+#if X3_CHAIN
+                // each tile's five correction products back to back on one accumulator, then the main
+                // products (the issue rate itself does not depend on the order, scripts/mfma_chain_probe.hip;
+                // this order measured 3 % faster at two passes, even at one)
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    f32x4 c = cor[t][ct];
+                    c = mfma_h(ring[S][t][2], b0, c);
+                    c = mfma_h(ring[S][t][0], b2, c);
+                    c = mfma_h(ring[S][t][1], b1, c);
+                    c = mfma_h(ring[S][t][1], b0, c);
+                    c = mfma_h(ring[S][t][0], b1, c);
+                    cor[t][ct] = c;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t][ct] = mfma_h(ring[S][t][0], b0, acc[t][ct]);
+#else
 #pragma unroll
                 for (int t = 0; t < TT; ++t) {
                     f32x4 c = cor[t][ct];
@@ -541,6 +574,7 @@ __device__ __forceinline__ void stream_x3_rec(__amdgpu_buffer_rsrc_t W, const in
                     cor[t][ct] = c;
                     acc[t][ct] = mfma_h(ring[S][t][0], b0, acc[t][ct]);
                 }
+#endif
                 __builtin_amdgcn_sched_barrier(0);
                 if (ct + 1 < NT || GG + 1 < KC_HID) {
 #pragma unroll
