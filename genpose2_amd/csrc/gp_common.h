@@ -136,6 +136,23 @@ __device__ __forceinline__ float row16_max(float v) {
 __device__ __forceinline__ f32x4 row16_max4(f32x4 v) {
     return f32x4{row16_max(v.x), row16_max(v.y), row16_max(v.z), row16_max(v.w)};
 }
+// The same four maxima scattered over the row: lane n (n = lane & 15) ends with the max of component
+// (n >> 2) & 3, every lane of its quad alike -- 16 instructions instead of row16_max4's 32. Lanes n and
+// n ^ 8 first trade halves (x, y stay below 8, z, w above), then each half-row trades with its mirror
+// lane 7 - n (the other quad of the half), which leaves one component per quad, reduced over the quad
+// by two more DPP levels. Maxima are exact, so the result equals row16_max4's bit for bit.
+__device__ __forceinline__ float row16_max_scatter4(f32x4 v, int n) {
+    const bool h8 = (n & 8) != 0, h4 = (n & 4) != 0;
+    float a0 = h8 ? v.z : v.x, a1 = h8 ? v.w : v.y;
+    const float s0 = h8 ? v.x : v.z, s1 = h8 ? v.y : v.w;
+    a0 = __builtin_elementwise_maximum(a0, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0x128, 0xF, 0xF, true)));
+    a1 = __builtin_elementwise_maximum(a1, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s1), 0x128, 0xF, 0xF, true)));
+    float r = h4 ? a1 : a0;
+    const float s = h4 ? a0 : a1;
+    r = __builtin_elementwise_maximum(r, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x141, 0xF, 0xF, true)));
+    r = dpp_max<0xB1>(r);
+    return dpp_max<0x4E>(r);
+}
 // value of lane 4*(l/4) (first lane of the quad)
 __device__ __forceinline__ float quad_bcast0(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x00, 0xF, 0xF, false));

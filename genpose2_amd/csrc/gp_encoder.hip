@@ -423,26 +423,38 @@ __device__ __forceinline__ int col_exponent(float m) { return m > 1e-30f ? ilog2
 // 32c + 16 + 4q + j (j < 4) of every chunk c -- exactly its B fragments.
 // Neighbour index and centroid of lane column n of column tile ct: loaded at kernel entry, one round trip
 // ahead of the layer-0 gather that depends on them.
-struct Gather0Pre {
-    int p;
-    float cx, cy, cz;
-};
-__device__ __forceinline__ Gather0Pre split_gather0_pre(const SplitArgs& a, int b, int col0, int ct, int lane) {
+__device__ __forceinline__ int split_gather0_pre(const SplitArgs& a, int b, int col0, int ct, int lane) {
     const int g = col0 + ct * 16 + (lane & 15);
-    if (g >= a.cols) return Gather0Pre{0, 0.f, 0.f, 0.f};   // past the last centroid (ragged last workgroup)
+    if (g >= a.cols) return 0;   // past the last centroid (ragged last workgroup)
     const int m = g / a.ns, s = g - (g / a.ns) * a.ns;
-    const float* cc = a.cent + ((size_t)b * a.m + m) * 3;
-    return Gather0Pre{a.nbr[((size_t)b * a.m + m) * a.ns + s], cc[0], cc[1], cc[2]};
+    return a.nbr[((size_t)b * a.m + m) * a.ns + s];
+}
+
+// The centroid term of layer 0, W0_xyz . x_c, for each of the workgroup's centroids and layer-0 channels
+// (P[ci][ch], ci = the workgroup's ci-th centroid), computed once per workgroup: every column of a 16-column
+// tile shares its centroid, so the gather reads it as one broadcast LDS read per 4 channels instead of
+// recomputing it from (wx, wy, wz) in all 16 lanes. Same expression and order as before: bit-identical.
+template <int CT, int KC0>
+__device__ __forceinline__ void split_centroid_term(const SplitArgs& a, float* P, int b, int col0, int tid) {
+#pragma clang fp contract(off)
+    const int nci = 16 * CT / a.ns, mi0 = col0 / a.ns;
+    for (int idx = tid; idx < nci * KC0 * 32; idx += SPLIT_WV * 64) {
+        const int ci = idx / (KC0 * 32), ch = idx - ci * (KC0 * 32);
+        const int mi = min(mi0 + ci, a.m - 1);   // past the last centroid: any value (never stored)
+        const float* cc = a.cent + ((size_t)b * a.m + mi) * 3;
+        const f32x4 w = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
+        P[idx] = (w.x * cc[0] + w.y * cc[1]) + w.z * cc[2];
+    }
 }
 
 template <int CT, int KC0>
-__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, const f32x4* w0x, int b,
-                                              int ct, int lane, const Gather0Pre pre) {
+__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, const f32x4* P4, int b,
+                                              int col0, int ct, int lane, const int p) {
 #pragma clang fp contract(off)
     const int q = lane >> 4, n = lane & 15;
     const int col = ct * 16 + n;
-    const int p = pre.p;
-    const float cx = pre.cx, cy = pre.cy, cz = pre.cz;
+    const int ci = (col0 + ct * 16) / a.ns - col0 / a.ns;   // the tile's centroid within the workgroup
+    const f32x4* pc = P4 + ci * KC0 * 8 + q;                 // channels 32 c + 16 h + 4 q .. + 3: pc[8 c + 4 h]
     const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
     f32x4 v[KC0][2];
 #pragma unroll
@@ -456,10 +468,10 @@ __device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int*
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             float r[4];
+            const f32x4 t = pc[8 * c + 4 * h];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const f32x4 w = w0x[32 * c + 16 * h + 4 * q + j];
-                r[j] = relu1(v[c][h][j] - ((w.x * cx + w.y * cy) + w.z * cz));
+                r[j] = relu1(v[c][h][j] - t[j]);
                 mx = fmax2(mx, r[j]);
             }
             v[c][h] = f32x4{r[0], r[1], r[2], r[3]};
@@ -480,16 +492,16 @@ __device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int*
 // 0 (waves < CT), streams, and leaves the planes of its outputs in X (over layer 0's) plus every
 // column's exponent in e1[ct] (for lane column n). Executes the same two barriers in every wave.
 template <int CT, int KC0, int NC, int D>
-__device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* w0x,
+__device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* P4,
                                              int b, int col0, int wid, int lane, int oc1, int (&e1)[CT],
-                                             const Gather0Pre pre) {
+                                             const int pre) {
     constexpr int C = 16 * CT;
     const int q = lane >> 4, n = lane & 15;
     float pmax[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) pmax[ct] = 0.f;
     if constexpr (NC == 0) {
-        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, wid, lane, pre);
+        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, P4, b, col0, wid, lane, pre);
         __syncthreads();
         if (q == 0)
 #pragma unroll
@@ -518,7 +530,7 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
         stream_hk_step<KC0, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
-        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, w0x, b, wid, lane, pre);
+        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, P4, b, col0, wid, lane, pre);
         __syncthreads();
         SPLIT_MARK(a, 2);
         stream_hk_step<KC0, D, KC0 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
@@ -598,11 +610,9 @@ __device__ __forceinline__ void split_layer2(const SplitArgs& a, const f16x8* X,
                 if (ct & 1) continue;
                 v[ct] = vmax4(v[ct], v[ct + 1]);
             }
-            const f32x4 r = row16_max4(v[ct]);
+            const float r = row16_max_scatter4(v[ct], n);   // channel 16 T[t] + 4 q + (n >> 2)
             const int mi = (col0 + ct * 16) / a.ns;
-            if (n == 0 && mi < a.m) {
-                st4(a.out + ((size_t)b * a.m + mi) * a.c_out_total + a.out_off + 16 * T[t] + 4 * q, r);
-            }
+            if ((n & 3) == 0 && mi < a.m) a.out[((size_t)b * a.m + mi) * a.c_out_total + a.out_off + 16 * T[t] + 4 * q + (n >> 2)] = r;
         }
     }
 }
@@ -611,16 +621,15 @@ template <int CT, int D, int KC0, int OC1, int OC2>
 __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     constexpr int C = 16 * CT, KX = KC0 > OC1 ? KC0 : OC1;
     f16x8* X = reinterpret_cast<f16x8*>(smem);                       // [chunk][ct][plane][lane]
-    f32x4* w0x = reinterpret_cast<f32x4*>(smem + (size_t)KX * CT * 2048);   // (wx, wy, wz, 0) per channel
-    float* pm = reinterpret_cast<float*>(w0x + KC0 * 32);           // [wave][column] partial maxima
+    float* P = reinterpret_cast<float*>(smem + (size_t)KX * CT * 2048);   // [centroid][channel] W0_xyz . x_c
+    float* pm = P + CT * KC0 * 32;                                   // [wave][column] partial maxima
     int* e0s = reinterpret_cast<int*>(pm + SPLIT_WV * C);           // layer-0 column exponents
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.y, col0 = blockIdx.x * C;
     SPLIT_MARK(a, 0);
-    const Gather0Pre pre = wid < CT ? split_gather0_pre(a, b, col0, wid, lane) : Gather0Pre{0, 0.f, 0.f, 0.f};
-    for (int ch = tid; ch < KC0 * 32; ch += SPLIT_WV * 64)   // packed layer-0 fragment of channel ch, q = 0
-        w0x[ch] = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
+    const int pre = wid < CT ? split_gather0_pre(a, b, col0, wid, lane) : 0;
+    split_centroid_term<CT, KC0>(a, P, b, col0, tid);
     __syncthreads();
     SPLIT_MARK(a, 1);
     int e1[CT];
@@ -628,9 +637,9 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     constexpr int NC1_HI = (OC1 + SPLIT_WV - 1) / SPLIT_WV;
     const int nc1 = wid < OC1 % SPLIT_WV || OC1 % SPLIT_WV == 0 ? NC1_HI : NC1_HI - 1;
     if (nc1 == NC1_HI)
-        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
+        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, reinterpret_cast<const f32x4*>(P), b, col0, wid, lane, OC1, e1, pre);
     else
-        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, w0x, b, col0, wid, lane, OC1, e1, pre);
+        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, reinterpret_cast<const f32x4*>(P), b, col0, wid, lane, OC1, e1, pre);
     static_assert(OC2 % SPLIT_WV == 0, "layer-2 chunks spread evenly over the waves");
     split_layer2<CT, OC1, OC2 / SPLIT_WV, D>(a, X, e1, b, col0, wid, lane, OC2);
     SPLIT_MARK(a, 7);
@@ -639,8 +648,9 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
 // Both branches of a level per launch (blockIdx.z = branch).
 // CT column tiles per workgroup (whole centroids; the last workgroup of a branch may be ragged), D
 // 32-deep weight chunks in flight per layer.
-template <int CT, int D, int KC0, int OC1A, int OC2A, int OC1B, int OC2B>
-__global__ __launch_bounds__(SPLIT_WV * 64) void sa_split_kernel(SplitArgs a0, SplitArgs a1) {
+// MINB: workgroups per CU the register budget is held to (2 at level 2, whose LDS fits two: 128 VGPRs).
+template <int CT, int D, int KC0, int OC1A, int OC2A, int OC1B, int OC2B, int MINB = 1>
+__global__ __launch_bounds__(SPLIT_WV * 64) __attribute__((amdgpu_waves_per_eu(2 * MINB))) void sa_split_kernel(SplitArgs a0, SplitArgs a1) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.z == 0) {
         if ((int)blockIdx.x * 16 * CT < a0.cols) sa_split_body<CT, D, KC0, OC1A, OC2A>(a0, smem);
@@ -670,7 +680,7 @@ __global__ __launch_bounds__(SPLIT_WV * 64) void sa_split_kernel(SplitArgs a0, S
 template <int CT, int KC0, int OC1>
 static size_t sa_split_lds() {
     constexpr int KX = KC0 > OC1 ? KC0 : OC1;
-    return (size_t)KX * CT * 2048 + (size_t)KC0 * 32 * 16 + sizeof(float) * SPLIT_WV * 16 * CT + sizeof(int) * 16 * CT;
+    return (size_t)KX * CT * 2048 + sizeof(float) * CT * KC0 * 32 + sizeof(float) * SPLIT_WV * 16 * CT + sizeof(int) * 16 * CT;
 }
 
 // ============================================================================ narrow levels
@@ -832,8 +842,9 @@ __device__ __forceinline__ void narrow_branch(const NarrowArgs& a, f32x4* lds) {
         float* o = a.out + (size_t)task * a.c_out_total + a.out_off + 4 * q;
 #pragma unroll
         for (int t = 0; t < NT2; ++t) {
-            const f32x4 v = relu4(row16_max4(rmax[t]) + ld4(&sB2[16 * t + 4 * q]));
-            if (nn == 0) st4(o + 16 * t, v);
+            const int j = nn >> 2;   // row16_max_scatter4 leaves channel 16 t + 4 q + j in this quad
+            const float r = relu1(row16_max_scatter4(rmax[t], nn) + sB2[16 * t + 4 * q + j]);
+            if ((nn & 3) == 0) o[16 * t + j] = r;
         }
         cur = nxt;
     }
@@ -950,8 +961,9 @@ __device__ __forceinline__ void narrow_branch_split(const NarrowArgs& a, f32x4* 
         float* o = a.out + (size_t)task * a.c_out_total + a.out_off + 4 * q;
 #pragma unroll
         for (int t = 0; t < NT2; ++t) {
-            const f32x4 v = relu4(row16_max4(rmax[t]) + ld4(&sB2[16 * t + 4 * q]));
-            if (nn == 0) st4(o + 16 * t, v);
+            const int j = nn >> 2;   // row16_max_scatter4 leaves channel 16 t + 4 q + j in this quad
+            const float r = relu1(row16_max_scatter4(rmax[t], nn) + sB2[16 * t + 4 * q + j]);
+            if ((nn & 3) == 0) o[16 * t + j] = r;
         }
         cur = nxt;
     }
@@ -1255,9 +1267,9 @@ __global__ __launch_bounds__(TG_THREADS) void tok_split_gemm_kernel(TokArgs a) {
         const int obj = (m0 + 64 * wt) >> 6;   // the wave's 64 points are one object
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const f32x4 v = relu4(row16_max4(pm[i]) + ld4(bias + (T0 + 4 * wo + i) * 16 + 4 * q));
-            if (n == 0 && obj * 64 < a.M)
-                st4(a.out + (size_t)obj * a.ldo + a.out_off[br] + (T0 + 4 * wo + i) * 16 + 4 * q, v);
+            const int j = n >> 2;   // row16_max_scatter4 leaves channel ... + 4 q + j in this quad
+            const float r = relu1(row16_max_scatter4(pm[i], n) + bias[(T0 + 4 * wo + i) * 16 + 4 * q + j]);
+            if ((n & 3) == 0 && obj * 64 < a.M) a.out[(size_t)obj * a.ldo + a.out_off[br] + (T0 + 4 * wo + i) * 16 + 4 * q + j] = r;
         }
     }
 }
@@ -1734,7 +1746,7 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
         const dim3 grid((cmax + 16 * CT - 1) / (16 * CT), B, 2), blk(SPLIT_WV * 64);
         if (l == 2) {
             const size_t lds = sa_split_lds<SPLIT_CT2, 4, 7>();
-            hipLaunchKernelGGL((sa_split_kernel<SPLIT_CT2, SPLIT_D2, 4, 7, 8, 7, 8>), grid, blk, lds, st, sp[0], sp[1]);
+            hipLaunchKernelGGL((sa_split_kernel<SPLIT_CT2, SPLIT_D2, 4, 7, 8, 7, 8, 2>), grid, blk, lds, st, sp[0], sp[1]);
         } else {
             const size_t lds = std::max(sa_split_lds<SPLIT_CT3, 8, 8>(), sa_split_lds<SPLIT_CT3, 8, 12>());
             hipLaunchKernelGGL((sa_split_kernel<SPLIT_CT3, SPLIT_D3, 8, 8, 16, 12, 16>), grid, blk, lds, st, sp[0],
