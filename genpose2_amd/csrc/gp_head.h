@@ -57,7 +57,6 @@ struct HeadSmem {
     float h2w[9 * HID];                // head layer 2, [head*3 + out][256]
     float h2b[12];
     f32x4 cscl[NT * 16][2];            // split trunk: per-column scales {s1, s2, u2, uh}, {sh} (ColScales)
-    int task;                          // f16x3 trunk, X3_DYN: next head-layer-1 task to hand out
 };
 
 // Threads [FIRST, WV*64) copy the small weights into LDS.
@@ -459,9 +458,6 @@ __device__ __forceinline__ float xin_row_absmax(f32x4 b) {
 #define X3_CHAIN 1               // each tile's correction products back to back (R=25,600 -3 %, R=12,800 even;
                                  // profiles/r4/ab_chain.json)
 #endif
-#ifndef X3_DYN
-#define X3_DYN 0                 // 1: head-layer-1 (head, tile pair) tasks handed out through an LDS counter (tuning)
-#endif
 #ifndef X3_DIAG
 #define X3_DIAG 0                // timing diagnostics only (wrong results), bits: 1 no B-plane LDS reads after
                                  // the first, 2 no weight loads after the ring's priming, 4 no head-layer-2
@@ -718,82 +714,6 @@ __device__ __forceinline__ void head_x3_head(__amdgpu_buffer_rsrc_t WH, const f1
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// X3_DYN: head layer 1 as 3 x WV tasks (head H, tile pair p) -- task (H, p) is exactly what wave p does for
-// head H in head_x3_head -- handed out by an LDS counter instead of statically: the older wave of a SIMD
-// wins MFMA issue and used to finish its three heads ~14k cycles before its partner, which then ran alone.
-// Partials go to sm.red[...][p] and head_out sums them in p order, so the result is bit-identical.
-template <int NT, int TPW>
-__device__ __forceinline__ void head_x3_init_load_rt(__amdgpu_buffer_rsrc_t RP, __amdgpu_buffer_rsrc_t RT, const int (&vo)[NT],
-                                                     int H, int p, int lane, f32x4 (&tpv)[TPW], f32x4 (&pov)[TPW][NT]) {
-    const int q = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        const int T = H * 16 + p * TPW + t;
-        tpv[t] = ldbuf4(RT, 16 * q, 64 * T);
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) pov[t][ct] = ldbuf4(RP, vo[ct], 64 * T);
-    }
-}
-template <int NT, int WV, int TPW, int DH>
-__device__ __forceinline__ void head_x3_task(int task, int next, __amdgpu_buffer_rsrc_t WH, const f16x8* __restrict__ act2h,
-                                             __amdgpu_buffer_rsrc_t RP, __amdgpu_buffer_rsrc_t RT, const int (&vo)[NT],
-                                             HeadSmem<NT, WV, X3P>& sm, const float (&uh)[NT], const float (&sh)[NT],
-                                             int lane, f16x8 (&ringh)[DH + 1][TPW][X3P], f32x4 (&tpv)[TPW],
-                                             f32x4 (&pov)[TPW][NT]) {
-    static_assert((3 * NT) % 4 == 0, "a task's 3 NT partials form whole reduce-scatter groups");
-    const int q = lane >> 4, n = lane & 15;
-    const int voff = lane * 16;
-    const int H = task / WV, p = task - (task / WV) * WV;
-    int TH[TPW];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) TH[t] = H * 16 + p * TPW + t;
-    f32x4 acc[TPW][NT], cor[TPW][NT];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-            acc[t][ct] = (pov[t][ct] + tpv[t]) * sh[ct];
-            cor[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    stream_x3_step<DH, KC_HID + DH, TPW, NT, DH>(WH, TH, act2h, lane, voff, ringh, acc, cor);
-    if (next < 3 * WV) {   // the next task's first chunks and init rows, in flight across this epilogue
-        const int Hn = next / WV, pn = next - (next / WV) * WV;
-        int TN[TPW];
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) TN[t] = Hn * 16 + pn * TPW + t;
-        stream_x3_step<0, DH, TPW, NT, DH>(WH, TN, act2h, lane, voff, ringh, acc, cor);
-    }
-    __builtin_amdgcn_sched_barrier(0);   // no row swap inside an MFMA stream (see head_x3_head)
-    float lv[3 * NT];
-#pragma unroll
-    for (int v = 0; v < 3 * NT; ++v) lv[v] = 0.f;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        const int ch = 16 * (p * TPW + t) + 4 * q;
-        const f32x4 w0 = ld4(&sm.h2w[(H * 3 + 0) * HID + ch]);
-        const f32x4 w1 = ld4(&sm.h2w[(H * 3 + 1) * HID + ch]);
-        const f32x4 w2 = ld4(&sm.h2w[(H * 3 + 2) * HID + ch]);
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-            const f32x4 u = relu4((acc[t][ct] + cor[t][ct]) * uh[ct]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                lv[ct * 3 + 0] = __builtin_fmaf(u[j], w0[j], lv[ct * 3 + 0]);
-                lv[ct * 3 + 1] = __builtin_fmaf(u[j], w1[j], lv[ct * 3 + 1]);
-                lv[ct * 3 + 2] = __builtin_fmaf(u[j], w2[j], lv[ct * 3 + 2]);
-            }
-        }
-    }
-    if (next < 3 * WV) {   // the next task's init rows, once this task's accumulators are dead
-        const int Hn = next / WV, pn = next - (next / WV) * WV;
-        head_x3_init_load_rt<NT, TPW>(RP, RT, vo, Hn, pn, lane, tpv, pov);
-    }
-#pragma unroll
-    for (int g = 0; g < 3 * NT / 4; ++g)
-        sm.red[4 * (H * 3 * NT / 4 + g) + q][n][p] = rows_sum_scatter4(lv[4 * g], lv[4 * g + 1], lv[4 * g + 2], lv[4 * g + 3]);
-    __builtin_amdgcn_sched_barrier(0);
-}
-
 template <int NT, int WV, bool PRE = false>
 __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const float* __restrict__ pobj,
                                               const float* __restrict__ tproj, const int* obj_of_col,
@@ -891,32 +811,12 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
             for (int p = 0; p < X3P; ++p) act2h[(((Ta >> 1) * NT + ct) * X3P + p) * 64 + lane] = pl[p];
         }
     }
-    if constexpr (X3_DYN) {
-        if (threadIdx.x == 0) sm.task = WV;   // tasks WV.. are handed out; the first WV are the waves' own
-    }
     __syncthreads();
     PC_MARK(4);
     // ---- head layer 1 (pose block 256 -> 3x256) head by head, each followed by its layer-2 partials
     float pv[SM::kRedV];
 #pragma unroll
     for (int v = 9 * NT; v < SM::kRedV; ++v) pv[v] = 0.f;
-#if X3_DYN
-    if constexpr ((3 * NT) % 4 == 0) {
-        int task = wid;   // tasks 0..WV-1 (head 0): the wave's own tiles, primed above
-        while (true) {
-            int nl = 0;
-            if (lane == 0) nl = atomicAdd(&sm.task, 1);
-            const int next = __builtin_amdgcn_readfirstlane(nl);
-            head_x3_task<NT, WV, TPW, DH>(task, next, WH, act2h, RP, RT, vo, sm, uh, sh, lane, ringh, tpv, pov);
-            if (next >= 3 * WV) break;
-            task = next;
-        }
-    } else {
-        head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
-        head_x3_head<1, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
-        head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
-    }
-#else
     head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
     if constexpr (X3_HEAD_BARRIER) __syncthreads();
     PC_MARK(13);
@@ -924,7 +824,6 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
     if constexpr (X3_HEAD_BARRIER) __syncthreads();
     PC_MARK(14);
     head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
-#endif
     if constexpr (X3_PRIO) __builtin_amdgcn_s_setprio(0);
     PC_MARK(5);
     if constexpr ((3 * NT) % 4 != 0) {
