@@ -188,9 +188,15 @@ static int run(const f16x8* in, f32x4* out, unsigned long long* cyc, int waves, 
     CK(hipDeviceSynchronize());
     static unsigned long long h[1024 * 8];
     CK(hipMemcpy(h, cyc, sizeof(unsigned long long) * g_wgs * waves, hipMemcpyDeviceToHost));
+    // the SIMD's time is its LAST wave's (the older wave of a pair wins issue and finishes first, so a
+    // mean over waves would overstate the pair's rate)
     double m = 0;
-    for (int i = 0; i < g_wgs * waves; ++i) m += (double)h[i];
-    m /= g_wgs * waves;
+    for (int g = 0; g < g_wgs; ++g) {
+        unsigned long long mx = 0;
+        for (int i = 0; i < waves; ++i) mx = h[g * waves + i] > mx ? h[g * waves + i] : mx;
+        m += (double)mx;
+    }
+    m /= g_wgs;
     // cycles per MFMA per SIMD: each wave issued 48 n MFMAs; waves / 4 waves share a SIMD
     printf("{\"pattern\": %d, \"unroll\": %d, \"fill\": %d, \"wgs\": %d, \"waves_per_simd\": %d, \"cycles_per_mfma_per_simd\": %.2f}\n", P, UNR, g_fill, g_wgs,
            waves / 4, m / (48.0 * n) / (waves / 4));
