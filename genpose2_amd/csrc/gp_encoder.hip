@@ -447,21 +447,26 @@ __device__ __forceinline__ void split_centroid_term(const SplitArgs& a, float* P
     }
 }
 
-template <int CT, int KC0>
-__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, const f32x4* P4, int b,
-                                              int col0, int ct, int lane, const int p) {
-#pragma clang fp contract(off)
-    const int q = lane >> 4, n = lane & 15;
-    const int col = ct * 16 + n;
-    const int ci = (col0 + ct * 16) / a.ns - col0 / a.ns;   // the tile's centroid within the workgroup
-    const f32x4* pc = P4 + ci * KC0 * 8 + q;                 // channels 32 c + 16 h + 4 q .. + 3: pc[8 c + 4 h]
-    const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * q;
-    f32x4 v[KC0][2];
+// The lane's layer-0 projection row of its neighbour (the gathered Q values of chunk c, half h),
+// loaded at kernel entry so the loads overlap the centroid-term staging and its barrier.
+template <int KC0>
+__device__ __forceinline__ void split_gather0_load(const SplitArgs& a, int b, int p, int lane, f32x4 (&v)[KC0][2]) {
+    const float* qrow = a.qin + ((size_t)b * a.n_prev + p) * a.q_stride + a.q_off + 4 * (lane >> 4);
 #pragma unroll
     for (int c = 0; c < KC0; ++c) {
         v[c][0] = ld4(qrow + 32 * c);
         v[c][1] = ld4(qrow + 32 * c + 16);
     }
+}
+
+template <int CT, int KC0>
+__device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int* e0s, const f32x4* P4, int col0,
+                                              int ct, int lane, f32x4 (&v)[KC0][2]) {
+#pragma clang fp contract(off)
+    const int q = lane >> 4, n = lane & 15;
+    const int col = ct * 16 + n;
+    const int ci = (col0 + ct * 16) / a.ns - col0 / a.ns;   // the tile's centroid within the workgroup
+    const f32x4* pc = P4 + ci * KC0 * 8 + q;                 // channels 32 c + 16 h + 4 q .. + 3: pc[8 c + 4 h]
     float mx = 0.f;
 #pragma unroll
     for (int c = 0; c < KC0; ++c)
@@ -494,14 +499,17 @@ __device__ __forceinline__ void split_gather0(const SplitArgs& a, f16x8* X, int*
 template <int CT, int KC0, int NC, int D>
 __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* P4,
                                              int b, int col0, int wid, int lane, int oc1, int (&e1)[CT],
-                                             const int pre) {
+                                             f32x4 (&gq)[KC0][2], bool loaded, int pnb) {
     constexpr int C = 16 * CT;
     const int q = lane >> 4, n = lane & 15;
     float pmax[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) pmax[ct] = 0.f;
     if constexpr (NC == 0) {
-        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, P4, b, col0, wid, lane, pre);
+        if (wid < CT) {
+            if (!loaded) split_gather0_load<KC0>(a, b, pnb, lane, gq);
+            split_gather0<CT, KC0>(a, X, e0s, P4, col0, wid, lane, gq);
+        }
         __syncthreads();
         if (q == 0)
 #pragma unroll
@@ -530,7 +538,10 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
         stream_hk_step<KC0, 0, D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
-        if (wid < CT) split_gather0<CT, KC0>(a, X, e0s, P4, b, col0, wid, lane, pre);
+        if (wid < CT) {
+            if (!loaded) split_gather0_load<KC0>(a, b, pnb, lane, gq);
+            split_gather0<CT, KC0>(a, X, e0s, P4, col0, wid, lane, gq);
+        }
         __syncthreads();
         SPLIT_MARK(a, 2);
         stream_hk_step<KC0, D, KC0 + D, 2 * NC, CT, D>(W, T, X, lane, voff, ring, acc);
@@ -628,18 +639,31 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.y, col0 = blockIdx.x * C;
     SPLIT_MARK(a, 0);
-    const int pre = wid < CT ? split_gather0_pre(a, b, col0, wid, lane) : 0;
+    // level 3 (256-wide layer 0): the gather's loads go out before the centroid-term barrier; level 2
+    // issues them after it (its 64 registers would not fit the 128 of two workgroups per CU)
+    constexpr bool EARLY = KC0 >= 8;
+    f32x4 gq[KC0][2];
+    const int pnb = wid < CT ? split_gather0_pre(a, b, col0, wid, lane) : 0;
     split_centroid_term<CT, KC0>(a, P, b, col0, tid);
-    __syncthreads();
+    // after the centroid terms' loads (vmcnt counts in order: issued before them, the gather loads would
+    // be waited for there)
+    if (EARLY && wid < CT) split_gather0_load<KC0>(a, b, pnb, lane, gq);
+    if constexpr (EARLY) {
+        // LDS-only barrier: the centroid terms' stores are complete (lgkmcnt), the gather loads stay in
+        // flight across it (__syncthreads would wait for them: vmcnt(0))
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+        __syncthreads();
+    }
     SPLIT_MARK(a, 1);
     int e1[CT];
     // layer-1 output chunks of this wave: wid, wid + 8, ... below OC1
     constexpr int NC1_HI = (OC1 + SPLIT_WV - 1) / SPLIT_WV;
     const int nc1 = wid < OC1 % SPLIT_WV || OC1 % SPLIT_WV == 0 ? NC1_HI : NC1_HI - 1;
     if (nc1 == NC1_HI)
-        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, reinterpret_cast<const f32x4*>(P), b, col0, wid, lane, OC1, e1, pre);
+        split_layer1<CT, KC0, NC1_HI, D>(a, X, e0s, pm, reinterpret_cast<const f32x4*>(P), b, col0, wid, lane, OC1, e1, gq, EARLY, pnb);
     else
-        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, reinterpret_cast<const f32x4*>(P), b, col0, wid, lane, OC1, e1, pre);
+        split_layer1<CT, KC0, (NC1_HI > 0 ? NC1_HI - 1 : 0), D>(a, X, e0s, pm, reinterpret_cast<const f32x4*>(P), b, col0, wid, lane, OC1, e1, gq, EARLY, pnb);
     static_assert(OC2 % SPLIT_WV == 0, "layer-2 chunks spread evenly over the waves");
     split_layer2<CT, OC1, OC2 / SPLIT_WV, D>(a, X, e1, b, col0, wid, lane, OC2);
     SPLIT_MARK(a, 7);
