@@ -513,13 +513,17 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
         __syncthreads();
         if (q == 0)
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) pm[wid * C + ct * 16 + n] = 0.f;
+            for (int ct = 0; ct < CT; ++ct) pm[(ct * 16 + n) * SPLIT_WV + wid] = 0.f;
         __syncthreads();
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             float M = 0.f;
+            {   // the column's SPLIT_WV wave partials, column-major: two 16-byte reads
+                const f32x4 p0 = ld4(&pm[(ct * 16 + n) * SPLIT_WV]), p1 = ld4(&pm[(ct * 16 + n) * SPLIT_WV + 4]);
+                const float pw[SPLIT_WV] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
 #pragma unroll
-            for (int w = 0; w < SPLIT_WV; ++w) M = fmaxf(M, pm[w * C + ct * 16 + n]);
+                for (int w = 0; w < SPLIT_WV; ++w) M = fmaxf(M, pw[w]);
+            }
             e1[ct] = col_exponent(M);
         }
     } else {
@@ -559,15 +563,19 @@ __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* 
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const float M = rows_max(pmax[ct]);
-            if (q == 0) pm[wid * C + ct * 16 + n] = M;
+            if (q == 0) pm[(ct * 16 + n) * SPLIT_WV + wid] = M;
         }
         __syncthreads();   // every read of layer 0's planes is done; the partial maxima are visible
         SPLIT_MARK(a, 4);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             float M = 0.f;
+            {   // the column's SPLIT_WV wave partials, column-major: two 16-byte reads
+                const f32x4 p0 = ld4(&pm[(ct * 16 + n) * SPLIT_WV]), p1 = ld4(&pm[(ct * 16 + n) * SPLIT_WV + 4]);
+                const float pw[SPLIT_WV] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
 #pragma unroll
-            for (int w = 0; w < SPLIT_WV; ++w) M = fmaxf(M, pm[w * C + ct * 16 + n]);
+                for (int w = 0; w < SPLIT_WV; ++w) M = fmaxf(M, pw[w]);
+            }
             e1[ct] = col_exponent(M);
             const float sc = exp2i(14 - e1[ct]);
 #pragma unroll
@@ -633,7 +641,7 @@ __device__ __forceinline__ void sa_split_body(const SplitArgs& a, char* smem) {
     constexpr int C = 16 * CT, KX = KC0 > OC1 ? KC0 : OC1;
     f16x8* X = reinterpret_cast<f16x8*>(smem);                       // [chunk][ct][plane][lane]
     float* P = reinterpret_cast<float*>(smem + (size_t)KX * CT * 2048);   // [centroid][channel] W0_xyz . x_c
-    float* pm = P + CT * KC0 * 32;                                   // [wave][column] partial maxima
+    float* pm = P + CT * KC0 * 32;                                   // [column][wave] partial maxima
     int* e0s = reinterpret_cast<int*>(pm + SPLIT_WV * C);           // layer-0 column exponents
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
