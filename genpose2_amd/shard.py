@@ -67,6 +67,10 @@ def broadcast_agent(agent, src: int = 0) -> None:
     host layer tables (``model_tables``), then drop caches derived from the old weights. Call it
     after construction and again after ``load_ckpt`` on ``src``."""
     dev_ = agent.device if agent.device.type == "cuda" else None
+    if dev_ is not None:
+        # and every write into them (a checkpoint's upload on src, on whatever stream) has landed before
+        # the collective copies them out
+        torch.cuda.synchronize(dev_)
     tabs = broadcast_packed(model_tensors(agent), model_tables(agent), src, dev_)
     if tabs:
         agent.encoder.set_table(tabs[0])
