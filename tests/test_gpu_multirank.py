@@ -61,6 +61,13 @@ def test_two_ranks_mismatched_seeds_equal_rank0_weights(tmp_path, with_ckpt):
         if with_ckpt:
             ref.score_agent.load_ckpt(model_dir=ckpt, model_path=True, load_model_only=True)
         parts.append(ref.run({k: v[lo:hi] for k, v in batch.items()}))
+    # every output's agreement first (per object), so a mismatch names what diverged, then the exact bar
+    report = {}
+    for k in ("pred_pose", "pts_feat", "energy", "aggregated", "length"):
+        want = torch.cat([getattr(p, k) for p in parts]).cpu().numpy()
+        got = np.load(tmp_path / f"{k}.npy")
+        report[k] = [int(i) for i in range(want.shape[0]) if not np.array_equal(got[i], want[i])]
+    print("objects differing from the per-shard reference:", report)
     for k in ("pred_pose", "pts_feat", "energy", "aggregated", "length"):
         want = torch.cat([getattr(p, k) for p in parts]).cpu().numpy()
         np.testing.assert_array_equal(np.load(tmp_path / f"{k}.npy"), want, err_msg=k)
