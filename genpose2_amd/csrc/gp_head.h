@@ -458,6 +458,10 @@ __device__ __forceinline__ float xin_row_absmax(f32x4 b) {
 #define X3_CHAIN 1               // each tile's correction products back to back (R=25,600 -3 %, R=12,800 even;
                                  // profiles/r4/ab_chain.json)
 #endif
+#ifndef X3_EPI_EARLY
+#define X3_EPI_EARLY 1           // pose_encoder.2 epilogue planes computed before the alias barrier
+                                 // (profiles/r4/ab_epi_early.json)
+#endif
 #ifndef X3_DIAG
 #define X3_DIAG 0                // timing diagnostics only (wrong results), bits: 1 no B-plane LDS reads after
                                  // the first, 2 no weight loads after the ring's priming, 4 no head-layer-2
@@ -797,6 +801,27 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
     for (int ct = 0; ct < NT; ++ct) vo[ct] = obj_of_col[ct * 16 + n] * (3 * HID * 4) + 16 * q;
     f32x4 tpv[TPW], pov[TPW][NT];
     head_x3_init_load<0, NT, TPW>(RP, RT, vo, wid, lane, tpv, pov);
+#if X3_EPI_EARLY
+    // the epilogue's planes are made before the alias barrier (a wave that finished its stream early does
+    // this VALU work while it waits for the last one) and only written after it
+    f16x8 pls[CPW][NT][X3P];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        const int Ta = T2[2 * c];
+        const f32x4 bias0 = ld4(&sm.pe2b[16 * Ta + 4 * q]), bias1 = ld4(&sm.pe2b[16 * (Ta + 1) + 4 * q]);
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+            split3_pair(relu4((acc2[2 * c][ct] + cor2[2 * c][ct]) * u2[ct] + bias0),
+                        relu4((acc2[2 * c + 1][ct] + cor2[2 * c + 1][ct]) * u2[ct] + bias1), s2[ct], pls[c][ct]);
+    }
+    if constexpr (SM::kAliasAct) __syncthreads();   // act2 overwrites act1: all reads done
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+            for (int p = 0; p < X3P; ++p) act2h[(((T2[2 * c] >> 1) * NT + ct) * X3P + p) * 64 + lane] = pls[c][ct][p];
+#else
     if constexpr (SM::kAliasAct) __syncthreads();   // act2 overwrites act1: all reads done
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
@@ -811,6 +836,7 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
             for (int p = 0; p < X3P; ++p) act2h[(((Ta >> 1) * NT + ct) * X3P + p) * 64 + lane] = pl[p];
         }
     }
+#endif
     __syncthreads();
     PC_MARK(4);
     // ---- head layer 1 (pose block 256 -> 3x256) head by head, each followed by its layer-2 partials
