@@ -50,6 +50,8 @@ class PoseNet:
         self._calls = 0
         self.after_encode = None                   # optional callable run by pred_func after the encoder
         self.ode_host_control = False              # ODE: True runs the RK45 controller on the host
+        self.ode_trace: Optional[list] = None      # ODE: a list receives [t, h, error norm] per step attempt
+                                                   # (host controller)
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(self.cfg.noise_seed)
         self.weights_source = f"synthetic(seed={self.cfg.seed})"
@@ -260,9 +262,9 @@ class PoseNet:
             x0 = rep_init.to(torch.float32) + x0
         be = DeviceRk45(self.heads, pobj, x0.to(self.device), K)
         t_eval = None if steps is None else np.linspace(T0, eps, steps)
-        if want_process or self.ode_host_control:
+        if want_process or self.ode_host_control or self.ode_trace is not None:
             # every solve_ivp output is kept: host-side controller, one error norm read per attempt
-            _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process)
+            _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process, trace=self.ode_trace)
         else:
             # default: the step controller runs on the device (no host round trip per attempt)
             x, nfev, status = rk45_device(be, T0, eps, t_eval=t_eval)
@@ -272,7 +274,7 @@ class PoseNet:
             be = DeviceRk45(self.heads, pobj, x0.to(self.device), K)
             _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=True)
             want_process = False
-        if want_process or self.ode_host_control or (status < 0 and t_eval is not None):
+        if want_process or self.ode_host_control or self.ode_trace is not None or (status < 0 and t_eval is not None):
             ys = be.outputs()                  # (n_t or 1, R*9) fp64
             if ys.shape[0] == 0:               # res.y[:, -1] of an empty solve_ivp result
                 raise IndexError("RK45 failed before collecting any t_eval point (res.y is empty)")

@@ -1721,8 +1721,18 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
         const dim3 grid(std::max(512, B), 3);
         if (l == 0 && na[1].w1h && na[1].w2h) {
             const size_t lds = std::max({narrow_lds(1, 1, 2), narrow_split_lds(1, 2, 4), fps_side_lds(fs)});
+#ifdef GP_NARROW_SEQ   // diagnostic builds only: the two branches as two launches (no co-resident mix)
+            NarrowArgs n0 = na[0], n1 = na[1];
+            n0.nobj = 0;
+            n1.nobj = 0;
+            hipLaunchKernelGGL((sa_narrow_mixed_kernel<1, 1, 2, 1, 1, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st,
+                               na[0], n1, fs);
+            hipLaunchKernelGGL((sa_narrow_mixed_kernel<1, 1, 2, 1, 1, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st,
+                               n0, na[1], FpsSide{});
+#else
             hipLaunchKernelGGL((sa_narrow_mixed_kernel<1, 1, 2, 1, 1, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st,
                                na[0], na[1], fs);
+#endif
         } else if (l == 0) {
             const size_t lds = std::max({narrow_lds(1, 1, 2), narrow_lds(2, 2, 4), fps_side_lds(fs)});
             hipLaunchKernelGGL((sa_narrow_kernel<1, 1, 2, 1, 2, 2, 4, 2>), grid, dim3(SA_THREADS), lds, st, na[0],

@@ -32,6 +32,9 @@ void gp_set_error(const char* fmt, ...) {
 }
 
 int gp_check_launch(const char* what) {
+#ifdef GP_DEBUG_SYNC   // diagnostic builds only: every launch completes before the host continues
+    (void)hipDeviceSynchronize();
+#endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gp_set_error("%s: %s", what, hipGetErrorString(e));

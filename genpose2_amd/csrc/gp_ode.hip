@@ -745,11 +745,14 @@ std::vector<StatusReader> g_status_pool;
 
 struct StatusLease {
     StatusReader r{nullptr, nullptr, -1};
-    int acquire(hipStream_t stream) {
+    hipStream_t stream = nullptr;
+    bool pending = false;   // a status copy into r.pinned was enqueued and may not have landed yet
+    int acquire(hipStream_t s) {
+        stream = s;
         int cur = 0, dev = 0;
         if (hipGetDevice(&cur) != hipSuccess) return -1;
         dev = cur;
-        if (stream != nullptr && hipStreamGetDevice(stream, &dev) != hipSuccess) return -1;
+        if (s != nullptr && hipStreamGetDevice(s, &dev) != hipSuccess) return -1;
         {
             std::lock_guard<std::mutex> lk(g_status_mu);
             for (size_t i = 0; i < g_status_pool.size(); ++i)
@@ -761,16 +764,24 @@ struct StatusLease {
         }
         if (dev != cur && hipSetDevice(dev) != hipSuccess) return -1;
         r.dev = dev;
-        const bool ok = hipHostMalloc(reinterpret_cast<void**>(&r.pinned), 64, hipHostMallocDefault) == hipSuccess &&
-                        hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) == hipSuccess;
+        bool ok = hipHostMalloc(reinterpret_cast<void**>(&r.pinned), 64, hipHostMallocDefault) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) == hipSuccess;
+        if (!ok) {   // a partial creation frees what it made (nothing of it is pooled)
+            if (r.pinned != nullptr) (void)hipHostFree(r.pinned);
+            r.pinned = nullptr;
+            r.ev = nullptr;
+        }
         if (dev != cur) (void)hipSetDevice(cur);
         return ok ? 0 : -1;
     }
     ~StatusLease() {
-        if (r.pinned != nullptr && r.ev != nullptr) {
-            std::lock_guard<std::mutex> lk(g_status_mu);
-            g_status_pool.push_back(r);
-        }
+        if (r.pinned == nullptr || r.ev == nullptr) return;
+        // an early return between the status copy and its wait leaves the copy in flight: it must land
+        // before another call can lease this pinned word (if the stream cannot be drained, the reader is
+        // dropped rather than pooled)
+        if (pending && hipStreamSynchronize(stream) != hipSuccess) return;
+        std::lock_guard<std::mutex> lk(g_status_mu);
+        g_status_pool.push_back(r);
     }
 };
 }  // namespace
@@ -862,10 +873,12 @@ extern "C" int gp_ode_sample(const gp_head_weights* w, const float* pobj, const 
         GP_REQUIRE(a < 100000, "ode_sample: attempt limit reached");
         if ((rc = launch(a + 1, 1))) return rc;   // decides attempt a, prepares a + 1
         const char* src = static_cast<const char*>(aws) + ((a + 2) & 1) * rec + stat_off;
+        status.pending = true;
         GP_REQUIRE(hipMemcpyAsync(status.r.pinned, src, 4, hipMemcpyDeviceToHost, stream) == hipSuccess &&
                        hipEventRecord(status.r.ev, stream) == hipSuccess, "ode_sample: status read");
         if ((rc = launch(a + 1, 2))) return rc;   // attempt a + 1 (a no-op once the solve has ended)
         GP_REQUIRE(hipEventSynchronize(status.r.ev) == hipSuccess, "ode_sample: status wait");
+        status.pending = false;
         if (*status.r.pinned != 0) break;
     }
     OdeCtl c;

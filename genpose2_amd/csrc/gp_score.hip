@@ -107,12 +107,19 @@ __global__ __launch_bounds__(EVAL_WV * 64) void head_eval_kernel(gp_head_weights
             if (r0 + c < rows) out[(size_t)(r0 + c) * 9 + o] = fdiv(head_out(sm, c, o), fadd(sigma, 1e-7f));
         }
     } else {
+        // energy = [sum_{o<6} pose_o * s_o, sum_{o>=6} pose_o * s_o] with s = f / sigma (energynet.py:175-193):
+        // each product rounded on its own (no contraction), summed in the order torch's CPU sum takes over a
+        // contiguous row -- ((((p0 + p4) + p5) + p1) + p2) + p3 for the six rotation entries, (p6 + p7) + p8
+        // for the translation (checked against torch.sum on 200k random rows) -- so rows whose energies tie
+        // to the last bits in the reference rank as they do there
         if (threadIdx.x < 32) {
             const int c = threadIdx.x >> 1, part = threadIdx.x & 1;
             if (r0 + c < rows) {
-                const int lo = part ? 6 : 0, hi = part ? 9 : 6;
-                float e = 0.f;
-                for (int o = lo; o < hi; ++o) e += sm.xin[c * 16 + o] * fdiv(head_out(sm, c, o), sigma);
+                float p[9];
+#pragma unroll
+                for (int o = 0; o < 9; ++o) p[o] = fmul(sm.xin[c * 16 + o], fdiv(head_out(sm, c, o), sigma));
+                const float e = part ? fadd(fadd(p[6], p[7]), p[8])
+                                     : fadd(fadd(fadd(fadd(fadd(p[0], p[4]), p[5]), p[1]), p[2]), p[3]);
                 out[(size_t)(r0 + c) * 2 + part] = e;
             }
         }

@@ -79,14 +79,15 @@ def initial_step(be, t0: float, tf: float, direction):
 
 
 def rk45_drive(be, t0: float, t_bound: float, rtol: float = 1e-5, atol: float = 1e-5,
-               t_eval: Optional[np.ndarray] = None, keep_all: bool = True):
+               t_eval: Optional[np.ndarray] = None, keep_all: bool = True, trace: Optional[list] = None):
     """solve_ivp(fun, (t0, t_bound), y0, method="RK45", rtol, atol, t_eval) over backend `be`.
 
     `be` holds y0 and provides: set_t_eval, rhs0(t), init_norms(), rhs_euler(t, h), diff_norm(),
     attempt(t, h) -> error norm, dense(t_old, t, lo, hi), accept(t_old, t), keep_y(keep, first).
     Returns (ts, nfev, status); the outputs stay in the backend (``be.ys`` for t_eval=None, the
     dense rows otherwise). With keep_all=False
-    only the final output is kept (the value ``res.y[:, -1]`` that pred_func uses).
+    only the final output is kept (the value ``res.y[:, -1]`` that pred_func uses). ``trace``: a list that
+    receives [t, h, error norm] per step attempt (scipy's _estimate_error_norm; accepted iff norm < 1).
     """
     t0, tf = map(float, (t0, t_bound))                          # ivp.py: t0, tf = map(float, t_span)
     direction = np.sign(tf - t0) if tf != t0 else 1             # base.py OdeSolver.__init__
@@ -129,6 +130,8 @@ def rk45_drive(be, t0: float, t_bound: float, rtol: float = 1e-5, atol: float = 
             h_abs = np.abs(h)
             error_norm = be.attempt(t, h)
             nfev += N_STAGES
+            if trace is not None:
+                trace.append([float(t), float(h), float(error_norm)])
             if error_norm < 1:
                 if error_norm == 0:
                     factor = MAX_FACTOR

@@ -288,13 +288,15 @@ def test_pc_f16x3_matches_exact_f32(B, T):
     at the PC golden tests' tolerances (1e-4 rotation, 1e-5 relative translation). 800 rows run
     16-candidate tiles; 4800 rows (> PC_SPLIT_NT2_MIN = 4096) run the f16x3 path's 32-candidate
     tiles against the fp32 path's 16-candidate tiles. The two differ only in how fp32 products are
-    accumulated, which the Langevin trajectories amplify unevenly: 99.9 % of candidates stay within
-    1e-4, the worst of 4800 within 3e-4. The bar against the reference itself is
+    accumulated, which the Langevin trajectories amplify unevenly (measured on the round-4 build: p99.9
+    1.7e-5 / 2.4e-5, max 2.3e-5 / 2.5e-5). The bar, 5e-5 at p99.9 and 1e-4 at the worst candidate, is
+    about 2x the measured spread, so the test holds the f16x3 accuracy claim rather than the old split-f16 bar
+    (p99.9 < 1e-4, max < 3e-4). The bar against the reference itself is
     test_pc_large_rows_vs_reference."""
     p, ref = _f16x3_vs_f32(B, T)
     err = np.abs(p[..., :6] - ref[..., :6]).max(-1)
     print(f"B={B} T={T}: f16x3 vs exact fp32 rotation p99.9 {np.quantile(err, 0.999):.2e} max {err.max():.2e}")
-    assert np.quantile(err, 0.999) < 1e-4 and err.max() < 3e-4, (np.quantile(err, 0.999), err.max())
+    assert np.quantile(err, 0.999) < 5e-5 and err.max() < 1e-4, (np.quantile(err, 0.999), err.max())
     assert rel(p[..., 6:], ref[..., 6:]) < 1e-5
     assert not np.array_equal(p, ref)   # the two paths really differ in arithmetic
 
@@ -350,13 +352,15 @@ def test_ode_large_rows_vs_reference(name, arith):
 
 
 # ---------------------------------------------------------------- ODE sampler
-@pytest.mark.parametrize("tag,rot_tol,tr_rel", [("t055_s20", 1e-4, 1e-5), ("t1_none", 5e-4, 1e-4)])
-def test_ode_pred_func_vs_golden(tag, rot_tol, tr_rel):
+def test_ode_pred_func_vs_golden():
+    """The shipped setting (T0=0.55, t_eval of 20 steps): identical nfev, final pose within the north-star
+    1e-4 / 1e-5, and the whole returned trajectory (return_process, host controller) within the same bar."""
     from genpose2_amd.agent import NoiseFeed, PoseNet
     from genpose2_amd.config import GenPoseConfig
     g = golden("ode")
+    tag, rot_tol, tr_rel = "t055_s20", 1e-4, 1e-5
     steps = int(g[f"{tag}_steps"])
-    agent = PoseNet(GenPoseConfig(device=DEV, sampler_mode=["ode"], sampling_steps=None if steps < 0 else steps))
+    agent = PoseNet(GenPoseConfig(device=DEV, sampler_mode=["ode"], sampling_steps=steps))
     agent.noise_feed = NoiseFeed(torch.from_numpy(g[f"{tag}_prior"]))
     data = {"pts": torch.from_numpy(g[f"{tag}_pts"]).to(DEV),
             "pts_center": torch.from_numpy(g[f"{tag}_pts_center"]).to(DEV)}
@@ -367,37 +371,84 @@ def test_ode_pred_func_vs_golden(tag, rot_tol, tr_rel):
     assert np.abs(p[..., :6] - ref[..., :6]).max() < rot_tol
     assert rel(p[..., 6:], ref[..., 6:]) < tr_rel
     assert np.abs(q.cpu().numpy()[..., :4] - g[f"{tag}_pred_q"][..., :4]).max() < rot_tol * 10
-    if tag == "t055_s20":   # the shipped T0; at T0=1 the controller may branch on ~1e-7 score differences
-        assert agent.last_nfev == int(g[f"{tag}_nfev"])
-    # return_process: the whole trajectory (solve_ivp outputs, GS'ed, + pts_center)
+    assert agent.last_nfev == int(g[f"{tag}_nfev"])
+    # return_process: the whole trajectory (solve_ivp outputs, GS'ed, + pts_center) from the host controller
+    # (device pow() vs glibc: last-bit scalar differences, which agree to 1e-6 at this T0)
     nfev_dev = agent.last_nfev
     agent.noise_feed = NoiseFeed(torch.from_numpy(g[f"{tag}_prior"]))
     pose2, xs = agent.pred_func(data, repeat_num=5, T0=float(g[f"{tag}_T0"]), return_process=True)
-    # return_process runs the host controller (device pow() vs glibc: last-bit scalar differences). At the
-    # shipped T0=0.55 the two agree to 1e-6. At T0=1 the adaptive path amplifies those last bits (the
-    # oracle, running scipy itself, is 1.3e-4 from the reference there), so the host-controlled result is
-    # held to the same golden bar as the device one
-    if tag == "t055_s20":
-        assert agent.last_nfev == nfev_dev
-        assert (pose2 - pose).abs().max().item() < 1e-6 * max(1.0, pose.abs().max().item())
-    else:
-        p2 = pose2.cpu().numpy()
-        assert np.abs(p2[..., :6] - ref[..., :6]).max() < rot_tol and rel(p2[..., 6:], ref[..., 6:]) < tr_rel
+    assert agent.last_nfev == nfev_dev
+    assert (pose2 - pose).abs().max().item() < 1e-6 * max(1.0, pose.abs().max().item())
     xr = g[f"{tag}_xs"]
-    if agent.last_nfev == int(g[f"{tag}_nfev"]):
-        assert xs.shape == xr.shape
-        x = xs.cpu().numpy()
-        # t_eval unset (T0=1): xs are the states at solve_ivp's own accepted step times, which move with the
-        # last bits of every error norm even at equal nfev, so the intermediate states are compared to the
-        # reference's at slightly different t (measured 1.1e-3 rotation / 3.1e-4 relative translation with the
-        # f16x3 head GEMMs, 3.6e-4 rotation with the round-3 split-f16 ones); the final state is held to the
-        # golden bar
-        mid_tol, mid_rel = (rot_tol, tr_rel) if tag == "t055_s20" else (3e-3, 1e-3)
-        err = np.abs(x[..., :6] - xr[..., :6])
-        print(f"{tag}: xs rotation max {err.max():.2e} (final state {err[..., -1, :].max():.2e}), translation rel "
-              f"{rel(x[..., 6:], xr[..., 6:]):.2e} (final state {rel(x[..., -1, 6:], xr[..., -1, 6:]):.2e})")
-        assert err.max() < mid_tol and err[..., -1, :].max() < rot_tol
-        assert rel(x[..., 6:], xr[..., 6:]) < mid_rel and rel(x[..., -1, 6:], xr[..., -1, 6:]) < tr_rel
+    assert xs.shape == xr.shape
+    x = xs.cpu().numpy()
+    err = np.abs(x[..., :6] - xr[..., :6])
+    print(f"{tag}: xs rotation max {err.max():.2e}, translation rel {rel(x[..., 6:], xr[..., 6:]):.2e}")
+    assert err.max() < rot_tol and rel(x[..., 6:], xr[..., 6:]) < tr_rel
+
+
+@pytest.mark.parametrize("arith", ARITHS)
+def test_ode_t1_calibrated_vs_float64(arith):
+    """T0=1 with t_eval unset (golden_ode "t1_none"). RK45 at rtol=atol=1e-5 from sigma(1)=50 lets the
+    float32 rounding of the score steer its accept/reject path: the reference itself takes 290 evaluations
+    with its float32 network and 278 with the same network in float64, and the two trajectories part by
+    1.4e-4 in rotation (golden_ode_trace.json, golden_ode_t1_grid.npz; tests/golden/make_ode_trace.py). So
+    this case is held to the calibrated bar, like the large PC fixtures: against the reference's float64 run,
+    the final pose and the whole trajectory -- compared on a fixed grid of 101 times through the t_eval
+    output, which RK45 interpolates without changing its steps -- within 2x the reference float32 run's own
+    error (rotation max, translation max relative). nfev and the first attempt where the controller parts
+    from the reference's float32 run are printed for the record."""
+    import json
+    from conftest import GOLDEN
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("ode")
+    cal = np.load(f"{GOLDEN}/golden_ode_t1_grid.npz")
+    with open(f"{GOLDEN}/golden_ode_trace.json") as f:
+        ref_trace = json.load(f)["t1_none"]["ref32"]["attempts"]
+    tag = "t1_none"
+    data = {"pts": torch.from_numpy(g[f"{tag}_pts"]).to(DEV),
+            "pts_center": torch.from_numpy(g[f"{tag}_pts_center"]).to(DEV)}
+    # final pose (t_eval unset: denoise step (1 - eps) / 1000), device controller and host controller
+    agent = PoseNet(GenPoseConfig(device=DEV, sampler_mode=["ode"], sampling_steps=None))
+    set_arith(agent, arith)
+    agent.noise_feed = NoiseFeed(torch.from_numpy(g[f"{tag}_prior"]))
+    pose = agent.pred_func(dict(data), repeat_num=5, T0=1.0)[0].cpu().numpy()
+    nfev = agent.last_nfev
+    trace = []
+    agent.ode_trace = trace
+    agent.noise_feed = NoiseFeed(torch.from_numpy(g[f"{tag}_prior"]))
+    pose_h = agent.pred_func(dict(data), repeat_num=5, T0=1.0)[0].cpu().numpy()
+    agent.ode_trace = None
+    assert agent.last_nfev == nfev
+    ref32, ref64 = g[f"{tag}_pred_pose"], cal["pred_pose64"]
+
+    def errs(a, b):
+        return float(np.abs(a[..., :6] - b[..., :6]).max()), rel(a[..., 6:], b[..., 6:])
+    r_rot, r_tr = errs(ref32, ref64)
+    o_rot, o_tr = errs(pose, ref64)
+    h_rot, h_tr = errs(pose_h, ref64)
+    part = next((i for i, (a, b) in enumerate(zip(trace, ref_trace)) if (a[2] < 1) != (b[2] < 1)), None)
+    print(f"t1_none {arith}: nfev {nfev} (reference fp32 {int(cal['nfev32'])}, float64 {int(cal['nfev64'])}); "
+          f"first accept/reject decision differing from the reference fp32 run: attempt {part} "
+          f"({trace[part] if part is not None else None} vs {ref_trace[part] if part is not None else None}); "
+          f"final pose vs float64: rotation {o_rot:.2e} (host controller {h_rot:.2e}), translation rel {o_tr:.2e} "
+          f"(reference fp32 {r_rot:.2e} / {r_tr:.2e}); vs reference fp32 rotation {errs(pose, ref32)[0]:.2e}")
+    assert o_rot <= 2 * r_rot and o_tr <= 2 * r_tr
+    assert h_rot <= 2 * r_rot and h_tr <= 2 * r_tr
+    # the trajectory on the grid
+    agent = PoseNet(GenPoseConfig(device=DEV, sampler_mode=["ode"], sampling_steps=len(cal["grid"])))
+    set_arith(agent, arith)
+    agent.noise_feed = NoiseFeed(torch.from_numpy(g[f"{tag}_prior"]))
+    _, xs = agent.pred_func(dict(data), repeat_num=5, T0=1.0, return_process=True)
+    assert agent.last_nfev == nfev    # t_eval interpolates; the steps are those of the run above
+    x = xs.cpu().numpy()
+    assert x.shape == cal["xs64"].shape
+    x_rot, x_tr = errs(x, cal["xs64"])
+    rx_rot, rx_tr = errs(cal["xs32"], cal["xs64"])
+    print(f"t1_none {arith}: trajectory on the grid vs float64: rotation {x_rot:.2e}, translation rel {x_tr:.2e} "
+          f"(reference fp32 {rx_rot:.2e} / {rx_tr:.2e}); vs reference fp32 rotation {errs(x, cal['xs32'])[0]:.2e}")
+    assert x_rot <= 2 * rx_rot and x_tr <= 2 * rx_tr
 
 
 @pytest.mark.parametrize("tag", ["t055_s20", "t1_none"])
