@@ -1859,12 +1859,18 @@ extern "C" int gp_encoder_forward(const float* wbuf, const int64_t* layer_off, c
     GP_REQUIRE(feat, "encoder_forward: null feat");
     const EncCtx c = enc_ctx(wbuf, layer_off, pts, B, N, workspace);
     // FPS level 0 here; levels 1-3 run beside the level-0 / level-1 MLP launches (FpsSide)
+#ifdef GP_NO_FPS_SIDE   // diagnostic builds only: the whole FPS chain up front, no FPS workgroups beside the MLPs
+    rc = gp_launch_fps_chain(pts, B, 4, c.nin, c.mout, (int* const*)c.fidx, (float* const*)c.nxyz, st);
+    constexpr bool side = false;
+#else
     rc = gp_launch_fps_chain(pts, B, 1, c.nin, c.mout, (int* const*)c.fidx, (float* const*)c.nxyz, st);
+    constexpr bool side = true;
+#endif
     if (rc) return rc;
     for (int l = 0; l < 5; ++l) {
         const float* fprev = l == 0 ? nullptr : reinterpret_cast<const float*>(c.ws + c.L.feat[l - 1]);
         float* out = l < 4 ? reinterpret_cast<float*>(c.ws + c.L.feat[l]) : feat;
-        rc = run_sa_level(c, l, l == 0 ? 0 : kCout[l - 1], fprev, out, true, st);
+        rc = run_sa_level(c, l, l == 0 ? 0 : kCout[l - 1], fprev, out, side, st);
         if (rc) return rc;
     }
     return GP_OK;

@@ -30,6 +30,15 @@ constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
 #endif
 
 
+// The thread id behind an opaque copy: per-lane values derived from it are computed where they are used and
+// cannot be hoisted out of an enclosing loop (the persistent PC sampler runs the trunk once per step; hoisted
+// lane addresses stayed live across every trunk and were spilled, their reloads draining the weight ring)
+__device__ __forceinline__ int tid_x() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // ============================================================================ shared head trunk
 // NT = column tiles (16 candidates each) per workgroup. PL = 0: the exact-fp32 trunk's activations
 // (fp32, accumulator-native); PL = 3: the f16x3 trunk's (three f16 planes per value, 6 B).
@@ -371,8 +380,9 @@ struct SplitScalars {
 __device__ __forceinline__ SplitScalars load_split_scalars(const gp_head_weights& w) {
     const f32x4 a = ld4(w.hsc), b = ld4(w.hsc + 4);
     SplitScalars r{a.x, a.y, a.z, a.w, (int)b.x, (int)b.y, {}, {}};
-    const int lane = threadIdx.x & 63, q = lane >> 4;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tid = tid_x();
+    const int lane = tid & 63, q = lane >> 4;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
     for (int t = 0; t < 16 / HSPLIT_WV; ++t) {
         const int T = wid * (16 / HSPLIT_WV) + t;
@@ -727,8 +737,9 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
     static_assert(WV == HSPLIT_WV, "SplitScalars carries the pose_encoder.0 fragments of HSPLIT_WV waves");
     constexpr int CPW = TPW / 2;
     using SM = HeadSmem<NT, WV, X3P>;
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tid = tid_x();
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = lane >> 4, n = lane & 15;
     const int voff = lane * 16;
     const __amdgpu_buffer_rsrc_t W2 = make_rsrc(w.pe2_h, HID * HID * 2 * X3P);

@@ -23,6 +23,10 @@
 
 #include "gp_common.h"
 
+#include <cstring>
+#include <mutex>
+#include <vector>
+
 // Phase timestamps for tuning builds only (make EXTRA=-DPC_TRACE; read by scripts/pc_trace.py).
 #ifdef PC_TRACE
 __device__ unsigned long long g_pc_trace[2 * 256 * 8 * 16];
@@ -178,6 +182,163 @@ struct PCArgs {
     float ls_coef;        // snr * sqrt(pose_dim)
 };
 
+// One update wave's part of step i-1 -> i for its 16 rows (wave g owns rows 16g .. 16g+15, four lanes per row:
+// part p < 3 owns elements [3p, 3p+3) -- rot6 columns a1, a2, translation; lane 4c+3 only pads the row).
+// gacc: the lane's share of sum_r ||s_r|| over every row of step i-1, summed by the caller in the fixed
+// lane / index order both kernels share, so every workgroup derives the identical grad_norm. x3: this lane's
+// entries of x (updated in place); sv, z1v, z2v: its entries of the previous score and the two draws.
+// Writes xin (the trunk's input), the split trunk's per-column scales, obj, and the outputs (x when store_x,
+// the trajectory, res / q at the last step).
+template <int NT, int WV, int PL>
+__device__ __forceinline__ void pc_update_rows(const PCArgs& a, int i, const PCStep& prev, HeadSmem<NT, WV, PL>& sm,
+                                               int* obj, int g, int lane, int r0, float gacc, float (&x3)[3],
+                                               const float (&sv)[3], const float (&z1v)[3], const float (&z2v)[3],
+                                               const SplitScalars& hs, bool store_x, int trace_slot) {
+#pragma clang fp contract(off)
+    constexpr bool SPLIT = PL != 0;
+    const int p = lane & 3;
+    const int e0 = 3 * (p < 3 ? p : 0);
+    if (lane < 16) {
+        const int r = r0 + 16 * g + lane;
+        obj[16 * g + lane] = (r < a.rows ? r : a.rows - 1) / a.kper;
+    }
+    PC_MARK(10);
+    gacc = wave_sum(gacc);
+    PC_MARK(11);
+    const int c = 16 * g + (lane >> 2);
+    const int r = r0 + c;
+    const bool upd = i > 0 && r < a.rows && p < 3;
+    if (upd) {
+        const float gn = udiv(gacc, (float)a.rows);
+        const float ratio = udiv(a.ls_coef, gn);
+        const float ls = 2.0f * (ratio * ratio);
+        const float sq2ls = usqrt(2.0f * ls);
+        float mean[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) x3[k] = (x3[k] + ls * sv[k]) + sq2ls * z1v[k];
+        if (p < 2) {   // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
+            const float nn = usqrt((x3[0] * x3[0] + x3[1] * x3[1]) + x3[2] * x3[2]);
+            x3[0] = udiv(x3[0], nn); x3[1] = udiv(x3[1], nn); x3[2] = udiv(x3[2], nn);
+        }
+        // reverse-SDE Euler-Maruyama predictor (samplers.py:163-166; sign as in the reference)
+        const float g2 = prev.g * prev.g;
+        const float gs = prev.g * prev.sqrt_dt;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float drift = 0.0f - g2 * sv[k];
+            mean[k] = x3[k] + drift * prev.dt;
+            x3[k] = mean[k] + gs * z2v[k];
+        }
+        gram_schmidt6_quad(x3, p, lane);
+        const float* cen = a.center + (size_t)(r / a.kper) * 3;
+        if (a.xs) {
+            float* o = a.xs + ((size_t)r * a.steps + (i - 1)) * 9 + e0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) o[k] = p == 2 ? x3[k] + cen[k] : x3[k];
+        }
+        if (i == a.steps) {  // res = mean_x of the last step (+centre, GS), samplers.py:174-177
+            if (p == 2) {
+                mean[0] += cen[0];
+                mean[1] += cen[1];
+                mean[2] += cen[2];
+            }
+            gram_schmidt6_quad(mean, p, lane);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                a.res[(size_t)r * 9 + e0 + k] = mean[k];
+                sm.xu[c * 9 + e0 + k] = mean[k];   // gathered below for the quaternion
+            }
+        }
+        if (store_x || i == a.steps) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.x[(size_t)r * 9 + e0 + k] = x3[k];
+        }
+    }
+    if (i == a.steps) {
+        wave_sync();
+        if (p == 0 && r < a.rows) {
+            float m9[9], qq[4];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) m9[j] = sm.xu[c * 9 + j];
+            quat_from_gs<float>(m9, qq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a.q[(size_t)r * 7 + j] = qq[j];
+            a.q[(size_t)r * 7 + 4] = m9[6];
+            a.q[(size_t)r * 7 + 5] = m9[7];
+            a.q[(size_t)r * 7 + 6] = m9[8];
+        }
+    }
+    if (p < 3) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sm.xin[c * 16 + e0 + k] = (r < a.rows) ? x3[k] : 0.f;
+    } else {
+#pragma unroll
+        for (int j = 9; j < 16; ++j) sm.xin[c * 16 + j] = 0.f;
+    }
+    if constexpr (SPLIT) {
+        // this row's split-trunk scales, from the entries just written to xin (max |x| over the row's four
+        // lanes by DPP), once here instead of in all eight waves of the trunk
+        float m = (p < 3 && r < a.rows) ? fmaxf(fmaxf(fabsf(x3[0]), fabsf(x3[1])), fabsf(x3[2])) : 0.f;
+        m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, true)));
+        m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, true)));
+        if (p == 0) {
+            const ColScales cs = split_col_scales(m, hs);
+            sm.cscl[c][0] = f32x4{cs.s1, cs.s2, cs.u2, cs.uh};
+            sm.cscl[c][1] = f32x4{cs.sh, 0.f, 0.f, 0.f};
+        }
+    }
+}
+
+// Draws for the update of step i (applied one launch / iteration later), made while waves 0..NT-1 update:
+// 2 streams x 3 blocks of 4 normals per row, streams 2i (corrector) and 2i+1 (predictor). dst(st, r, e)
+// receives normal e < 9 of stream st for row r.
+template <int NT, int WV, typename Dst>
+__device__ __forceinline__ void pc_make_draws(const PCArgs& a, int i, int r0, Dst dst) {
+    constexpr int ROWS = NT * 16;
+    for (int e = tid_x() - 64 * NT; e < ROWS * 6; e += (WV - NT) * 64) {
+        const int c = e / 6, st = (e - c * 6) / 3, blk = e - c * 6 - st * 3;
+        const int r = r0 + c;
+        if (r < a.rows) {
+            const f32x4 v = philox_normal4(a.seed, (uint32_t)(st + 2 * i), (uint32_t)r, (uint32_t)blk);
+            dst(st, c, blk * 4 + 0, v.x);
+            if (blk < 2) {
+                dst(st, c, blk * 4 + 1, v.y);
+                dst(st, c, blk * 4 + 2, v.z);
+                dst(st, c, blk * 4 + 3, v.w);
+            }
+        }
+    }
+}
+
+// s = f / (sigma + 1e-7) for the workgroup's rows (a lane per (row, output): 4 rows per wave as 16-lane rows,
+// outputs 0..8 valid, row norms by a DPP row sum) handed to put(c, o, s); the waves' partials of sum_r ||s_r||
+// combined in wave order after one barrier. Returns the workgroup partial (valid in thread 0).
+template <int NT, int WV, int PL, typename Put>
+__device__ __forceinline__ float pc_score_norm(const PCArgs& a, const PCStep& cur, HeadSmem<NT, WV, PL>& sm, int r0,
+                                               int wid, int lane, Put put) {
+    constexpr int ROWS = NT * 16;
+    const float den = fadd(cur.sigma, 1e-7f);
+    float wsum = 0.f;
+    for (int cg = wid; cg < ROWS / 4; cg += WV) {
+        const int c = 4 * cg + (lane >> 4), o = lane & 15;
+        const int r = r0 + c;
+        float v = 0.f;
+        if (o < 9 && r < a.rows) {
+            v = fdiv(head_out(sm, c, o), den);
+            put(c, o, v);
+        }
+        wsum += rows_sum(sqrtf(row16_sum(fmul(v, v))));
+    }
+    if (lane == 0) sm.scratch[wid] = wsum;
+    __syncthreads();
+    float t = 0.f;
+    if (wid == 0 && lane == 0) {
+#pragma unroll
+        for (int v = 0; v < WV; ++v) t += sm.scratch[v];
+    }
+    return t;
+}
+
 // Launch i in [0, steps]: finish step i-1 (if i > 0), then score at step i (if i < steps).
 // Waves 0..NT-1 run the update, one 16-row column tile each (their global loads, the draws and the
 // grad-norm reduction overlap), while the other waves make the next step's draws, stage the small
@@ -201,8 +362,6 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
         // ---- every load first and unconditional (rows clamped: a guarded load becomes a branch,
         //      and the compiler then drains the first batch before issuing the next): the
         //      grad-norm partials of step i-1, then this lane's elements of x, s and the two draws.
-        //      Four lanes per row: part p < 3 owns elements [3p, 3p+3) (rot6 columns a1, a2,
-        //      translation); lane 4c+3 only pads the row. Wave g owns rows 16g .. 16g+15.
         const int g = wid;
         const bool inj = a.z1 != nullptr;
         const float* zslot = a.zbuf + (size_t)((i - 1) & 1) * 2 * a.rows * 9;
@@ -225,9 +384,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
                 z2v[k] = z2p[e + k];
             }
         }
-        // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); the same lane
-        // order and xor tree in every wave of every workgroup, so all derive the identical value
-        // (unused at i=0)
+        // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); unused at i=0
         float gacc = 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u) gacc += lane + 64 * u < a.nwg ? pv[u] : 0.f;
@@ -238,147 +395,189 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             for (int u = 0; u < 8; ++u) gacc += t0 + lane + 64 * u < a.nwg ? pv[u] : 0.f;
         }
         PC_MARK(9);
-        if (lane < 16) {
-            const int r = r0 + 16 * g + lane;
-            obj[16 * g + lane] = (r < a.rows ? r : a.rows - 1) / a.kper;
-        }
-        PC_MARK(10);
-        gacc = wave_sum(gacc);
-        PC_MARK(11);
-        {
-#pragma clang fp contract(off)
-            const int c = 16 * g + (lane >> 2);
-            const int r = r0 + c;
-            const bool upd = i > 0 && r < a.rows && p < 3;
-            if (upd) {
-                const float gn = udiv(gacc, (float)a.rows);
-                const float ratio = udiv(a.ls_coef, gn);
-                const float ls = 2.0f * (ratio * ratio);
-                const float sq2ls = usqrt(2.0f * ls);
-                float mean[3];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) x3[k] = (x3[k] + ls * sv[k]) + sq2ls * z1v[k];
-                if (p < 2) {   // x[:, :3] /= ||x[:, :3]||, x[:, 3:6] /= ||x[:, 3:6]|| (samplers.py:157-160)
-                    const float nn = usqrt((x3[0] * x3[0] + x3[1] * x3[1]) + x3[2] * x3[2]);
-                    x3[0] = udiv(x3[0], nn); x3[1] = udiv(x3[1], nn); x3[2] = udiv(x3[2], nn);
-                }
-                // reverse-SDE Euler-Maruyama predictor (samplers.py:163-166; sign as in the reference)
-                const float g2 = prev.g * prev.g;
-                const float gs = prev.g * prev.sqrt_dt;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float drift = 0.0f - g2 * sv[k];
-                    mean[k] = x3[k] + drift * prev.dt;
-                    x3[k] = mean[k] + gs * z2v[k];
-                }
-                gram_schmidt6_quad(x3, p, lane);
-                const float* cen = a.center + (size_t)(r / a.kper) * 3;
-                if (a.xs) {
-                    float* o = a.xs + ((size_t)r * a.steps + (i - 1)) * 9 + e0;
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) o[k] = p == 2 ? x3[k] + cen[k] : x3[k];
-                }
-                if (i == a.steps) {  // res = mean_x of the last step (+centre, GS), samplers.py:174-177
-                    if (p == 2) {
-                        mean[0] += cen[0];
-                        mean[1] += cen[1];
-                        mean[2] += cen[2];
-                    }
-                    gram_schmidt6_quad(mean, p, lane);
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        a.res[(size_t)r * 9 + e0 + k] = mean[k];
-                        sm.xu[c * 9 + e0 + k] = mean[k];   // gathered below for the quaternion
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < 3; ++k) a.x[(size_t)r * 9 + e0 + k] = x3[k];
-            }
-            if (i == a.steps) {
-                wave_sync();
-                if (p == 0 && r < a.rows) {
-                    float m9[9], qq[4];
-#pragma unroll
-                    for (int j = 0; j < 9; ++j) m9[j] = sm.xu[c * 9 + j];
-                    quat_from_gs<float>(m9, qq);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) a.q[(size_t)r * 7 + j] = qq[j];
-                    a.q[(size_t)r * 7 + 4] = m9[6];
-                    a.q[(size_t)r * 7 + 5] = m9[7];
-                    a.q[(size_t)r * 7 + 6] = m9[8];
-                }
-            }
-            if (p < 3) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) sm.xin[c * 16 + e0 + k] = (r < a.rows) ? x3[k] : 0.f;
-            } else {
-#pragma unroll
-                for (int j = 9; j < 16; ++j) sm.xin[c * 16 + j] = 0.f;
-            }
-            if constexpr (SPLIT) {
-                // this row's split-trunk scales, from the entries just written to xin (max |x| over the
-                // row's four lanes by DPP), once here instead of in all eight waves of the trunk
-                float m = (p < 3 && r < a.rows) ? fmaxf(fmaxf(fabsf(x3[0]), fabsf(x3[1])), fabsf(x3[2])) : 0.f;
-                m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, true)));
-                m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, true)));
-                if (p == 0) {
-                    const ColScales cs = split_col_scales(m, hs);
-                    sm.cscl[c][0] = f32x4{cs.s1, cs.s2, cs.u2, cs.uh};
-                    sm.cscl[c][1] = f32x4{cs.sh, 0.f, 0.f, 0.f};
-                }
-            }
-        }
+        pc_update_rows<NT, WV, PL>(a, i, prev, sm, obj, g, lane, r0, gacc, x3, sv, z1v, z2v, hs, true, trace_slot);
         PC_MARK(12);
     }
     if (i == a.steps) return;  // finalize launch: no score evaluation
-    if (wid >= NT && a.z1 == nullptr) {
-        // draws for the update of step i (applied by launch i+1), made while waves 0..NT-1 update:
-        // 2 streams x 3 blocks of 4 normals per row, streams 2i (corrector) and 2i+1 (predictor)
-        for (int e = tid - 64 * NT; e < ROWS * 6; e += (WV - NT) * 64) {
-            const int c = e / 6, st = (e - c * 6) / 3, blk = e - c * 6 - st * 3;
-            const int r = r0 + c;
-            if (r < a.rows) {
-                const f32x4 v = philox_normal4(a.seed, (uint32_t)(st + 2 * i), (uint32_t)r, (uint32_t)blk);
-                float* dst = a.zbuf + ((size_t)((i & 1) * 2 + st) * a.rows + r) * 9 + blk * 4;
-                dst[0] = v.x;
-                if (blk < 2) {
-                    dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
-                }
-            }
-        }
-    }
+    if (wid >= NT && a.z1 == nullptr)
+        pc_make_draws<NT, WV>(a, i, r0, [&](int st, int c, int e, float v) {
+            a.zbuf[((size_t)((i & 1) * 2 + st) * a.rows + r0 + c) * 9 + e] = v;
+        });
     stage_small_weights<NT, WV, 64 * NT, !SPLIT>(a.w, sm);
     if constexpr (SPLIT)
         head_trunk_x3<NT, WV, true>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
     else
         head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
     PC_MARK(7);
-    // ---- s = f / (sigma + 1e-7); workgroup partial of sum_r ||s_r||. A lane per (row, output):
-    //      4 rows per wave as 16-lane rows (outputs 0..8 valid), row norms by a DPP row sum, the
-    //      waves' partials combined in wave order after one barrier
-    {
-        const float den = fadd(cur.sigma, 1e-7f);
-        float wsum = 0.f;
-        for (int cg = wid; cg < ROWS / 4; cg += WV) {
-            const int c = 4 * cg + (lane >> 4), o = lane & 15;
-            const int r = r0 + c;
-            float v = 0.f;
-            if (o < 9 && r < a.rows) {
-                v = fdiv(head_out(sm, c, o), den);
-                a.s[(size_t)r * 9 + o] = v;
-            }
-            wsum += rows_sum(sqrtf(row16_sum(fmul(v, v))));
-        }
-        if (lane == 0) sm.scratch[wid] = wsum;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        float t = 0.f;
-#pragma unroll
-        for (int v = 0; v < WV; ++v) t += sm.scratch[v];
-        a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = t;
-    }
+    const float t = pc_score_norm<NT, WV, PL>(a, cur, sm, r0, wid, lane,
+                                              [&](int c, int o, float v) { a.s[(size_t)(r0 + c) * 9 + o] = v; });
+    if (tid == 0) a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = t;
     PC_MARK(8);
+}
+
+// ============================================================================ persistent PC sampler
+// The whole T-step loop in one launch: each workgroup keeps its rows for every step, so x stays in the
+// update waves' registers, s and the next step's draws in LDS, the weight planes stay resident in each
+// XCD's L2 across steps (a kernel boundary writes back and invalidates it: 17.8 MB of fabric traffic per
+// launch for 0.92 MB of state), and the per-launch staging disappears. The grid-wide dependency of a
+// step -- grad_norm, the mean score norm over all rows (samplers.py:143) -- becomes an all-gather of one
+// 8-byte granule per workgroup {partial's bits, step tag}, stored write-through (agent-scope relaxed atomic:
+// global_store_dwordx2 sc1) by one lane after the workgroup's barrier and polled by every update wave
+// with sc1 loads (MI355X_MICROARCH.md, hand-off table row 1 with R2 granules: the payload travels inside
+// the polled word, so no ordering is needed). The granules are double-buffered by step parity: a workgroup
+// can only overwrite slot j&1 (step j+2) after every workgroup published step j+1, i.e. finished polling
+// step j. Every workgroup sums the same granules in the multi-launch kernel's order, so the two kernels
+// agree bit for bit. Requires every workgroup resident at once (gp_pc_sample checks nwg <= CUs; one
+// 64-candidate workgroup per CU by LDS); every wait is bounded: a workgroup that waits ~1 s sets the
+// status word, poisons its rows (NaN) and stops waiting, so a co-residency failure ends as an error and
+// never as a hang.
+struct PCPersist {
+    PCArgs* args;                  // the kernel's arguments (uploaded with the table)
+    const float* tab;              // (steps, 5) step table
+    unsigned long long* gran;      // (2, nwg) granules, zero at launch
+    unsigned* cnt;                 // PC_SHARDS arrival counters, 128 B apart, zero at launch
+    int* status;                   // 0 ok; 1 a wait timed out
+};
+
+#ifndef PC_PERSIST_SPIN
+#define PC_PERSIST_SPIN (1u << 20)   // polls before a wait gives up (each ~1 us + 64 cycles of sleep)
+#endif
+
+// Arrival counters, one per XCD-sized shard (workgroup b counts on shard b % 8: the round-robin dealing puts
+// those workgroups on one XCD, so a shard's adds stay local -- for speed only, correctness does not depend on
+// placement), each on a 128-byte line of its own. A workgroup publishes step j's partial as its granule
+// (write-through store), waits for that store, then adds 1 to its shard: after step j, shard s holds
+// j * (workgroups in s). A waiting wave polls the 8 counters with 8 lanes (32 bytes a round instead of
+// every granule: polling all of them from 800 waves took ~3 TB/s of fabric from the weight streams), then
+// reads the granules once.
+constexpr int PC_SHARDS = 8;
+constexpr int PC_SHARD_STRIDE = 32;   // uint32 words per shard (128 B)
+
+__device__ __forceinline__ void pc_publish(unsigned long long* gran, unsigned* cnt, uint32_t tag, float partial) {
+    __hip_atomic_store(gran + blockIdx.x, ((unsigned long long)tag << 32) | __float_as_uint(partial), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the granule has landed before the arrival counts
+    __hip_atomic_fetch_add(cnt + (blockIdx.x % PC_SHARDS) * PC_SHARD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float pc_gather_norms(const unsigned long long* gran, unsigned* cnt, int nwg, uint32_t tag,
+                                                 int lane, bool& timed_out, int* status) {
+    // arrivals first: lane s < 8 waits for shard s to reach tag * (its workgroup count)
+    const int s = lane < PC_SHARDS ? lane : 0;
+    const unsigned want = (unsigned)(nwg / PC_SHARDS + (s < nwg % PC_SHARDS ? 1 : 0)) * tag;
+    for (uint32_t spin = 0; !timed_out; ++spin) {
+        const unsigned have = __hip_atomic_load(cnt + s * PC_SHARD_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all(have >= want)) break;
+        if (spin >= PC_PERSIST_SPIN) {
+            if (lane == 0) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            timed_out = true;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    // then every granule once, in the multi-launch kernel's lane / index order; a stale tag (not expected
+    // once the counts are complete) is read again
+    float gacc = 0.f;
+    for (int t0 = 0; t0 < nwg; t0 += 512) {
+        float pv[8];
+        for (uint32_t spin = 0;; ++spin) {
+            bool ok = true;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const unsigned long long v = __hip_atomic_load(const_cast<unsigned long long*>(gran) + min(t0 + lane + 64 * u, nwg - 1),
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pv[u] = __uint_as_float((uint32_t)v);
+                ok = ok && (uint32_t)(v >> 32) == tag;
+            }
+            if (__all(ok)) break;
+            if (timed_out || spin >= PC_PERSIST_SPIN) {
+                if (!timed_out && lane == 0) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                timed_out = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) gacc += t0 + lane + 64 * u < nwg ? pv[u] : 0.f;
+    }
+    return timed_out ? __builtin_nanf("") : gacc;
+}
+
+template <int NT, int WV, int PL>
+__global__ __launch_bounds__(WV * 64) void pc_persist_kernel(const PCArgs* __restrict__ args, PCPersist pp) {
+    constexpr int ROWS = NT * 16;
+    static_assert(NT < WV, "at least one wave besides the update waves");
+    __shared__ HeadSmem<NT, WV, PL> sm;
+    constexpr bool SPLIT = PL != 0;
+    __shared__ int obj[ROWS];
+    __shared__ float s_l[ROWS * 9];          // score of the last step, [row][9]
+    __shared__ float z_l[2][2][ROWS * 9];    // draws: [step parity][stream][row][9]
+    const PCArgs& a0 = *args;
+    bool timed_out = false;
+    stage_small_weights<NT, WV, 0, !SPLIT>(a0.w, sm);   // once (published by the trunk's first barrier)
+    const int steps = a0.steps;
+    for (int i = 0; i <= steps; ++i) {
+        // every per-lane and per-wave value is derived again from a laundered thread id each step, so nothing
+        // is hoisted out of the loop and kept live (spilled) across the trunk
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const PCArgs* ap = args;
+        asm volatile("" : "+s"(ap));
+        const PCArgs& a = *ap;
+        const int lane = tid & 63;
+        const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int r0 = blockIdx.x * ROWS;
+        const bool inj = a.z1 != nullptr;
+        const int p = lane & 3;
+        const int e0 = 3 * (p < 3 ? p : 0);
+        const int c_row = 16 * (wid < NT ? wid : 0) + (lane >> 2);              // update waves: this lane's row
+        const int trace_slot = i & 1;
+        PC_MARK(0);
+        SplitScalars hs = {};
+        if constexpr (SPLIT) hs = load_split_scalars(a.w);
+        if (wid < NT) {
+            PCStep prev = {};
+            if (i > 0) {
+                const float* tp = pp.tab + (size_t)(i - 1) * 5;
+                prev = PCStep{tp[0], tp[1], tp[2], tp[3], tp[4]};
+            }
+            // x: from the input at i = 0, then from xin, which holds the update's result for every valid row
+            // (the trunk only reads it), so no register carries it across the trunk
+            float x3[3], sv[3], z1v[3], z2v[3];
+            {
+                const int cc = min(c_row, ROWS - 1);
+                const size_t e = (size_t)min(r0 + c_row, a.rows - 1) * 9 + e0;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) x3[k] = i == 0 ? a.x[e + k] : sm.xin[cc * 16 + e0 + k];
+                const float* z1p = a.z1 + (size_t)(i > 0 ? i - 1 : 0) * a.rows * 9;
+                const float* z2p = a.z2 + (size_t)(i > 0 ? i - 1 : 0) * a.rows * 9;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    sv[k] = s_l[cc * 9 + e0 + k];
+                    z1v[k] = inj ? z1p[e + k] : z_l[(i - 1) & 1][0][cc * 9 + e0 + k];
+                    z2v[k] = inj ? z2p[e + k] : z_l[(i - 1) & 1][1][cc * 9 + e0 + k];
+                }
+            }
+            const float gacc = i > 0 ? pc_gather_norms(pp.gran + (size_t)((i - 1) & 1) * a.nwg, pp.cnt, a.nwg, (uint32_t)i,
+                                                       lane, timed_out, pp.status)
+                                     : 0.f;
+            PC_MARK(9);
+            pc_update_rows<NT, WV, PL>(a, i, prev, sm, obj, wid, lane, r0, gacc, x3, sv, z1v, z2v, hs, false, trace_slot);
+            PC_MARK(12);
+        }
+        if (i == steps) break;
+        const float* tc = pp.tab + (size_t)i * 5;
+        const PCStep cur = PCStep{tc[0], tc[1], tc[2], tc[3], tc[4]};
+        if (wid >= NT && !inj)
+            pc_make_draws<NT, WV>(a, i, r0, [&](int st, int c, int e, float v) { z_l[i & 1][st][c * 9 + e] = v; });
+        if constexpr (SPLIT)
+            head_trunk_x3<NT, WV, true>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
+        else
+            head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
+        PC_MARK(7);
+        const float t = pc_score_norm<NT, WV, PL>(a, cur, sm, r0, wid, lane, [&](int c, int o, float v) { s_l[c * 9 + o] = v; });
+        PC_MARK(8);
+        if (tid == 0) pc_publish(pp.gran + (size_t)(i & 1) * a.nwg, pp.cnt, (uint32_t)(i + 1), t);
+    }
 }
 
 // Device standard normals in the PC sampler's draw layout: out[r][c] = philox_normal4(seed, stream,
@@ -411,6 +610,74 @@ extern "C" size_t gp_pc_workspace_size(int rows) {
 }
 
 static int pc_pick_nt(int rows, bool split) { return head_pick_nt(rows, split); }
+
+// The persistent sampler (pc_persist_kernel) runs when enabled (GENPOSE2_PC_PERSIST, default PC_PERSIST_DEFAULT),
+// when every workgroup fits on the device at once (nwg <= compute units: the grid-wide exchange waits for all of
+// them) and when its granules, status word and step table fit the workspace's draw region, which the persistent
+// kernel does not use (its draws stay in LDS). Fills pp and returns true then.
+#ifndef PC_PERSIST_DEFAULT
+#define PC_PERSIST_DEFAULT 1
+#endif
+// Pinned host staging for the persistent sampler's per-call upload (its arguments and step table): a slot is
+// written again only after the copy that read it has completed (its event), so the upload never depends on
+// how hipMemcpyAsync treats pageable memory.
+struct PinnedSlot {
+    char* host;
+    size_t bytes;
+    hipEvent_t ev;
+};
+static std::mutex g_stage_mu;
+static std::vector<PinnedSlot> g_stage;
+static int pinned_upload(void* dev, const void* a, size_t na, const void* b, size_t nb, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    PinnedSlot* slot = nullptr;
+    for (auto& sl : g_stage)
+        if (sl.bytes >= na + nb && hipEventQuery(sl.ev) == hipSuccess) {
+            slot = &sl;
+            break;
+        }
+    if (!slot) {
+        PinnedSlot sl{nullptr, std::max<size_t>(na + nb, 64 << 10), nullptr};
+        if (hipHostMalloc(reinterpret_cast<void**>(&sl.host), sl.bytes, hipHostMallocDefault) != hipSuccess)
+            return gp_check_launch("pc_sample: pinned staging");
+        if (hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipHostFree(sl.host);
+            return gp_check_launch("pc_sample: staging event");
+        }
+        g_stage.push_back(sl);
+        slot = &g_stage.back();
+    }
+    memcpy(slot->host, a, na);
+    memcpy(slot->host + na, b, nb);
+    if (hipMemcpyAsync(dev, slot->host, na + nb, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(slot->ev, st) != hipSuccess)
+        return gp_check_launch("pc_sample: staging copy");
+    return GP_OK;
+}
+
+static int pc_device_cus() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return n;
+}
+static constexpr size_t pc_sync_bytes() { return sizeof(unsigned) * PC_SHARDS * PC_SHARD_STRIDE + 128; }
+static constexpr size_t pc_args_bytes() { return (sizeof(PCArgs) + 255) & ~(size_t)255; }
+static bool pc_persist_layout(const PCArgs& a, int rows, int steps, PCPersist& pp) {
+    const char* env = getenv("GENPOSE2_PC_PERSIST");
+    const bool on = env ? env[0] != '0' : PC_PERSIST_DEFAULT != 0;
+    if (!on || a.nwg > pc_device_cus()) return false;
+    const uintptr_t base = ((uintptr_t)a.zbuf + 15) & ~(uintptr_t)15;
+    const size_t gran = ((sizeof(unsigned long long) * 2 * a.nwg + 127) & ~(size_t)127) + pc_sync_bytes();
+    const size_t need = gran + pc_args_bytes() + sizeof(float) * 5 * (size_t)steps;
+    if (base + need > (uintptr_t)(a.zbuf + (size_t)rows * 36)) return false;
+    pp.gran = reinterpret_cast<unsigned long long*>(base);
+    pp.cnt = reinterpret_cast<unsigned*>(base + gran - pc_sync_bytes());
+    pp.status = reinterpret_cast<int*>(pp.cnt + PC_SHARDS * PC_SHARD_STRIDE);
+    pp.args = reinterpret_cast<PCArgs*>(base + gran);
+    pp.tab = reinterpret_cast<const float*>(base + gran + pc_args_bytes());
+    return true;
+}
 
 // Candidates per PC-step workgroup that gp_pc_sample picks for `rows` (split: head weights with
 // the f16 planes) -- lets callers size their accounting from the kernel's real tiling.
@@ -483,6 +750,28 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     a.nwg = (rows + 16 * nt - 1) / (16 * nt);
     a.ls_coef = snr * 3.0f;  // snr * sqrt(pose_dim=9) in fp32 (0.48 rounds identically)
     const dim3 grid(a.nwg);
+    PCPersist pp;
+    if (pc_persist_layout(a, rows, steps, pp)) {
+        // one launch for the whole loop (pc_persist_kernel): the step table and zeroed granules in the workspace
+        if (hipMemsetAsync(pp.gran, 0, reinterpret_cast<char*>(pp.args) - reinterpret_cast<char*>(pp.gran), stream) != hipSuccess)
+            return gp_check_launch("pc_sample: persistent set-up");
+        PCArgs blob[pc_args_bytes() / sizeof(PCArgs) + 1] = {};
+        blob[0] = a;
+        const int rc = pinned_upload(pp.args, blob, pc_args_bytes(), step_tab, sizeof(float) * 5 * steps, stream);
+        if (rc) return rc;
+        const PCArgs* args = pp.args;
+        if (nt == 4)
+            hipLaunchKernelGGL((pc_persist_kernel<4, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, args, pp);
+        else if (nt == 2 && split)
+            hipLaunchKernelGGL((pc_persist_kernel<2, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, args, pp);
+        else if (nt == 2)
+            hipLaunchKernelGGL((pc_persist_kernel<2, PC_WV2, 0>), grid, dim3(PC_WV2 * 64), 0, stream, args, pp);
+        else if (split)
+            hipLaunchKernelGGL((pc_persist_kernel<1, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, args, pp);
+        else
+            hipLaunchKernelGGL((pc_persist_kernel<1, PC_WV1, 0>), grid, dim3(PC_WV1 * 64), 0, stream, args, pp);
+        return gp_check_launch("pc_persist_kernel");
+    }
     for (int i = 0; i <= steps; ++i) {
         PCStep cur = {}, prev = {};
         if (i < steps) cur = PCStep{step_tab[5 * i], step_tab[5 * i + 1], step_tab[5 * i + 2], step_tab[5 * i + 3],

@@ -252,9 +252,125 @@ def levels_worker(w, nprocs, reps, outdir, geom, load="none", nprobe=4, barrier=
         json.dump(log, f)
 
 
+def level0_worker(w, nprocs, reps, outdir, inner=5, into_ws=False, on_device=False):
+    """Level 0 alone (gp_sa_level: ball query, per-point projection Q0, the narrow MLP kernel), INNER times per
+    repetition on a fresh workspace: Q0, both ball lists and the level-0 features compared bit for bit with the
+    first call, so a difference names the stage (inputs vs the MLP kernel)."""
+    import ctypes
+    from genpose2_amd import _lib, device as dev, synthetic, weights
+    torch.cuda.set_device(0)
+    B = 3 if w % 2 == 0 else 256
+    N = 1024
+    pts, _ = synthetic.make_batch(12, B, N)
+    pts = torch.from_numpy(pts).to(DEV)
+    enc = dev.EncoderModel(weights.synthetic_state_dict("score", seed=7), torch.device(DEV))
+    lib = _lib.load()
+    off = np.zeros(25, np.int64)
+    lib.gp_encoder_workspace_layout(B, N, off.ctypes.data_as(_lib.c_int64_p))
+    q0_bytes = B * N * 48 * 4
+    # proj[0] follows feat[0..4] in the layout: its offset is the end of feat[4] rounded up to 256
+    q0_off = (int(off[4 * 5 + 4]) + B * 1024 * 4 + 255) // 256 * 256
+    first, log = None, []
+    for r in range(reps):
+        garbage()
+        enc._ws = None
+        ws = enc.workspace(B, N)
+        feat0 = ws[int(off[4]):].view(torch.float32)[: B * 512 * 96].view(B, 512, 96) if into_ws else \
+            torch.empty(B, 512, 96, device=DEV)
+        lib.gp_encoder_fps(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                           ctypes.c_void_p(dev.stream_handle(torch.device(DEV))))
+        for k in range(inner):
+            _lib.check(lib.gp_sa_level(ctypes.c_void_p(enc.wbuf.data_ptr()), enc.offsets.ctypes.data_as(_lib.c_int64_p), 0, 0,
+                                       ctypes.c_void_p(pts.data_ptr()), B, N, None, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                       ctypes.c_void_p(feat0.data_ptr()), ctypes.c_void_p(dev.stream_handle(torch.device(DEV)))))
+            out = {"q0": ws[q0_off:q0_off + q0_bytes].view(torch.float32).view(B, N, 48),
+                   "ball0": ws[int(off[2]):].view(torch.int32)[: B * 512 * 16],
+                   "ball1": ws[int(off[3]):].view(torch.int32)[: B * 512 * 32],
+                   "cent": ws[int(off[1]):].view(torch.float32)[: B * 512 * 3],
+                   "feat0": feat0}
+            if on_device:   # compared on the device: no host round trip between calls
+                out = {n: v.clone() for n, v in out.items()}
+                if first is None:
+                    first = out
+                diff = [n for n in out if not torch.equal(out[n], first[n])]
+                if diff:
+                    out = {n: v.cpu().numpy() for n, v in out.items()}
+                    first_np = {n: v.cpu().numpy() for n, v in first.items()}
+            else:
+                out = {n: v.cpu().numpy().copy() for n, v in out.items()}
+                if first is None:
+                    first = out
+                diff = [n for n in out if not np.array_equal(out[n], first[n], equal_nan=True)]
+                first_np = first
+            rec = {"worker": w, "B": B, "rep": r, "call": k, "differ": diff}
+            if diff:
+                a, b = out[diff[0]], first_np[diff[0]]
+                rec["n_elems"] = int((a != b).sum())
+                if "feat0" in diff:
+                    bad = np.argwhere(out["feat0"] != first_np["feat0"])
+                    rec["feat_objects"] = sorted({int(x) for x in bad[:, 0]})[:20]
+                    rec["feat_branch_a"] = int((bad[:, 2] < 32).sum())
+                    rec["feat_branch_b"] = int((bad[:, 2] >= 32).sum())
+                    rec["feat_maxdiff"] = float(np.abs(out["feat0"].astype(np.float64) - first_np["feat0"]).max())
+                    if sum(1 for x in log if x["differ"]) < 4:
+                        np.savez(os.path.join(outdir, f"race_level0_w{w}_r{r}_c{k}.npz"), **{f"got_{n}": v for n, v in out.items()},
+                                 **{f"first_{n}": v for n, v in first_np.items()})
+                print(json.dumps(rec), flush=True)
+            log.append(rec)
+    with open(os.path.join(outdir, f"race_level0_w{w}.json"), "w") as f:
+        json.dump(log, f)
+
+
+def snap_worker(w, nprocs, reps, outdir):
+    """The Light encoder level by level (gp_encoder_fps, then gp_sa_level 0..4 into the workspace's own level
+    buffers, as gp_encoder_forward_geom runs them), with every level's features -- and every EARLIER level's
+    features again -- copied out right after each level: the first (level, snapshot) that differs from the
+    first repetition separates a level computing a wrong value from a later kernel overwriting it."""
+    import ctypes
+    from genpose2_amd import _lib, arch, device as dev, synthetic, weights
+    torch.cuda.set_device(0)
+    B = 3 if w % 2 == 0 else 256
+    N = 1024
+    pts, _ = synthetic.make_batch(12, B, N)
+    pts = torch.from_numpy(pts).to(DEV)
+    enc = dev.EncoderModel(weights.synthetic_state_dict("score", seed=7), torch.device(DEV))
+    lib = _lib.load()
+    off = np.zeros(25, np.int64)
+    lib.gp_encoder_workspace_layout(B, N, off.ctypes.data_as(_lib.c_int64_p))
+    couts = [arch.level_out_channels(lv) for lv in range(5)]
+    ms = [arch.NPOINTS[lv] if lv < 4 else 1 for lv in range(5)]
+    st = ctypes.c_void_p(dev.stream_handle(torch.device(DEV)))
+    first, log = None, []
+    for r in range(reps):
+        garbage()
+        enc._ws = None
+        ws = enc.workspace(B, N)
+        feat4 = torch.empty(B, 1024, device=DEV)
+        _lib.check(lib.gp_encoder_fps(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()), ws.numel(), st))
+        views = [ws[int(off[lv * 5 + 4]):].view(torch.float32)[: B * ms[lv] * couts[lv]] for lv in range(4)] + [feat4.view(-1)]
+        snaps = {}
+        for lv in range(5):
+            prev = views[lv - 1] if lv else None
+            _lib.check(lib.gp_sa_level(ctypes.c_void_p(enc.wbuf.data_ptr()), enc.offsets.ctypes.data_as(_lib.c_int64_p), lv,
+                                       couts[lv - 1] if lv else 0, ctypes.c_void_p(pts.data_ptr()), B, N,
+                                       ctypes.c_void_p(prev.data_ptr()) if lv else None, ctypes.c_void_p(ws.data_ptr()),
+                                       ws.numel(), ctypes.c_void_p(views[lv].data_ptr()), st))
+            for k in range(lv + 1):
+                snaps[f"after{lv}_l{k}"] = views[k].clone()   # kept on the device: compared there
+        torch.cuda.synchronize()
+        if first is None:
+            first = snaps
+        diff = [k for k in snaps if not torch.equal(snaps[k], first[k])]
+        rec = {"worker": w, "B": B, "rep": r, "differ": diff}
+        print(json.dumps(rec), flush=True)
+        log.append(rec)
+    with open(os.path.join(outdir, f"race_snap_w{w}.json"), "w") as f:
+        json.dump(log, f)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="fresh", choices=("fresh", "sharded", "levels", "levels_geom"))
+    ap.add_argument("--mode", default="fresh", choices=("fresh", "sharded", "levels", "levels_geom", "level0", "level0_ws", "level0_dev", "level0_ws_dev", "snap"))
     ap.add_argument("--procs", type=int, default=3)
     ap.add_argument("--sync", action="store_true", help="levels modes: probe workers start each repetition together")
     ap.add_argument("--load", default="none", choices=("none", "matmul", "mem", "pipeline"))
@@ -267,6 +383,33 @@ def main():
     os.makedirs(args.outdir, exist_ok=True)
     ckpt = write_reference_checkpoint(os.path.join(tempfile.mkdtemp(), "score.pth"), "score", seed=7)
     t0 = time.time()
+    if args.mode == "snap":
+        mp.spawn(snap_worker, args=(args.procs, args.reps, args.outdir), nprocs=args.procs, join=True)
+        bad, firsts = 0, {}
+        for w in range(args.procs):
+            with open(os.path.join(args.outdir, f"race_snap_w{w}.json")) as f:
+                for r in json.load(f):
+                    if r["differ"]:
+                        bad += 1
+                        firsts[r["differ"][0]] = firsts.get(r["differ"][0], 0) + 1
+        print(json.dumps({"mode": "snap", "procs": args.procs, "reps": args.reps, "differing_reps": bad,
+                          "first_differing_snapshot": firsts, "lib": os.environ.get("GENPOSE_HIP_LIB", "default"),
+                          "seconds": time.time() - t0}))
+        return
+    if args.mode.startswith("level0"):
+        mp.spawn(level0_worker, args=(args.procs, args.reps, args.outdir, 5, "_ws" in args.mode, args.mode.endswith("_dev")),
+                 nprocs=args.procs, join=True)
+        bad, stages = 0, {}
+        for w in range(args.procs):
+            with open(os.path.join(args.outdir, f"race_level0_w{w}.json")) as f:
+                for r in json.load(f):
+                    if r["differ"]:
+                        bad += 1
+                        stages[",".join(r["differ"])] = stages.get(",".join(r["differ"]), 0) + 1
+        print(json.dumps({"mode": args.mode, "procs": args.procs, "reps": args.reps, "differing_calls": bad,
+                          "stages": stages, "lib": os.environ.get("GENPOSE_HIP_LIB", "default"),
+                          "seconds": time.time() - t0}))
+        return
     if args.mode.startswith("levels"):
         nprobe = args.procs if args.nprobe is None else args.nprobe
         import multiprocessing

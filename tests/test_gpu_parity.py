@@ -744,6 +744,43 @@ def test_pc_philox_equals_injected_draws(score_agent, B, K):
     assert torch.equal(res_p, res_i) and torch.equal(q_p, q_i) and torch.equal(xs_p, xs_i)
 
 
+@pytest.mark.parametrize("arith", ["f16x3", "f32"])
+@pytest.mark.parametrize("B,K,inject", [(4, 8, False), (90, 50, True), (164, 50, False), (256, 50, False),
+                                        (256, 50, True)])
+def test_pc_persistent_equals_per_step_launches(score_agent, monkeypatch, B, K, inject, arith):
+    """The persistent sampler (one launch, grid-wide norm exchange through polled granules) against one launch
+    per step (the kernel boundary as the exchange): final poses, quaternions, the final state x and the whole
+    trajectory bit for bit, over every tile width (16 / 32 / 64 candidates, ragged last tiles), both GEMM
+    arithmetics, Philox and injected noise."""
+    from genpose2_amd import device, sde
+    T, seed = 12, 5
+    R = B * K
+    heads = score_agent.heads
+    heads.set_arith(arith)
+    try:
+        tab = sde.pc_step_table(T)
+        tproj = heads.time_proj(torch.from_numpy(tab[:, 0]).to(DEV))
+        g = torch.Generator(device=DEV).manual_seed(B)
+        pobj = heads.object_proj(torch.rand(B, 1024, device=DEV, generator=g))
+        center = torch.rand(B, 3, device=DEV, generator=g)
+        x0 = torch.randn(R, 9, device=DEV, generator=g) * 50
+        kw = {}
+        if inject:
+            kw = dict(z1=torch.randn(T, R, 9, device=DEV, generator=g), z2=torch.randn(T, R, 9, device=DEV, generator=g))
+        out = {}
+        for persist in ("0", "1"):
+            monkeypatch.setenv("GENPOSE2_PC_PERSIST", persist)
+            x = x0.clone()
+            res, q, xs = heads.pc_sample(pobj, tproj, tab, x, K, center, seed=seed, want_xs=True, **kw)
+            torch.cuda.synchronize()
+            out[persist] = (res, q, xs, x)
+        for name, a, b in zip(("res", "q", "xs", "x"), out["0"], out["1"]):
+            assert torch.isfinite(b).all(), name
+            assert torch.equal(a, b), f"{name}: max diff {(a - b).abs().max().item()}"
+    finally:
+        heads.set_arith("f16x3")
+
+
 # ---------------------------------------------------------------- stage hand-off (SURVEY 8f rank 4)
 @pytest.mark.parametrize("n,c", [(1024, 3), (1000, 6), (2048, 3)])
 def test_points_mean_and_bbox_length_vs_oracle(n, c):
