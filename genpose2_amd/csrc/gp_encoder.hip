@@ -1310,33 +1310,43 @@ __global__ __launch_bounds__(TG_THREADS) void tok_split_gemm_kernel(TokArgs a) {
 // both branches, a thread per (point, 4 channels), from the packed layer-0 fragments' xyz k-group (lane
 // ch % 16 of tile ch / 16 holds (wx, wy, wz, 0)). The fma chain in k order is what the fp32 MFMA path
 // (sa_pair_kernel) computes.
+// The branch is the grid's y index, so its weight / bias pointers are picked by a wave-uniform index
+// (scalar loads of the kernel arguments). Picked per lane, as this kernel once did, they were read with
+// VECTOR loads from the kernel-argument segment, which the dispatch does not make coherent for the vector
+// caches: with other processes' kernels on the GPU, a wave now and then read another dispatch's stale
+// pointer and projected its points with the other branch's bias -- the one-off wrong level-0 features
+// behind the round-4 multirank mismatch (scripts/race_probe.py; tests/test_cpu_host.py checks every kernel
+// of the library for vector loads from the argument segment).
 struct ProjXyzArgs {
     const float* xyz;       // (B * n, 3)
     int npts;               // B * n
     const float* w0[2];     // packed layer-0 fragments (k-groups kg0 = 1, xyz group 0)
     const float* b0[2];
     int ch[2];              // padded channel counts (16 | 32)
-    float* q;               // (B * n, q_stride)
+    float* q;               // (B * n, q_stride): branch 0's channels, then branch 1's
     int q_stride;
 };
 __global__ __launch_bounds__(256) void proj_xyz_kernel(ProjXyzArgs a) {
-    const int g4 = (a.ch[0] + a.ch[1]) / 4;
+    const int br = blockIdx.y;   // wave-uniform
+    const int g4 = a.ch[br] / 4, qoff = br ? a.ch[0] : 0;
+    const float* w0 = a.w0[br];
+    const float* b0 = a.b0[br];
     const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= (size_t)a.npts * g4) return;
     const int p = (int)(t / g4), g = (int)(t - (size_t)p * g4);
-    const int br = 4 * g < a.ch[0] ? 0 : 1, c0 = 4 * g - (br ? a.ch[0] : 0);
+    const int c0 = 4 * g;
     const float x = a.xyz[(size_t)p * 3 + 0], y = a.xyz[(size_t)p * 3 + 1], z = a.xyz[(size_t)p * 3 + 2];
     float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int ch = c0 + j;
-        const f32x4 w = ld4(a.w0[br] + ((size_t)(ch >> 4) * 64 + (ch & 15)) * 4);
+        const f32x4 w = ld4(w0 + ((size_t)(ch >> 4) * 64 + (ch & 15)) * 4);
         float acc = __builtin_fmaf(w.x, x, 0.f);
         acc = __builtin_fmaf(w.y, y, acc);
         acc = __builtin_fmaf(w.z, z, acc);
-        v[j] = acc + a.b0[br][ch];
+        v[j] = acc + b0[ch];
     }
-    st4(a.q + (size_t)p * a.q_stride + 4 * g, f32x4{v[0], v[1], v[2], v[3]});
+    st4(a.q + (size_t)p * a.q_stride + qoff + 4 * g, f32x4{v[0], v[1], v[2], v[3]});
 }
 
 // ============================================================================ host side
@@ -1650,8 +1660,8 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             GP_REQUIRE(pa.ch[0] + pa.ch[1] == proj_stride(0), "encoder: level-0 projection layout");
             pa.q = qbuf;
             pa.q_stride = proj_stride(0);
-            const size_t threads = (size_t)pa.npts * (pa.ch[0] + pa.ch[1]) / 4;
-            hipLaunchKernelGGL(proj_xyz_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, pa);
+            const size_t threads = (size_t)pa.npts * std::max(pa.ch[0], pa.ch[1]) / 4;   // per branch (grid y)
+            hipLaunchKernelGGL(proj_xyz_kernel, dim3((unsigned)((threads + 255) / 256), 2), dim3(256), 0, st, pa);
             rc = gp_check_launch("proj_xyz_kernel");
         } else {
             rc = split0 ? run_proj_split(c, l, c_prev, feat_prev, xyz_prev, n_prev, qbuf, st)

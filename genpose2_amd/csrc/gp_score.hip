@@ -432,7 +432,6 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
 // status word, poisons its rows (NaN) and stops waiting, so a co-residency failure ends as an error and
 // never as a hang.
 struct PCPersist {
-    PCArgs* args;                  // the kernel's arguments (uploaded with the table)
     const float* tab;              // (steps, 5) step table
     unsigned long long* gran;      // (2, nwg) granules, zero at launch
     unsigned* cnt;                 // PC_SHARDS arrival counters, 128 B apart, zero at launch
@@ -503,7 +502,7 @@ __device__ __forceinline__ float pc_gather_norms(const unsigned long long* gran,
 }
 
 template <int NT, int WV, int PL>
-__global__ __launch_bounds__(WV * 64) void pc_persist_kernel(const PCArgs* __restrict__ args, PCPersist pp) {
+__global__ __launch_bounds__(WV * 64) void pc_persist_kernel(PCArgs a, PCPersist pp) {
     constexpr int ROWS = NT * 16;
     static_assert(NT < WV, "at least one wave besides the update waves");
     __shared__ HeadSmem<NT, WV, PL> sm;
@@ -511,7 +510,7 @@ __global__ __launch_bounds__(WV * 64) void pc_persist_kernel(const PCArgs* __res
     __shared__ int obj[ROWS];
     __shared__ float s_l[ROWS * 9];          // score of the last step, [row][9]
     __shared__ float z_l[2][2][ROWS * 9];    // draws: [step parity][stream][row][9]
-    const PCArgs& a0 = *args;
+    const PCArgs& a0 = a;
     bool timed_out = false;
     stage_small_weights<NT, WV, 0, !SPLIT>(a0.w, sm);   // once (published by the trunk's first barrier)
     const int steps = a0.steps;
@@ -520,9 +519,6 @@ __global__ __launch_bounds__(WV * 64) void pc_persist_kernel(const PCArgs* __res
         // is hoisted out of the loop and kept live (spilled) across the trunk
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
-        const PCArgs* ap = args;
-        asm volatile("" : "+s"(ap));
-        const PCArgs& a = *ap;
         const int lane = tid & 63;
         const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int r0 = blockIdx.x * ROWS;
@@ -574,7 +570,11 @@ __global__ __launch_bounds__(WV * 64) void pc_persist_kernel(const PCArgs* __res
         else
             head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
         PC_MARK(7);
-        const float t = pc_score_norm<NT, WV, PL>(a, cur, sm, r0, wid, lane, [&](int c, int o, float v) { s_l[c * 9 + o] = v; });
+        const bool last = i == steps - 1;   // the last score also goes to the workspace's s, as per-step launches leave it
+        const float t = pc_score_norm<NT, WV, PL>(a, cur, sm, r0, wid, lane, [&](int c, int o, float v) {
+            s_l[c * 9 + o] = v;
+            if (last) a.s[(size_t)(r0 + c) * 9 + o] = v;
+        });
         PC_MARK(8);
         if (tid == 0) pc_publish(pp.gran + (size_t)(i & 1) * a.nwg, pp.cnt, (uint32_t)(i + 1), t);
     }
@@ -616,9 +616,9 @@ static int pc_pick_nt(int rows, bool split) { return head_pick_nt(rows, split); 
 // them) and when its granules, status word and step table fit the workspace's draw region, which the persistent
 // kernel does not use (its draws stay in LDS). Fills pp and returns true then.
 #ifndef PC_PERSIST_DEFAULT
-#define PC_PERSIST_DEFAULT 1
+#define PC_PERSIST_DEFAULT 0
 #endif
-// Pinned host staging for the persistent sampler's per-call upload (its arguments and step table): a slot is
+// Pinned host staging for the persistent sampler's per-call upload of the step table: a slot is
 // written again only after the copy that read it has completed (its event), so the upload never depends on
 // how hipMemcpyAsync treats pageable memory.
 struct PinnedSlot {
@@ -628,16 +628,16 @@ struct PinnedSlot {
 };
 static std::mutex g_stage_mu;
 static std::vector<PinnedSlot> g_stage;
-static int pinned_upload(void* dev, const void* a, size_t na, const void* b, size_t nb, hipStream_t st) {
+static int pinned_upload(void* dev, const void* a, size_t na, hipStream_t st) {
     std::lock_guard<std::mutex> lk(g_stage_mu);
     PinnedSlot* slot = nullptr;
     for (auto& sl : g_stage)
-        if (sl.bytes >= na + nb && hipEventQuery(sl.ev) == hipSuccess) {
+        if (sl.bytes >= na && hipEventQuery(sl.ev) == hipSuccess) {
             slot = &sl;
             break;
         }
     if (!slot) {
-        PinnedSlot sl{nullptr, std::max<size_t>(na + nb, 64 << 10), nullptr};
+        PinnedSlot sl{nullptr, std::max<size_t>(na, 64 << 10), nullptr};
         if (hipHostMalloc(reinterpret_cast<void**>(&sl.host), sl.bytes, hipHostMallocDefault) != hipSuccess)
             return gp_check_launch("pc_sample: pinned staging");
         if (hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) {
@@ -648,8 +648,7 @@ static int pinned_upload(void* dev, const void* a, size_t na, const void* b, siz
         slot = &g_stage.back();
     }
     memcpy(slot->host, a, na);
-    memcpy(slot->host + na, b, nb);
-    if (hipMemcpyAsync(dev, slot->host, na + nb, hipMemcpyHostToDevice, st) != hipSuccess ||
+    if (hipMemcpyAsync(dev, slot->host, na, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipEventRecord(slot->ev, st) != hipSuccess)
         return gp_check_launch("pc_sample: staging copy");
     return GP_OK;
@@ -662,20 +661,18 @@ static int pc_device_cus() {
     return n;
 }
 static constexpr size_t pc_sync_bytes() { return sizeof(unsigned) * PC_SHARDS * PC_SHARD_STRIDE + 128; }
-static constexpr size_t pc_args_bytes() { return (sizeof(PCArgs) + 255) & ~(size_t)255; }
 static bool pc_persist_layout(const PCArgs& a, int rows, int steps, PCPersist& pp) {
     const char* env = getenv("GENPOSE2_PC_PERSIST");
     const bool on = env ? env[0] != '0' : PC_PERSIST_DEFAULT != 0;
     if (!on || a.nwg > pc_device_cus()) return false;
     const uintptr_t base = ((uintptr_t)a.zbuf + 15) & ~(uintptr_t)15;
     const size_t gran = ((sizeof(unsigned long long) * 2 * a.nwg + 127) & ~(size_t)127) + pc_sync_bytes();
-    const size_t need = gran + pc_args_bytes() + sizeof(float) * 5 * (size_t)steps;
+    const size_t need = gran + sizeof(float) * 5 * (size_t)steps;
     if (base + need > (uintptr_t)(a.zbuf + (size_t)rows * 36)) return false;
     pp.gran = reinterpret_cast<unsigned long long*>(base);
     pp.cnt = reinterpret_cast<unsigned*>(base + gran - pc_sync_bytes());
     pp.status = reinterpret_cast<int*>(pp.cnt + PC_SHARDS * PC_SHARD_STRIDE);
-    pp.args = reinterpret_cast<PCArgs*>(base + gran);
-    pp.tab = reinterpret_cast<const float*>(base + gran + pc_args_bytes());
+    pp.tab = reinterpret_cast<const float*>(base + gran);
     return true;
 }
 
@@ -753,23 +750,21 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     PCPersist pp;
     if (pc_persist_layout(a, rows, steps, pp)) {
         // one launch for the whole loop (pc_persist_kernel): the step table and zeroed granules in the workspace
-        if (hipMemsetAsync(pp.gran, 0, reinterpret_cast<char*>(pp.args) - reinterpret_cast<char*>(pp.gran), stream) != hipSuccess)
+        if (hipMemsetAsync(pp.gran, 0, reinterpret_cast<const char*>(pp.tab) - reinterpret_cast<char*>(pp.gran), stream) !=
+            hipSuccess)
             return gp_check_launch("pc_sample: persistent set-up");
-        PCArgs blob[pc_args_bytes() / sizeof(PCArgs) + 1] = {};
-        blob[0] = a;
-        const int rc = pinned_upload(pp.args, blob, pc_args_bytes(), step_tab, sizeof(float) * 5 * steps, stream);
+        const int rc = pinned_upload(const_cast<float*>(pp.tab), step_tab, sizeof(float) * 5 * steps, stream);
         if (rc) return rc;
-        const PCArgs* args = pp.args;
         if (nt == 4)
-            hipLaunchKernelGGL((pc_persist_kernel<4, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, args, pp);
+            hipLaunchKernelGGL((pc_persist_kernel<4, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, pp);
         else if (nt == 2 && split)
-            hipLaunchKernelGGL((pc_persist_kernel<2, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, args, pp);
+            hipLaunchKernelGGL((pc_persist_kernel<2, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, pp);
         else if (nt == 2)
-            hipLaunchKernelGGL((pc_persist_kernel<2, PC_WV2, 0>), grid, dim3(PC_WV2 * 64), 0, stream, args, pp);
+            hipLaunchKernelGGL((pc_persist_kernel<2, PC_WV2, 0>), grid, dim3(PC_WV2 * 64), 0, stream, a, pp);
         else if (split)
-            hipLaunchKernelGGL((pc_persist_kernel<1, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, args, pp);
+            hipLaunchKernelGGL((pc_persist_kernel<1, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, pp);
         else
-            hipLaunchKernelGGL((pc_persist_kernel<1, PC_WV1, 0>), grid, dim3(PC_WV1 * 64), 0, stream, args, pp);
+            hipLaunchKernelGGL((pc_persist_kernel<1, PC_WV1, 0>), grid, dim3(PC_WV1 * 64), 0, stream, a, pp);
         return gp_check_launch("pc_persist_kernel");
     }
     for (int i = 0; i <= steps; ++i) {

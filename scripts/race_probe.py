@@ -252,7 +252,7 @@ def levels_worker(w, nprocs, reps, outdir, geom, load="none", nprobe=4, barrier=
         json.dump(log, f)
 
 
-def level0_worker(w, nprocs, reps, outdir, inner=5, into_ws=False, on_device=False):
+def level0_worker(w, nprocs, reps, outdir, inner=5, into_ws=False, on_device=False, poison=False):
     """Level 0 alone (gp_sa_level: ball query, per-point projection Q0, the narrow MLP kernel), INNER times per
     repetition on a fresh workspace: Q0, both ball lists and the level-0 features compared bit for bit with the
     first call, so a difference names the stage (inputs vs the MLP kernel)."""
@@ -265,6 +265,7 @@ def level0_worker(w, nprocs, reps, outdir, inner=5, into_ws=False, on_device=Fal
     pts = torch.from_numpy(pts).to(DEV)
     enc = dev.EncoderModel(weights.synthetic_state_dict("score", seed=7), torch.device(DEV))
     lib = _lib.load()
+    plib = ctypes.CDLL(os.path.join(REPO, "scripts", "libpoison.so")) if poison else None
     off = np.zeros(25, np.int64)
     lib.gp_encoder_workspace_layout(B, N, off.ctypes.data_as(_lib.c_int64_p))
     q0_bytes = B * N * 48 * 4
@@ -280,6 +281,8 @@ def level0_worker(w, nprocs, reps, outdir, inner=5, into_ws=False, on_device=Fal
         lib.gp_encoder_fps(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
                            ctypes.c_void_p(dev.stream_handle(torch.device(DEV))))
         for k in range(inner):
+            if poison:   # junk in every CU's LDS and every SIMD's registers before the call (scripts/poison.hip)
+                plib.poison_gpu(ctypes.c_uint32(r * 7919 + k * 104729 + w), 2048, ctypes.c_void_p(dev.stream_handle(torch.device(DEV))))
             _lib.check(lib.gp_sa_level(ctypes.c_void_p(enc.wbuf.data_ptr()), enc.offsets.ctypes.data_as(_lib.c_int64_p), 0, 0,
                                        ctypes.c_void_p(pts.data_ptr()), B, N, None, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
                                        ctypes.c_void_p(feat0.data_ptr()), ctypes.c_void_p(dev.stream_handle(torch.device(DEV)))))
@@ -348,6 +351,9 @@ def snap_worker(w, nprocs, reps, outdir):
         feat4 = torch.empty(B, 1024, device=DEV)
         _lib.check(lib.gp_encoder_fps(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()), ws.numel(), st))
         views = [ws[int(off[lv * 5 + 4]):].view(torch.float32)[: B * ms[lv] * couts[lv]] for lv in range(4)] + [feat4.view(-1)]
+        if os.environ.get("SNAP_SENTINEL") == "1":   # Q0's buffer set to NaN first: a projection that never lands shows
+            q0o = (int(off[4 * 5 + 4]) + B * 1024 * 4 + 255) // 256 * 256
+            ws[q0o:q0o + B * N * 48 * 4].view(torch.float32).fill_(float("nan"))
         snaps = {}
         for lv in range(5):
             prev = views[lv - 1] if lv else None
@@ -355,6 +361,12 @@ def snap_worker(w, nprocs, reps, outdir):
                                        couts[lv - 1] if lv else 0, ctypes.c_void_p(pts.data_ptr()), B, N,
                                        ctypes.c_void_p(prev.data_ptr()) if lv else None, ctypes.c_void_p(ws.data_ptr()),
                                        ws.numel(), ctypes.c_void_p(views[lv].data_ptr()), st))
+            if lv == 0:   # level 0's inputs as the MLP saw them (Q0 is reused by level 1 for its row maxima)
+                q0_off = (int(off[4 * 5 + 4]) + B * 1024 * 4 + 255) // 256 * 256
+                snaps["after0_q0"] = ws[q0_off:q0_off + B * N * 48 * 4].clone()
+                snaps["after0_ball0"] = ws[int(off[2]):int(off[2]) + B * 512 * 16 * 4].clone()
+                snaps["after0_ball1"] = ws[int(off[3]):int(off[3]) + B * 512 * 32 * 4].clone()
+                snaps["after0_cent"] = ws[int(off[1]):int(off[1]) + B * 512 * 3 * 4].clone()
             for k in range(lv + 1):
                 snaps[f"after{lv}_l{k}"] = views[k].clone()   # kept on the device: compared there
         torch.cuda.synchronize()
@@ -362,6 +374,41 @@ def snap_worker(w, nprocs, reps, outdir):
             first = snaps
         diff = [k for k in snaps if not torch.equal(snaps[k], first[k])]
         rec = {"worker": w, "B": B, "rep": r, "differ": diff}
+        if "after0_q0" in diff:
+            # where Q0 differs: level 1 later writes its per-point row maxima over the first B*512 floats of
+            # this buffer, so a stale Q0 from the previous repetition differs exactly there
+            qa = snaps["after0_q0"].view(torch.float32).cpu().numpy()
+            qf = first["after0_q0"].view(torch.float32).cpu().numpy()
+            bad = np.nonzero(qa != qf)[0]
+            rec["q0_n"] = int(len(bad))
+            rec["q0_first_last"] = [int(bad.min()), int(bad.max())]
+            rec["q0_in_rowmax_region"] = int((bad < B * 512).sum())
+            rec["q0_nan"] = int(np.isnan(qa).sum())
+            rec["q0_got_sample"] = [float(v) for v in qa[bad[:6]]]
+            rec["q0_first_sample"] = [float(v) for v in qf[bad[:6]]]
+            # per differing point row: which 16-float blocks, and whether the bad block equals the same block of
+            # another point's correct row (a wrong source point) -- and which
+            QA, QF = qa.reshape(B * N, 3, 16), qf.reshape(B * N, 3, 16)
+            rows = sorted({int(i) // 48 for i in bad})
+            info = []
+            for p in rows[:12]:
+                blks = [k for k in range(3) if not np.array_equal(QA[p, k], QF[p, k])]
+                src = []
+                for k in blks:
+                    hit = np.nonzero((QF[:, k] == QA[p, k]).all(1))[0]
+                    src.append(int(hit[0]) if len(hit) else -1)
+                info.append([p, blks, src])
+            rec["q0_rows"] = info
+            if B <= 8 and sum(1 for x in log if x["differ"]) < 3:
+                np.savez(os.path.join(outdir, f"race_snap_q0_w{w}_r{r}.npz"), got=qa, first=qf)
+        if "after0_l0" in diff:
+            a0 = snaps["after0_l0"].view(B, 512, 96).cpu().numpy()
+            f0 = first["after0_l0"].view(B, 512, 96).cpu().numpy()
+            bad = np.argwhere(a0 != f0)
+            rec["l0_objects"] = sorted({int(x) for x in bad[:, 0]})[:20]
+            rec["l0_branch_a"] = int((bad[:, 2] < 32).sum())
+            rec["l0_branch_b"] = int((bad[:, 2] >= 32).sum())
+            rec["l0_maxdiff"] = float(np.abs(a0.astype(np.float64) - f0).max())
         print(json.dumps(rec), flush=True)
         log.append(rec)
     with open(os.path.join(outdir, f"race_snap_w{w}.json"), "w") as f:
@@ -370,7 +417,7 @@ def snap_worker(w, nprocs, reps, outdir):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="fresh", choices=("fresh", "sharded", "levels", "levels_geom", "level0", "level0_ws", "level0_dev", "level0_ws_dev", "snap"))
+    ap.add_argument("--mode", default="fresh", choices=("fresh", "sharded", "levels", "levels_geom", "level0", "level0_ws", "level0_dev", "level0_ws_dev", "level0_poison", "snap"))
     ap.add_argument("--procs", type=int, default=3)
     ap.add_argument("--sync", action="store_true", help="levels modes: probe workers start each repetition together")
     ap.add_argument("--load", default="none", choices=("none", "matmul", "mem", "pipeline"))
@@ -397,8 +444,8 @@ def main():
                           "seconds": time.time() - t0}))
         return
     if args.mode.startswith("level0"):
-        mp.spawn(level0_worker, args=(args.procs, args.reps, args.outdir, 5, "_ws" in args.mode, args.mode.endswith("_dev")),
-                 nprocs=args.procs, join=True)
+        mp.spawn(level0_worker, args=(args.procs, args.reps, args.outdir, 5, "_ws" in args.mode, args.mode.endswith("_dev"),
+                                      args.mode.endswith("_poison")), nprocs=args.procs, join=True)
         bad, stages = 0, {}
         for w in range(args.procs):
             with open(os.path.join(args.outdir, f"race_level0_w{w}.json")) as f:

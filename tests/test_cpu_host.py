@@ -28,6 +28,81 @@ def test_library_exports_every_declared_symbol():
     assert lib.gp_encoder_workspace_size(64, 1024) > 0 and lib.gp_pc_workspace_size(3200) >= 3200 * 36
 
 
+def _gfx950_code_objects(so):
+    """The gfx950 ELF code objects of a HIP shared library (its .hip_fatbin clang offload bundles)."""
+    import struct
+    import tempfile
+    objcopy = "/opt/rocm/lib/llvm/bin/llvm-objcopy"
+    with tempfile.TemporaryDirectory() as d:
+        fb = os.path.join(d, "fatbin")
+        subprocess.run([objcopy, "--dump-section", f".hip_fatbin={fb}", so, os.path.join(d, "copy")], check=True,
+                       capture_output=True)
+        b = open(fb, "rb").read()
+    magic, out, pos = b"__CLANG_OFFLOAD_BUNDLE__", [], 0
+    while (i := b.find(magic, pos)) >= 0:
+        n = struct.unpack_from("<Q", b, i + 24)[0]
+        off = i + 32
+        for _ in range(n):
+            o, sz, tl = struct.unpack_from("<QQQ", b, off)
+            off += 24
+            triple = b[off:off + tl].decode()
+            off += tl
+            if triple.endswith("gfx950"):
+                out.append(b[i + o:i + o + sz])
+        pos = i + 1
+    return out
+
+
+def test_no_vector_loads_from_the_kernel_argument_segment():
+    """Every kernel reads its arguments with scalar loads only. An argument array indexed per lane (the old
+    proj_xyz_kernel's w0[br] / b0[br]) compiles to VECTOR loads from the kernel-argument segment, which the
+    dispatch does not keep coherent for the vector caches: with other processes' kernels on the GPU a wave
+    now and then read a stale pointer (the round-4 multirank mismatch, DESIGN (c)). Scans the disassembly of
+    every gfx950 kernel for a vector memory instruction addressed from the argument pointer before that
+    pointer's registers are overwritten, or a copy of it into a VGPR."""
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    so = os.path.join(REPO, "genpose2_amd", "libgenpose_hip.so")
+    cos = _gfx950_code_objects(so)
+    assert cos, "no gfx950 code object in the library"
+    import tempfile
+    bad, kernels = [], 0
+    sreg = re.compile(r"^s\[?(\d+)(?::(\d+))?\]?$")
+    for k, co in enumerate(cos):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            dis = subprocess.run([objdump, "-d", "--mcpu=gfx950", f.name], capture_output=True, text=True, check=True).stdout
+        for fn, body in re.findall(r"^[0-9a-f]+ <(\w+)>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", dis, re.M | re.S):
+            kernels += 1
+            base = None           # the SGPR pair the first scalar load reads the arguments through
+            for line in body.split("\n"):
+                ins = line.split("//")[0].strip().replace(",", " ").split()
+                if not ins:
+                    continue
+                op, args = ins[0], ins[1:]
+                if base is None:
+                    if op.startswith("s_load") and len(args) > 1:
+                        base = args[1]
+                    continue
+                lo, hi = map(int, sreg.match(base).groups())
+                if op.startswith(("global_load", "buffer_load", "flat_load")) and base in args[1:]:
+                    bad.append(f"{fn}: {' '.join(ins)}")
+                if op.startswith("v_mov") and len(args) > 1 and args[1] in (f"s{lo}", f"s{hi}"):
+                    bad.append(f"{fn}: {' '.join(ins)}")
+                # the pointer's registers overwritten: later uses are not the argument segment
+                if args and op.startswith("s_") and not op.startswith(("s_cmp", "s_cbranch", "s_waitcnt", "s_barrier")):
+                    m = sreg.match(args[0])
+                    if m:
+                        d0 = int(m.group(1))
+                        d1 = int(m.group(2)) if m.group(2) else d0
+                        if d0 <= hi and d1 >= lo:
+                            break
+    assert kernels > 50, kernels
+    assert not bad, "\n".join(bad)
+
+
 def test_invalid_arguments_return_status_not_exit():
     from genpose2_amd import _lib
     lib = _lib.load()
