@@ -316,9 +316,9 @@ __global__ __launch_bounds__(256) void points_mean_kernel(const float* __restric
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
     const float* p = pts + (size_t)b * n * c;
     for (int i = tid; i < n; i += 256) {
-        s0 += p[(size_t)i * c + 0];
-        s1 += p[(size_t)i * c + 1];
-        s2 += p[(size_t)i * c + 2];
+        s0 += ld1(p + (size_t)i * c + 0);
+        s1 += ld1(p + (size_t)i * c + 1);
+        s2 += ld1(p + (size_t)i * c + 2);
     }
     red[0][tid] = s0;
     red[1][tid] = s1;
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void bbox_length_kernel(const float* __restric
     float m0 = 0.f, m1 = 0.f, m2 = 0.f;
     const float* p = pcl + (size_t)b * n * c;
     for (int i = tid; i < n; i += 256) {
-        const float d0 = p[(size_t)i * c] - t0, d1 = p[(size_t)i * c + 1] - t1, d2 = p[(size_t)i * c + 2] - t2;
+        const float d0 = ld1(p + (size_t)i * c) - t0, d1 = ld1(p + (size_t)i * c + 1) - t1, d2 = ld1(p + (size_t)i * c + 2) - t2;
         // bmm(R^T, d): row j of R^T is column j of R
         m0 = fmaxf(m0, fabsf((r00 * d0 + r10 * d1) + r20 * d2));
         m1 = fmaxf(m1, fabsf((r01 * d0 + r11 * d1) + r21 * d2));

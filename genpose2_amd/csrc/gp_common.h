@@ -52,6 +52,17 @@ typedef __attribute__((address_space(3))) void* lds_void_ptr;   // LDS-DMA desti
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
+// One 4-byte global load that the backend never merges with its neighbours (a relaxed workgroup-scope atomic
+// load: a plain global_load_dword, sc0, cached as usual). Three consecutive floats (coordinates, a pose
+// row's three entries) are read through it: merged, they become a global_load_dwordx3, and gfx950 returned a
+// stale second dword to a packed-FP32 instruction (v_pk_fma_f32 / v_pk_add_f32 reading the load's register
+// pair) in a few 16-lane groups per thousand launches when other processes' kernels shared the GPU -- the
+// level-0 projection then lost its y term (DESIGN (c); scripts/race_probe.py). tests/test_cpu_host.py checks
+// the library for any dwordx3 load feeding a packed-FP32 instruction.
+__device__ __forceinline__ float ld1(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Buffer resource over `bytes` bytes at p (p must be wave-uniform: a kernel argument).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);

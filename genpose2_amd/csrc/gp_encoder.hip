@@ -127,9 +127,9 @@ __device__ __forceinline__ void sa_layer(const SAArgs& a, f32x4* lds, int L, int
                 const float* px = a.xyz_prev + ((size_t)b * a.n_prev + p) * 3;
                 if (a.cent) {  // grouped_xyz -= new_xyz (pointnet2_utils.py:281-282)
                     const float* cc = a.cent + ((size_t)b * a.m + m) * 3;
-                    v = f32x4{fsub(px[0], cc[0]), fsub(px[1], cc[1]), fsub(px[2], cc[2]), 0.f};
+                    v = f32x4{fsub(ld1(px), ld1(cc)), fsub(ld1(px + 1), ld1(cc + 1)), fsub(ld1(px + 2), ld1(cc + 2)), 0.f};
                 } else {       // GroupAll keeps raw xyz (pointnet2_utils.py:316-324)
-                    v = f32x4{px[0], px[1], px[2], 0.f};
+                    v = f32x4{ld1(px), ld1(px + 1), ld1(px + 2), 0.f};
                 }
             }
             bx[c] = v;
@@ -259,7 +259,7 @@ __device__ __forceinline__ void sa_gather0(const SAArgs& a, f32x4* lds, int b, i
         const int c = e / H0p, ch = e - (e / H0p) * H0p;
         const float* cc = a.cent + ((size_t)b * a.m + mfirst + c) * 3;
         const f32x4 w = w0[((ch >> 4) * KG0 + gx) * 64 + (ch & 15)];   // W0[ch][c_prev + 0..2]
-        cx[e] = (w.x * cc[0] + w.y * cc[1]) + w.z * cc[2];
+        cx[e] = (w.x * ld1(cc) + w.y * ld1(cc + 1)) + w.z * ld1(cc + 2);
     }
     int pcol[CT], mcol[CT];
     bool ok[CT];
@@ -443,7 +443,7 @@ __device__ __forceinline__ void split_centroid_term(const SplitArgs& a, float* P
         const int mi = min(mi0 + ci, a.m - 1);   // past the last centroid: any value (never stored)
         const float* cc = a.cent + ((size_t)b * a.m + mi) * 3;
         const f32x4 w = ld4(a.w0 + ((size_t)((ch >> 4) * a.kg0 + a.gx) * 64 + (ch & 15)) * 4);
-        P[idx] = (w.x * cc[0] + w.y * cc[1]) + w.z * cc[2];
+        P[idx] = (w.x * ld1(cc) + w.y * ld1(cc + 1)) + w.z * ld1(cc + 2);
     }
 }
 
@@ -778,9 +778,9 @@ __device__ __forceinline__ void narrow_fetch(const NarrowArgs& a, int task, cons
                                              NarrowGather<SPAN, KG>& g) {
     const int b = task / a.m;
     const float* cc = a.cent + (size_t)task * 3;
-    g.cx = cc[0];
-    g.cy = cc[1];
-    g.cz = cc[2];
+    g.cx = ld1(cc);
+    g.cy = ld1(cc + 1);
+    g.cz = ld1(cc + 2);
 #pragma unroll
     for (int ct = 0; ct < SPAN; ++ct) {
         const float* qrow = a.qin + ((size_t)b * a.n_prev + p[ct]) * a.q_stride + a.q_off + 4 * q;
@@ -1317,6 +1317,9 @@ __global__ __launch_bounds__(TG_THREADS) void tok_split_gemm_kernel(TokArgs a) {
 // pointer and projected its points with the other branch's bias -- the one-off wrong level-0 features
 // behind the round-4 multirank mismatch (scripts/race_probe.py; tests/test_cpu_host.py checks every kernel
 // of the library for vector loads from the argument segment).
+#ifndef PROJ_DIAG
+#define PROJ_DIAG 0
+#endif
 struct ProjXyzArgs {
     const float* xyz;       // (B * n, 3)
     int npts;               // B * n
@@ -1335,16 +1338,28 @@ __global__ __launch_bounds__(256) void proj_xyz_kernel(ProjXyzArgs a) {
     if (t >= (size_t)a.npts * g4) return;
     const int p = (int)(t / g4), g = (int)(t - (size_t)p * g4);
     const int c0 = 4 * g;
-    const float x = a.xyz[(size_t)p * 3 + 0], y = a.xyz[(size_t)p * 3 + 1], z = a.xyz[(size_t)p * 3 + 2];
+    const float x = ld1(a.xyz + (size_t)p * 3 + 0), y = ld1(a.xyz + (size_t)p * 3 + 1), z = ld1(a.xyz + (size_t)p * 3 + 2);
     float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int ch = c0 + j;
         const f32x4 w = ld4(w0 + ((size_t)(ch >> 4) * 64 + (ch & 15)) * 4);
         float acc = __builtin_fmaf(w.x, x, 0.f);
+#if PROJ_DIAG & 2   // diagnostic: opaque values between the chains, so no packed-FP32 (v_pk_fma_f32) forms
+        asm volatile("" : "+v"(acc));
+#endif
         acc = __builtin_fmaf(w.y, y, acc);
+#if PROJ_DIAG & 2
+        asm volatile("" : "+v"(acc));
+#endif
         acc = __builtin_fmaf(w.z, z, acc);
+#if PROJ_DIAG & 2
+        asm volatile("" : "+v"(acc));
+#endif
         v[j] = acc + b0[ch];
+#if PROJ_DIAG & 2
+        asm volatile("" : "+v"(v[j]));
+#endif
     }
     st4(a.q + (size_t)p * a.q_stride + qoff + 4 * g, f32x4{v[0], v[1], v[2], v[3]});
 }

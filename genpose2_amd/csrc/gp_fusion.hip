@@ -582,9 +582,9 @@ __global__ __launch_bounds__(FUS_THREADS) void relpe_bias_kernel(const float* __
     float rx, ry, rz;
     {
 #pragma clang fp contract(off)
-        rx = pj[0] - pi[0];   // xyz[j] - xyz[i]
-        ry = pj[1] - pi[1];
-        rz = pj[2] - pi[2];
+        rx = ld1(pj) - ld1(pi);   // xyz[j] - xyz[i]
+        ry = ld1(pj + 1) - ld1(pi + 1);
+        rz = ld1(pj + 2) - ld1(pi + 2);
     }
     float hb[FUS_HEADS];
     relpe_heads(pe, rx, ry, rz, hb);
@@ -803,8 +803,8 @@ __global__ __launch_bounds__(FUS_THREADS) void mha_relpe_kernel(const float* __r
     const float* base = qkv + (size_t)b * n * ld;
     const int i = qb * 64 + wid * 16 + nl;
     const int ii = i < n ? i : n - 1;
-    const float px = xyz[((size_t)b * n + ii) * 3], py = xyz[((size_t)b * n + ii) * 3 + 1],
-                pz = xyz[((size_t)b * n + ii) * 3 + 2];
+    const float px = ld1(xyz + ((size_t)b * n + ii) * 3), py = ld1(xyz + ((size_t)b * n + ii) * 3 + 1),
+                pz = ld1(xyz + ((size_t)b * n + ii) * 3 + 2);
     f32x4 qf[FUS_HEADS][NG], o[FUS_HEADS][NG];
     float m[FUS_HEADS], lsum[FUS_HEADS];
 #pragma unroll
@@ -856,9 +856,9 @@ __global__ __launch_bounds__(FUS_THREADS) void mha_relpe_kernel(const float* __r
                     float rx, ry, rz;
                     {
 #pragma clang fp contract(off)
-                        rx = kx[3 * j] - px;   // xyz[key] - xyz[query]
-                        ry = kx[3 * j + 1] - py;
-                        rz = kx[3 * j + 2] - pz;
+                        rx = ld1(kx + 3 * j) - px;   // xyz[key] - xyz[query]; 4-byte LDS reads (gp_common.h ld1)
+                        ry = ld1(kx + 3 * j + 1) - py;
+                        rz = ld1(kx + 3 * j + 2) - pz;
                     }
                     relpe_heads(pe, rx, ry, rz, bb[r]);
                 } else {

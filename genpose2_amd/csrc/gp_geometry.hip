@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const flo
     const int b = blockIdx.y;
     const float* pts = xyz + (size_t)b * n * 3;
     if constexpr (LDSP) {
-        for (int i = threadIdx.x; i < n; i += 256) sp[i] = f32x4{pts[3 * i + 0], pts[3 * i + 1], pts[3 * i + 2], 0.f};
+        for (int i = threadIdx.x; i < n; i += 256) sp[i] = f32x4{ld1(pts + 3 * i), ld1(pts + 3 * i + 1), ld1(pts + 3 * i + 2), 0.f};
         __syncthreads();
     }
     const unsigned long long lt = (1ull << lane) - 1ull;
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const flo
         const int q = p + 4 < pend ? p + 4 : p;   // second centroid (a repeat of the first when absent)
         const float* c0 = new_xyz + ((size_t)b * m + p) * 3;
         const float* c1 = new_xyz + ((size_t)b * m + q) * 3;
-        const f32x2 cx = {c0[0], c1[0]}, cy = {c0[1], c1[1]}, cz = {c0[2], c1[2]};
+        const f32x2 cx = {ld1(c0), ld1(c1)}, cy = {ld1(c0 + 1), ld1(c1 + 1)}, cz = {ld1(c0 + 2), ld1(c1 + 2)};
         int* oa0 = idxa + ((size_t)b * m + p) * nsa;
         int* oa1 = idxa + ((size_t)b * m + q) * nsa;
         int* ob0 = NR > 1 ? idxb + ((size_t)b * m + p) * nsb : nullptr;
@@ -240,10 +240,11 @@ __global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const flo
 #pragma clang fp contract(off)
                 float px, py, pz;
                 if constexpr (LDSP) {
-                    const f32x4 v = sp[k];
+                    f32x4 v = sp[k];
+                    asm volatile("" : "+v"(v));   // one 16-byte LDS read: no 12-byte loads (gp_common.h ld1)
                     px = v.x; py = v.y; pz = v.z;
                 } else {
-                    px = pts[3 * k + 0]; py = pts[3 * k + 1]; pz = pts[3 * k + 2];
+                    px = ld1(pts + 3 * k + 0); py = ld1(pts + 3 * k + 1); pz = ld1(pts + 3 * k + 2);
                 }
                 const f32x2 dx = cx - f32x2{px, px}, dy = cy - f32x2{py, py}, dz = cz - f32x2{pz, pz};
                 d2 = (dx * dx + dy * dy) + dz * dz;
@@ -264,7 +265,11 @@ int gp_launch_ball_query2(int b, int n, int m, float ra, float rb, int nsa, int 
                           hipStream_t st) {
     const float r2a = ra * ra, r2b = rb * rb;  // radius2 = radius * radius in fp32
     dim3 grid((m + 4 * BQ_CPW - 1) / (4 * BQ_CPW), b);
+#ifdef GP_BQ_NO_LDS   // diagnostic builds only: every point read from global memory
+    const bool lds = false;
+#else
     const bool lds = n <= BQ_LDS_MAX;
+#endif
     const size_t bytes = lds ? sizeof(f32x4) * (size_t)n : 0;
 #define GP_BQ(NR, L) hipLaunchKernelGGL((ball_query_kernel<NR, L>), grid, dim3(256), bytes, st, n, m, new_xyz, xyz, \
                                         r2a, NR > 1 ? r2b : 0.f, nsa, NR > 1 ? nsb : 0, idxa, NR > 1 ? idxb : nullptr)

@@ -344,9 +344,9 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_denoise_kernel(OdeDenoiseArg
         for (int j = 0; j < 9; ++j) v[j] = xm[tid * 9 + j];
         gram_schmidt6<double>(v);
         const float* cen = a.center + (size_t)obj[tid] * 3;
-        v[6] += (double)cen[0];
-        v[7] += (double)cen[1];
-        v[8] += (double)cen[2];
+        v[6] += (double)ld1(cen);
+        v[7] += (double)ld1(cen + 1);
+        v[8] += (double)ld1(cen + 2);
         quat_from_gs<double>(v, qq);
 #pragma unroll
         for (int j = 0; j < 9; ++j) a.pose[(size_t)r * 9 + j] = v[j];

@@ -230,7 +230,8 @@ __device__ __forceinline__ void pc_update_rows(const PCArgs& a, int i, const PCS
             x3[k] = mean[k] + gs * z2v[k];
         }
         gram_schmidt6_quad(x3, p, lane);
-        const float* cen = a.center + (size_t)(r / a.kper) * 3;
+        const float* cp = a.center + (size_t)(r / a.kper) * 3;
+        const float cen[3] = {ld1(cp), ld1(cp + 1), ld1(cp + 2)};
         if (a.xs) {
             float* o = a.xs + ((size_t)r * a.steps + (i - 1)) * 9 + e0;
 #pragma unroll
@@ -378,10 +379,10 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
             const size_t e = (size_t)min(r0 + 16 * g + (lane >> 2), a.rows - 1) * 9 + e0;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                x3[k] = a.x[e + k];
-                sv[k] = a.s[e + k];
-                z1v[k] = z1p[e + k];
-                z2v[k] = z2p[e + k];
+                x3[k] = ld1(a.x + e + k);
+                sv[k] = ld1(a.s + e + k);
+                z1v[k] = ld1(z1p + e + k);
+                z2v[k] = ld1(z2p + e + k);
             }
         }
         // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); unused at i=0
@@ -534,7 +535,7 @@ __global__ __launch_bounds__(WV * 64) void pc_persist_kernel(PCArgs a, PCPersist
             PCStep prev = {};
             if (i > 0) {
                 const float* tp = pp.tab + (size_t)(i - 1) * 5;
-                prev = PCStep{tp[0], tp[1], tp[2], tp[3], tp[4]};
+                prev = PCStep{ld1(tp), ld1(tp + 1), ld1(tp + 2), ld1(tp + 3), ld1(tp + 4)};
             }
             // x: from the input at i = 0, then from xin, which holds the update's result for every valid row
             // (the trunk only reads it), so no register carries it across the trunk
@@ -543,14 +544,14 @@ __global__ __launch_bounds__(WV * 64) void pc_persist_kernel(PCArgs a, PCPersist
                 const int cc = min(c_row, ROWS - 1);
                 const size_t e = (size_t)min(r0 + c_row, a.rows - 1) * 9 + e0;
 #pragma unroll
-                for (int k = 0; k < 3; ++k) x3[k] = i == 0 ? a.x[e + k] : sm.xin[cc * 16 + e0 + k];
+                for (int k = 0; k < 3; ++k) x3[k] = i == 0 ? ld1(a.x + e + k) : sm.xin[cc * 16 + e0 + k];
                 const float* z1p = a.z1 + (size_t)(i > 0 ? i - 1 : 0) * a.rows * 9;
                 const float* z2p = a.z2 + (size_t)(i > 0 ? i - 1 : 0) * a.rows * 9;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     sv[k] = s_l[cc * 9 + e0 + k];
-                    z1v[k] = inj ? z1p[e + k] : z_l[(i - 1) & 1][0][cc * 9 + e0 + k];
-                    z2v[k] = inj ? z2p[e + k] : z_l[(i - 1) & 1][1][cc * 9 + e0 + k];
+                    z1v[k] = inj ? ld1(z1p + e + k) : z_l[(i - 1) & 1][0][cc * 9 + e0 + k];
+                    z2v[k] = inj ? ld1(z2p + e + k) : z_l[(i - 1) & 1][1][cc * 9 + e0 + k];
                 }
             }
             const float gacc = i > 0 ? pc_gather_norms(pp.gran + (size_t)((i - 1) & 1) * a.nwg, pp.cnt, a.nwg, (uint32_t)i,
@@ -562,7 +563,7 @@ __global__ __launch_bounds__(WV * 64) void pc_persist_kernel(PCArgs a, PCPersist
         }
         if (i == steps) break;
         const float* tc = pp.tab + (size_t)i * 5;
-        const PCStep cur = PCStep{tc[0], tc[1], tc[2], tc[3], tc[4]};
+        const PCStep cur = PCStep{ld1(tc), ld1(tc + 1), ld1(tc + 2), ld1(tc + 3), ld1(tc + 4)};
         if (wid >= NT && !inj)
             pc_make_draws<NT, WV>(a, i, r0, [&](int st, int c, int e, float v) { z_l[i & 1][st][c * 9 + e] = v; });
         if constexpr (SPLIT)
@@ -795,9 +796,9 @@ __global__ void pose_epilogue_f64_kernel(double* pose, int rows, int kper, const
     for (int j = 0; j < 9; ++j) v[j] = pose[(size_t)r * 9 + j];
     gram_schmidt6<double>(v);
     const float* c = center + (size_t)(r / kper) * 3;
-    v[6] += (double)c[0];
-    v[7] += (double)c[1];
-    v[8] += (double)c[2];
+    v[6] += (double)ld1(c);
+    v[7] += (double)ld1(c + 1);
+    v[8] += (double)ld1(c + 2);
     double qq[4];
     quat_from_gs<double>(v, qq);
     for (int j = 0; j < 9; ++j) pose[(size_t)r * 9 + j] = v[j];

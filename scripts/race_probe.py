@@ -363,6 +363,7 @@ def snap_worker(w, nprocs, reps, outdir):
                                        ws.numel(), ctypes.c_void_p(views[lv].data_ptr()), st))
             if lv == 0:   # level 0's inputs as the MLP saw them (Q0 is reused by level 1 for its row maxima)
                 q0_off = (int(off[4 * 5 + 4]) + B * 1024 * 4 + 255) // 256 * 256
+                snaps["after0_pts"] = pts.clone()   # the input itself, after the level-0 kernels read it
                 snaps["after0_q0"] = ws[q0_off:q0_off + B * N * 48 * 4].clone()
                 snaps["after0_ball0"] = ws[int(off[2]):int(off[2]) + B * 512 * 16 * 4].clone()
                 snaps["after0_ball1"] = ws[int(off[3]):int(off[3]) + B * 512 * 32 * 4].clone()
@@ -401,6 +402,26 @@ def snap_worker(w, nprocs, reps, outdir):
             rec["q0_rows"] = info
             if B <= 8 and sum(1 for x in log if x["differ"]) < 3:
                 np.savez(os.path.join(outdir, f"race_snap_q0_w{w}_r{r}.npz"), got=qa, first=qf)
+        if "after0_ball0" in diff:   # which centroids' lists changed, and how
+            ga = snaps["after0_ball0"].view(torch.int32).view(B, 512, 16).cpu().numpy()
+            gf = first["after0_ball0"].view(torch.int32).view(B, 512, 16).cpu().numpy()
+            rows = np.argwhere((ga != gf).any(-1))
+            rec["ball0_rows"] = int(len(rows))
+            rec["ball0_first_rows"] = rows[:8].tolist()
+            rec["ball0_got_first"] = [[ga[tuple(r)].tolist(), gf[tuple(r)].tolist()] for r in rows[:3]]
+            # per object: the points in one list but not the other, over all its differing rows
+            moved = {}
+            for bb, mm in rows:
+                d = set(ga[bb, mm].tolist()) ^ set(gf[bb, mm].tolist())
+                moved.setdefault(int(bb), set()).update(int(x) for x in d)
+            rec["ball0_moved_points"] = {k: sorted(v)[:24] for k, v in list(moved.items())[:12]}
+        if "after0_pts" in diff:
+            pa = snaps["after0_pts"].cpu().numpy().reshape(-1)
+            pf = first["after0_pts"].cpu().numpy().reshape(-1)
+            bad = np.nonzero(pa != pf)[0]
+            rec["pts_bad_floats"] = bad[:32].tolist()
+            rec["pts_got"] = pa[bad[:8]].tolist()
+            rec["pts_first"] = pf[bad[:8]].tolist()
         if "after0_l0" in diff:
             a0 = snaps["after0_l0"].view(B, 512, 96).cpu().numpy()
             f0 = first["after0_l0"].view(B, 512, 96).cpu().numpy()

@@ -103,6 +103,35 @@ def test_no_vector_loads_from_the_kernel_argument_segment():
     assert not bad, "\n".join(bad)
 
 
+def test_no_12_byte_global_loads():
+    """No kernel of the library reads memory with a 12-byte load (global/buffer/flat_load_dwordx3, ds_read_b96).
+    Under other processes' kernels on the same GPU such a load now and then handed a wave a wrong second dword
+    -- the level-0 projection lost its y term, then (with the projection fixed) the ball lists of levels 0-3
+    changed from run to run: the round-4 multirank mismatch, DESIGN (c). Every 3-float read goes through
+    gp_common.h ld1 (three 4-byte loads the compiler cannot merge). Scans the disassembly of every gfx950
+    kernel."""
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    import tempfile
+    cos = _gfx950_code_objects(os.path.join(REPO, "genpose2_amd", "libgenpose_hip.so"))
+    assert cos, "no gfx950 code object in the library"
+    bad, kernels = [], 0
+    for co in cos:
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            dis = subprocess.run([objdump, "-d", "--mcpu=gfx950", f.name], capture_output=True, text=True, check=True).stdout
+        for fn, body in re.findall(r"^[0-9a-f]+ <(\w+)>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", dis, re.M | re.S):
+            kernels += 1
+            for line in body.split("\n"):
+                ins = line.split("//")[0].strip().split()
+                if ins and re.match(r"((global|buffer|flat)_load_dwordx3|ds_read_b96)$", ins[0]):
+                    bad.append(f"{fn}: {' '.join(ins)}")
+    assert kernels > 20
+    assert not bad, "\n".join(bad[:20])
+
+
 def test_invalid_arguments_return_status_not_exit():
     from genpose2_amd import _lib
     lib = _lib.load()
