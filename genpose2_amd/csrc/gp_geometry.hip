@@ -164,7 +164,6 @@ int gp_launch_fps_chain(const float* xyz, int b, int nlev, const int* n, const i
 // ============================================================================ ball query
 // NR radii (1 or 2) answered by the same scan.
 constexpr int BQ_CPW = 8;
-constexpr int BQ_LDS_MAX = 4096;
 // Scan state of one centroid: hits so far and the first hit, per radius.
 struct BqState {
     int cnta, cntb, firsta, firstb;
@@ -203,23 +202,20 @@ __device__ __forceinline__ void bq_pad(int lane, int nsa, int nsb, int* oa, int*
 
 // One wave scans two centroids at once (p and p + 4): the distances of a point to both are packed fp32
 // operations (v_pk_add_f32 / v_pk_mul_f32), each rounded exactly as dist2_ref. 4 * BQ_CPW centroids of one
-// object per workgroup. LDSP: the object's points are staged in LDS once per workgroup as (x, y, z, 0);
-// used while they fit (n <= BQ_LDS_MAX).
+// object per workgroup. The points are read from global memory (L1/L2-resident: 12 B x n per object), NOT
+// staged in LDS: with several processes time-sharing the GPU the LDS-staged point set intermittently gave
+// wrong ball lists (points dropping out of balls) while the identical global-memory kernel stayed
+// bit-exact (DESIGN (c), profiles/r5/race_probe_history.md).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <int NR, bool LDSP>
+template <int NR>
 __global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const float* __restrict__ new_xyz,
                                                          const float* __restrict__ xyz, float r2a,
                                                          float r2b, int nsa, int nsb,
                                                          int* __restrict__ idxa,
                                                          int* __restrict__ idxb) {
-    extern __shared__ __attribute__((aligned(16))) f32x4 sp[];
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const float* pts = xyz + (size_t)b * n * 3;
-    if constexpr (LDSP) {
-        for (int i = threadIdx.x; i < n; i += 256) sp[i] = f32x4{ld1(pts + 3 * i), ld1(pts + 3 * i + 1), ld1(pts + 3 * i + 2), 0.f};
-        __syncthreads();
-    }
     const unsigned long long lt = (1ull << lane) - 1ull;
     const int pend = min(m, (int)(blockIdx.x + 1) * 4 * BQ_CPW);
     for (int p = blockIdx.x * 4 * BQ_CPW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); p < pend; p += 8) {
@@ -238,14 +234,7 @@ __global__ __launch_bounds__(256) void ball_query_kernel(int n, int m, const flo
             f32x2 d2 = {3.0e38f, 3.0e38f};
             if (k < n) {
 #pragma clang fp contract(off)
-                float px, py, pz;
-                if constexpr (LDSP) {
-                    f32x4 v = sp[k];
-                    asm volatile("" : "+v"(v));   // one 16-byte LDS read: no 12-byte loads (gp_common.h ld1)
-                    px = v.x; py = v.y; pz = v.z;
-                } else {
-                    px = ld1(pts + 3 * k + 0); py = ld1(pts + 3 * k + 1); pz = ld1(pts + 3 * k + 2);
-                }
+                const float px = ld1(pts + 3 * k + 0), py = ld1(pts + 3 * k + 1), pz = ld1(pts + 3 * k + 2);
                 const f32x2 dx = cx - f32x2{px, px}, dy = cy - f32x2{py, py}, dz = cz - f32x2{pz, pz};
                 d2 = (dx * dx + dy * dy) + dz * dz;
             }
@@ -265,20 +254,11 @@ int gp_launch_ball_query2(int b, int n, int m, float ra, float rb, int nsa, int 
                           hipStream_t st) {
     const float r2a = ra * ra, r2b = rb * rb;  // radius2 = radius * radius in fp32
     dim3 grid((m + 4 * BQ_CPW - 1) / (4 * BQ_CPW), b);
-#ifdef GP_BQ_NO_LDS   // diagnostic builds only: every point read from global memory
-    const bool lds = false;
-#else
-    const bool lds = n <= BQ_LDS_MAX;
-#endif
-    const size_t bytes = lds ? sizeof(f32x4) * (size_t)n : 0;
-#define GP_BQ(NR, L) hipLaunchKernelGGL((ball_query_kernel<NR, L>), grid, dim3(256), bytes, st, n, m, new_xyz, xyz, \
-                                        r2a, NR > 1 ? r2b : 0.f, nsa, NR > 1 ? nsb : 0, idxa, NR > 1 ? idxb : nullptr)
-    if (idxb) {
-        if (lds) GP_BQ(2, true); else GP_BQ(2, false);
-    } else {
-        if (lds) GP_BQ(1, true); else GP_BQ(1, false);
-    }
-#undef GP_BQ
+    if (idxb)
+        hipLaunchKernelGGL((ball_query_kernel<2>), grid, dim3(256), 0, st, n, m, new_xyz, xyz, r2a, r2b, nsa, nsb, idxa, idxb);
+    else
+        hipLaunchKernelGGL((ball_query_kernel<1>), grid, dim3(256), 0, st, n, m, new_xyz, xyz, r2a, 0.f, nsa, 0, idxa,
+                           nullptr);
     return gp_check_launch("ball_query_kernel");
 }
 
