@@ -46,7 +46,8 @@ template <int NT, int WV, int PL = 0>
 struct HeadSmem {
     // 64-candidate tiles (NT = 4) alias pose_encoder.2's output onto pose_encoder.0's (written after
     // a barrier that retires every read of act1), so one workgroup still fits the 160 KiB of a CU
-    static constexpr bool kAliasAct = NT >= 4;
+    // (also the f16x3 trunk of 4-wave workgroups: two of them share a CU, PC_PAIR)
+    static constexpr bool kAliasAct = NT >= 4 || (PL != 0 && WV <= 4);
     static constexpr int kAct = PL ? (HID / 32) * NT * PL * 64 : KG_HID * NT * 64;   // 16-byte entries
     float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
     f32x4 act1[kAct];                  // pose_encoder.0 output: [g][ct][lane] (fp32) / [chunk][ct][plane][lane]
@@ -371,21 +372,23 @@ __device__ __forceinline__ void stream_hk_step(__amdgpu_buffer_rsrc_t W, const i
 // on the critical path between the PC update and pose_encoder.0.
 // Also this wave's pose_encoder.0 A fragments and bias (output tiles 2 wid, 2 wid + 1 of an 8-wave
 // workgroup): loaded at kernel entry instead of being staged through LDS for every launch.
-constexpr int HSPLIT_WV = 8;   // waves per workgroup of every split-trunk kernel
+constexpr int HSPLIT_WV = 8;   // waves per workgroup of the split-trunk kernels (the paired PC step: 4)
 struct SplitScalars {
     float A0, B0, A2, B2;
     int ew2, ewh;
-    f32x4 pe0a[16 / HSPLIT_WV], pe0b[16 / HSPLIT_WV];
+    f32x4 pe0a[4], pe0b[4];   // this wave's 16 / WV output tiles (entries past them unused)
 };
+template <int WV = HSPLIT_WV>
 __device__ __forceinline__ SplitScalars load_split_scalars(const gp_head_weights& w) {
+    static_assert(WV == 4 || WV == 8, "the split trunk runs 4- or 8-wave workgroups");
     const f32x4 a = ld4(w.hsc), b = ld4(w.hsc + 4);
     SplitScalars r{a.x, a.y, a.z, a.w, (int)b.x, (int)b.y, {}, {}};
     const int tid = tid_x();
     const int lane = tid & 63, q = lane >> 4;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
-    for (int t = 0; t < 16 / HSPLIT_WV; ++t) {
-        const int T = wid * (16 / HSPLIT_WV) + t;
+    for (int t = 0; t < 16 / WV; ++t) {
+        const int T = wid * (16 / WV) + t;
         r.pe0a[t] = ld4(w.pe0_w + ((size_t)T * 64 + lane) * 4);
         r.pe0b[t] = ld4(w.pe0_b + 16 * T + 4 * q);
     }
@@ -734,7 +737,7 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
                                               HeadSmem<NT, WV, X3P>& sm, int trace_slot, const SplitScalars hs) {
     constexpr int TPW = 16 / WV;   // output tiles per wave and 256-wide layer; tiles (2c, 2c+1) form chunk c
     static_assert(TPW % 2 == 0, "the f16x3 trunk pairs a wave's output tiles into 32-deep chunks");
-    static_assert(WV == HSPLIT_WV, "SplitScalars carries the pose_encoder.0 fragments of HSPLIT_WV waves");
+    static_assert(TPW <= 4, "SplitScalars carries at most four pose_encoder.0 tiles per wave");
     constexpr int CPW = TPW / 2;
     using SM = HeadSmem<NT, WV, X3P>;
     const int tid = tid_x();

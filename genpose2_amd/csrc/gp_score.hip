@@ -345,7 +345,8 @@ __device__ __forceinline__ float pc_score_norm(const PCArgs& a, const PCStep& cu
 // grad-norm reduction overlap), while the other waves make the next step's draws, stage the small
 // weights and issue their first weight-stream loads; one barrier (inside the trunk) joins them.
 template <int NT, int WV, int PL>   // PL 0: exact fp32 GEMMs, X3P: f16x3
-__global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
+__global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(2))) void pc_step_kernel(PCArgs a, int i,
+                                                                                                PCStep cur, PCStep prev) {
     constexpr int ROWS = NT * 16;
     static_assert(NT < WV, "at least one wave besides the update waves");
     __shared__ HeadSmem<NT, WV, PL> sm;
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     const int r0 = blockIdx.x * ROWS;
     const int trace_slot = i & 1;
     SplitScalars hs = {};
-    if constexpr (SPLIT) hs = load_split_scalars(a.w);   // in flight across the update
+    if constexpr (SPLIT) hs = load_split_scalars<WV>(a.w);   // in flight across the update
     PC_MARK(0);
     if (wid < NT) {
         // ---- every load first and unconditional (rows clamped: a guarded load becomes a branch,
@@ -610,7 +611,21 @@ extern "C" size_t gp_pc_workspace_size(int rows) {
     return sizeof(float) * ((size_t)rows * 9 * 5 + 2 * ntiles) + 256;
 }
 
-static int pc_pick_nt(int rows, bool split) { return head_pick_nt(rows, split); }
+// PC_PAIR: where the f16x3 path would take 64-candidate workgroups of 8 waves, take 32-candidate workgroups
+// of 4 waves instead, two per CU (pc_step_kernel<2, 4, X3P>: <= 256 VGPRs, ~68 KiB of LDS each). The two
+// workgroups on a CU run independently, so one's serial VALU phases (update, pose_encoder.0, epilogues) overlap
+// the other's MFMA stream (scripts/mix16_probe.hip: f32 VALU beside f16 MFMA leaves the MFMA rate unchanged),
+// at the price of streaming the GEMM weights once per 32 instead of 64 candidates. GENPOSE2_PC_PAIR=0/1
+// overrides the build default.
+#ifndef PC_PAIR_DEFAULT
+#define PC_PAIR_DEFAULT 0
+#endif
+static bool pc_pair(int rows, bool split) {
+    if (!split || head_pick_nt(rows, split) != 4) return false;
+    const char* env = getenv("GENPOSE2_PC_PAIR");
+    return env ? env[0] != '0' : PC_PAIR_DEFAULT != 0;
+}
+static int pc_pick_nt(int rows, bool split) { return pc_pair(rows, split) ? 2 : head_pick_nt(rows, split); }
 
 // The persistent sampler (pc_persist_kernel) runs when enabled (GENPOSE2_PC_PERSIST, default PC_PERSIST_DEFAULT),
 // when every workgroup fits on the device at once (nwg <= compute units: the grid-wide exchange waits for all of
@@ -726,6 +741,7 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     // split-f16 GEMMs when the packed planes are given (gp_head_weights), exact fp32 otherwise
     const bool split = w->pe2_h != nullptr;
     const int nt = pc_pick_nt(rows, split);
+    const bool pair = pc_pair(rows, split);
     GP_REQUIRE(!split || (w->h1p_h && w->hsc), "pc_sample: pe2_h, h1p_h and hsc must be given together");
     PCArgs a;
     a.w = *w;
@@ -749,7 +765,7 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     a.ls_coef = snr * 3.0f;  // snr * sqrt(pose_dim=9) in fp32 (0.48 rounds identically)
     const dim3 grid(a.nwg);
     PCPersist pp;
-    if (pc_persist_layout(a, rows, steps, pp)) {
+    if (!pair && pc_persist_layout(a, rows, steps, pp)) {
         // one launch for the whole loop (pc_persist_kernel): the step table and zeroed granules in the workspace
         if (hipMemsetAsync(pp.gran, 0, reinterpret_cast<const char*>(pp.tab) - reinterpret_cast<char*>(pp.gran), stream) !=
             hipSuccess)
@@ -776,6 +792,8 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
                                  step_tab[5 * (i - 1) + 3], step_tab[5 * (i - 1) + 4]};
         if (nt == 4)
             hipLaunchKernelGGL((pc_step_kernel<4, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+        else if (pair)
+            hipLaunchKernelGGL((pc_step_kernel<2, 4, X3P>), grid, dim3(4 * 64), 0, stream, a, i, cur, prev);
         else if (nt == 2 && split)
             hipLaunchKernelGGL((pc_step_kernel<2, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else if (nt == 2)
