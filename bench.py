@@ -550,6 +550,8 @@ def main():
             a.heads.set_arith("f32")
             if hasattr(a.encoder, "set_arith"):
                 a.encoder.set_arith("f32")
+            if getattr(a, "img_encoder", None) is not None:
+                a.img_encoder.set_arith("f32")
         n_ev = len(samp_ev)
         one_step(last=True)
         torch.cuda.synchronize(dev)
@@ -572,6 +574,8 @@ def main():
             a.heads.set_arith("f16x3")
             if hasattr(a.encoder, "set_arith"):
                 a.encoder.set_arith("split_f16")
+            if getattr(a, "img_encoder", None) is not None:
+                a.img_encoder.set_arith("split_f16")
         us32 = ms32 / 1e3 / (T + 1) * 1e6
         fl = B * K * arch.score_flops_per_candidate_step()
         k32 = f"void pc_step_kernel<{int(_tile_rows(B * K, False)) // 16}, 8, 0>"
@@ -612,7 +616,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": ("f32 (pose_encoder.2 / head-1 GEMMs: f16x3 -- three f16 planes per fp32 operand, six MFMA "
-                      "products, products to 2^-33, fp32 accumulation; encoder SA levels 1-3: split-f16)") if fast else "f32",
+                      "products, products to 2^-33, fp32 accumulation; encoder SA levels 1-3: split-f16, per-level error "
+                      "vs float64 within exact fp32 MFMA's: tests/test_gpu_precision.py)") if fast else "f32",
             "data": "synthetic (seeded point clouds, seeded synthetic weights; no checkpoint exists for dino=none)",
             "config": {"workload": f"config{args.config}: B={B} objects/GPU, N={N} pts, K={K} candidates, T={T} PC "
                                    f"steps, {'ScoreNet+EnergyNet+ranking/aggregation' if cfgd['energy'] else 'ScoreNet'}"

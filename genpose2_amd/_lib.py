@@ -112,6 +112,9 @@ _SIGS: Dict[str, tuple] = {
     "gp_img_encoder": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
                                c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_size_t, c_void_p]),
+    "gp_img_encoder2": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
+                                c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_size_t, c_void_p]),
     "gp_img_geo_table": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "gp_gather_patch_points": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_void_p, c_void_p]),

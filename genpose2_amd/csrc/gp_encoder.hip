@@ -500,7 +500,6 @@ template <int CT, int KC0, int NC, int D>
 __device__ __forceinline__ void split_layer1(const SplitArgs& a, f16x8* X, int* e0s, float* pm, const f32x4* P4,
                                              int b, int col0, int wid, int lane, int oc1, int (&e1)[CT],
                                              f32x4 (&gq)[KC0][2], bool loaded, int pnb) {
-    constexpr int C = 16 * CT;
     const int q = lane >> 4, n = lane & 15;
     float pmax[CT];
 #pragma unroll

@@ -266,7 +266,7 @@ namespace {
 constexpr int IE_EDGE_CHUNK = 32;   // objects per im2col GEMM (col: chunk * np * 9d floats)
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 struct ImgLayout {
-    size_t h, fused, s, ft, o, col, ey, edge, total;
+    size_t h, fused, s, ft, o, col, ey, edge, rmax, total;
 };
 ImgLayout img_layout(int b, int np, int d) {
     ImgLayout L = {};
@@ -280,6 +280,7 @@ ImgLayout img_layout(int b, int np, int d) {
     L.col = off;   off += al256(sizeof(float) * (size_t)chunk * np * 9 * d);
     L.ey = off;    off += al256(sizeof(float) * (size_t)chunk * np * co);
     L.edge = off;  off += al256(sizeof(float) * (size_t)b * co);
+    L.rmax = off;  off += al256(sizeof(float) * (size_t)b * np);   // split GEMMs: per-token row maxima
     L.total = off;
     return L;
 }
@@ -289,11 +290,19 @@ extern "C" size_t gp_img_encoder_workspace_size(int b, int np, int d) {
     return b >= 1 && np >= 1 && d >= 4 ? img_layout(b, np, d).total : 0;
 }
 
-extern "C" int gp_img_encoder(const float* l0, const float* l1, const float* l2, int b, int np, int d,
-                              const float* la_w1, const float* la_b1, const float* la_w2, float la_b2,
-                              const float* geo_table, const float* conv_w, const float* conv_b, float geo_gate,
-                              float edge_gate, float* out, float* layer_w, float* edge_out, void* workspace,
-                              size_t workspace_bytes, hipStream_t st) {
+// y = relu(x W^T + b): split-f16 (gp_linear_split, the token linears' arithmetic: per-token power-of-two scaling,
+// three f16 products) when the weight planes are given, exact fp32 MFMA (gp_linear) otherwise
+static int img_linear_relu(const float* x, int m, int k, const float* w, const int32_t* wh, const float* bias, int n,
+                           float* y, float* rmax, hipStream_t st) {
+    if (wh) return gp_linear_split(x, k, m, k, wh, bias, n, 1, y, n, rmax, 0, nullptr, st);
+    return gp_linear(x, k, m, k, w, bias, n, 1, y, n, st);
+}
+
+extern "C" int gp_img_encoder2(const float* l0, const float* l1, const float* l2, int b, int np, int d,
+                               const float* la_w1, const float* la_b1, const float* la_w2, float la_b2,
+                               const float* geo_table, const float* conv_w, const float* conv_b, float geo_gate,
+                               float edge_gate, const int32_t* la_w1_h, const int32_t* conv_w_h, float* out,
+                               float* layer_w, float* edge_out, void* workspace, size_t workspace_bytes, hipStream_t st) {
     GP_REQUIRE(l0 && l1 && l2 && la_w1 && la_b1 && la_w2 && geo_table && conv_w && conv_b && out && workspace,
                "img_encoder: null pointer");
     GP_REQUIRE(b >= 0 && np >= 4 && d % 64 == 0, "img_encoder: need np >= 4 and d a multiple of 64 (d=%d)", d);
@@ -312,12 +321,14 @@ extern "C" int gp_img_encoder(const float* l0, const float* l1, const float* l2,
     float* col = reinterpret_cast<float*>(ws + L.col);
     float* ey = reinterpret_cast<float*>(ws + L.ey);
     float* edge = edge_out ? edge_out : reinterpret_cast<float*>(ws + L.edge);
+    float* rmax = reinterpret_cast<float*>(ws + L.rmax);
     const int T = b * np, hid = d / 2, co = d / 4;
     int rc;
     // 1. layer attention: Linear(d, d/2) + ReLU over each layer's tokens, then the fuse kernel
     const float* layers[3] = {l0, l1, l2};
     for (int l = 0; l < 3; ++l)
-        if ((rc = gp_linear(layers[l], d, T, d, la_w1, la_b1, hid, 1, h + (size_t)l * T * hid, hid, st))) return rc;
+        if ((rc = img_linear_relu(layers[l], T, d, la_w1, la_w1_h, la_b1, hid, h + (size_t)l * T * hid, rmax, st)))
+            return rc;
     hipLaunchKernelGGL(imgenc_layer_fuse_kernel, dim3((T + 3) / 4), dim3(IE_THREADS), 0, st, (const float*)h, hid,
                        la_w2, la_b2, l0, l1, l2, T, d, fused, layer_w);
     if ((rc = gp_check_launch("imgenc_layer_fuse_kernel"))) return rc;
@@ -327,7 +338,7 @@ extern "C" int gp_img_encoder(const float* l0, const float* l1, const float* l2,
         hipLaunchKernelGGL(imgenc_im2col_kernel, dim3(nb * np), dim3(IE_THREADS), 0, st,
                            (const float*)(fused + (size_t)c0 * np * d), np, g, d, col);
         if ((rc = gp_check_launch("imgenc_im2col_kernel"))) return rc;
-        if ((rc = gp_linear(col, 9 * d, nb * np, 9 * d, conv_w, conv_b, co, 1, ey, co, st))) return rc;
+        if ((rc = img_linear_relu(col, nb * np, 9 * d, conv_w, conv_w_h, conv_b, co, ey, rmax, st))) return rc;
         hipLaunchKernelGGL(imgenc_pool_kernel, dim3((nb * co + 255) / 256), dim3(256), 0, st, (const float*)ey, nb, np,
                            co, edge + (size_t)c0 * co);
         if ((rc = gp_check_launch("imgenc_pool_kernel"))) return rc;
@@ -349,4 +360,13 @@ extern "C" int gp_img_encoder(const float* l0, const float* l1, const float* l2,
                        st, (const float*)fused, (const float*)o, (const float*)edge, np, d, co, geo_gate, edge_gate, n,
                        out);
     return gp_check_launch("imgenc_combine_kernel");
+}
+
+extern "C" int gp_img_encoder(const float* l0, const float* l1, const float* l2, int b, int np, int d,
+                              const float* la_w1, const float* la_b1, const float* la_w2, float la_b2,
+                              const float* geo_table, const float* conv_w, const float* conv_b, float geo_gate,
+                              float edge_gate, float* out, float* layer_w, float* edge_out, void* workspace,
+                              size_t workspace_bytes, hipStream_t st) {
+    return gp_img_encoder2(l0, l1, l2, b, np, d, la_w1, la_b1, la_w2, la_b2, geo_table, conv_w, conv_b, geo_gate,
+                           edge_gate, nullptr, nullptr, out, layer_w, edge_out, workspace, workspace_bytes, st);
 }

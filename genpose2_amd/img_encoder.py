@@ -14,6 +14,7 @@ with torch's own row sums, as the reference computes it.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -36,10 +37,16 @@ def geo_table(sd: weights.StateDict, prefix: str = "img_encoder", grid: int = ar
 
 
 def pack_img_encoder(sd: weights.StateDict, prefix: str = "img_encoder") -> Dict[str, np.ndarray]:
+    """Device buffers of gp_img_encoder2: the fp32 weights as stored, plus the layer-attention Linear and the edge
+    conv (as its (d/4, 9d) im2col rows) in gp_linear_split's split-f16 layout (``*_h``)."""
+    from .fus_encoder import pack_split_linear
     g = lambda k: np.ascontiguousarray(sd[f"{prefix}.{k}"], dtype=np.float32)  # noqa: E731
-    return {"la_w1": g("layer_attn.0.weight"), "la_b1": g("layer_attn.0.bias"),
-            "la_w2": g("layer_attn.2.weight").reshape(-1), "geo_table": geo_table(sd, prefix),
-            "conv_w": g("edge_guide.0.weight"), "conv_b": g("edge_guide.0.bias")}
+    out = {"la_w1": g("layer_attn.0.weight"), "la_b1": g("layer_attn.0.bias"),
+           "la_w2": g("layer_attn.2.weight").reshape(-1), "geo_table": geo_table(sd, prefix),
+           "conv_w": g("edge_guide.0.weight"), "conv_b": g("edge_guide.0.bias")}
+    out["la_w1_h"] = pack_split_linear(out["la_w1"])
+    out["conv_w_h"] = pack_split_linear(out["conv_w"].reshape(out["conv_w"].shape[0], -1))
+    return out
 
 
 def pack_img_scalars(sd: weights.StateDict, prefix: str = "img_encoder") -> np.ndarray:
@@ -62,6 +69,14 @@ class ImgEncoderModel:
         self.t = {k: torch.from_numpy(v).to(device) for k, v in pack_img_encoder(sd).items()}
         self.scalars = pack_img_scalars(sd)
         self._ws: Optional[torch.Tensor] = None
+        self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
+
+    def set_arith(self, arith: str) -> None:
+        """GEMM arithmetic of the layer-attention Linear and the edge conv: "split_f16" (gp_linear_split, as
+        the fused encoder's token linears) or "f32" (exact fp32 MFMA)."""
+        if arith not in ("split_f16", "f32"):
+            raise ValueError(f"unknown encoder arithmetic {arith!r} (split_f16 | f32)")
+        self.arith = arith
 
     @property
     def table(self) -> np.ndarray:
@@ -88,10 +103,13 @@ class ImgEncoderModel:
         lw = torch.empty((B, n, 3), dtype=torch.float32, device=self.device) if return_parts else None
         edge = torch.empty((B, d // 4), dtype=torch.float32, device=self.device) if return_parts else None
         b2, gg, eg = (float(v) for v in self.scalars)
-        check(self.lib.gp_img_encoder(_vp(ls[0]), _vp(ls[1]), _vp(ls[2]), B, n, d, _vp(self.t["la_w1"]),
-                                      _vp(self.t["la_b1"]), _vp(self.t["la_w2"]), b2, _vp(self.t["geo_table"]),
-                                      _vp(self.t["conv_w"]), _vp(self.t["conv_b"]), gg, eg, _vp(out), _vp(lw),
-                                      _vp(edge), _vp(self._ws), self._ws.numel(), self._s()), "img_encoder")
+        split = self.arith == "split_f16"
+        check(self.lib.gp_img_encoder2(_vp(ls[0]), _vp(ls[1]), _vp(ls[2]), B, n, d, _vp(self.t["la_w1"]),
+                                       _vp(self.t["la_b1"]), _vp(self.t["la_w2"]), b2, _vp(self.t["geo_table"]),
+                                       _vp(self.t["conv_w"]), _vp(self.t["conv_b"]), gg, eg,
+                                       _vp(self.t["la_w1_h"] if split else None),
+                                       _vp(self.t["conv_w_h"] if split else None), _vp(out), _vp(lw),
+                                       _vp(edge), _vp(self._ws), self._ws.numel(), self._s()), "img_encoder")
         if return_parts:
             return out, {"layer_w": lw, "edge": edge}
         return out

@@ -344,6 +344,15 @@ int gp_img_encoder(const float *l0, const float *l1, const float *l2, int b, int
                    const float *geo_table, const float *conv_w, const float *conv_b, float geo_gate,
                    float edge_gate, float *out, float *layer_w, float *edge_out, void *workspace,
                    size_t workspace_bytes, hipStream_t stream);
+/* gp_img_encoder with the layer-attention Linear and the edge conv as split-f16 GEMMs (gp_linear_split's
+ * arithmetic): la_w1_h / conv_w_h are those weights in fus_encoder.pack_split_linear's layout (conv_w as its
+ * (d/4, 9d) rows); NULL runs that GEMM in exact fp32 (gp_img_encoder passes NULL for both). */
+int gp_img_encoder2(const float *l0, const float *l1, const float *l2, int b, int np, int d,
+                    const float *la_w1, const float *la_b1, const float *la_w2, float la_b2,
+                    const float *geo_table, const float *conv_w, const float *conv_b, float geo_gate,
+                    float edge_gate, const int32_t *la_w1_h, const int32_t *conv_w_h, float *out,
+                    float *layer_w, float *edge_out, void *workspace, size_t workspace_bytes,
+                    hipStream_t stream);
 /* HOST: the geometric attention's position table rel_pos_emb(rel_pos_idx).sum(-1) (img_encoder.py:
  * 68-76): table[i][j] = sum_k E[clamp((r_j - r_i + g - 1)(2g - 1) + (c_j - c_i + g - 1), 0, num_emb - 1)][k]
  * for patches i, j at (row, col) = (p / g, p % g). rel_pos_emb (num_emb, edim) host -> table (g^2, g^2)

@@ -3,7 +3,7 @@
 # usage: bash scripts/gpu.sh TAG STEP [STEP ...]; every step writes gpurun_out/TAG_<step>.* and runs
 # under its own time limit; the first failing step ends the call (no GPU work after a failure).
 #   tests            python -m pytest tests -m gpu (thread timeout per test)
-#   tests:EXPR       the same with -k EXPR
+#   tests:EXPR       the same with -k EXPR (commas for spaces: tests:a,or,b)
 #   smoke            __graft_entry__.smoke()
 #   bench[:ARGS]     python bench.py ARGS (comma-separated, e.g. bench:--config,5,--steps,2)
 #   prof[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS (--steps 3 --warmup 1 by default)
@@ -25,7 +25,7 @@ for step in "$@"; do
   echo "[$(date +%T)] step $n: $step" >&2
   case $name in
     tests)
-      K=(); [ -n "$arg" ] && K=(-k "$arg")
+      K=(); [ -n "$arg" ] && K=(-k "${arg//,/ }")   # commas stand for spaces: tests:a,or,b -> -k "a or b"
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${K[@]}" > $out.log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out.log 2>&1 ;;

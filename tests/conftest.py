@@ -30,6 +30,8 @@ def set_arith(agent, arith, encoder=None):
     agent.heads.set_arith("f32" if arith == "f32" else "f16x3")
     if hasattr(agent.encoder, "set_arith"):
         agent.encoder.set_arith("split_f16" if enc == "fast" else "f32")
+    if getattr(agent, "img_encoder", None) is not None:
+        agent.img_encoder.set_arith("split_f16" if enc == "fast" else "f32")
 
 
 def golden(name):

@@ -324,8 +324,9 @@ def test_pointwise_agent_pred_func():
 
 
 # ---------------------------------------------------------------- ImgEncoder + patch gather
+@pytest.mark.parametrize("arith", ["split_f16", "f32"])
 @pytest.mark.parametrize("tag", ["hard", "soft"])
-def test_img_encoder_vs_reference_golden(tag):
+def test_img_encoder_vs_reference_golden(tag, arith):
     """gp_img_encoder against the reference's own ImgEncoder (golden_img.npz, make_golden_img.py): the final
     (B, 256, 384) features, the layer-attention weights and the edge weights within 1e-5 of max|ref|; the
     patch -> point gather (roi pixels out of range included) bit-exact against the gathered golden rows
@@ -336,6 +337,7 @@ def test_img_encoder_vs_reference_golden(tag):
     g = golden("img")
     B, scale, seed = mi.CASES[tag]
     model = ImgEncoderModel(weights.synthetic_state_dict("score_pointwise", seed=0), torch.device(DEV))
+    model.set_arith(arith)   # the layer-attention Linear and the edge conv: split-f16 (default) or exact fp32
     layers = [torch.from_numpy(v).to(DEV) for v in mi.dino_layers(B, scale, seed)]
     final, parts = model.forward(layers, return_parts=True)
     f = final.cpu().numpy()
@@ -343,7 +345,7 @@ def test_img_encoder_vs_reference_golden(tag):
             "layer_w": rel(parts["layer_w"].cpu().numpy().transpose(0, 2, 1), g[f"{tag}_layer_w"]),
             "sum": float(np.abs(f.astype(np.float64).sum(axis=(1, 2)) - g[f"{tag}_final_sum"]).max()
                          / np.abs(g[f"{tag}_final_sum"]).max())}
-    print(tag, errs)
+    print(tag, arith, errs)
     assert max(errs.values()) < 1e-5, errs
     xs, ys = mi.roi_pixels(B, 1024, seed)
     got = model.gather(final, torch.from_numpy(xs), torch.from_numpy(ys)).cpu().numpy()
