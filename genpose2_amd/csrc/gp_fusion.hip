@@ -250,8 +250,9 @@ extern "C" int gp_linear(const float* x, int ldx, int m, int k, const float* w, 
 // (W: one exponent per matrix, packed on the host by pack.pack_h16_fragments; x: per token from its row
 // max |x|, split on the way into LDS) and three v_mfma_f32_16x16x32_f16 products (hi.hi + hi.lo + lo.hi)
 // accumulated in fp32 -- the encoder's split arithmetic (tok_split_gemm_kernel), 16x the MACs per MFMA of
-// the fp32 path. Workgroup: 64*WO outputs x 64*(8/WO) tokens, 8 waves of 64 x 64, two LDS stages of one
-// 32-deep chunk, one barrier per chunk.
+// the fp32 path. Workgroup: 64*WO outputs x 16*JT*(8/WO) tokens, 8 waves of 64 outputs x 16*JT tokens, two
+// LDS stages of one 32-deep chunk, one barrier per chunk. JT = 8 (WO = 4): every A fragment read from LDS
+// feeds 8 token tiles instead of 4, so the LDS traffic per MFMA drops by a third.
 constexpr int SL_THREADS = 512;
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 struct SplitLinArgs {
@@ -265,9 +266,9 @@ struct SplitLinArgs {
     int ldy;
     unsigned* ymax;       // or null: per-row max |y| (bits of a float >= 0 order as unsigned: atomicMax)
 };
-template <int WO>
+template <int WO, int JT = 4>
 constexpr size_t sl_lds_bytes() {
-    return 2 * (size_t)(4 * WO + 4 * (8 / WO)) * 2048 + sizeof(int) * 64 * (8 / WO);
+    return 2 * (size_t)(4 * WO + JT * (8 / WO)) * 2048 + sizeof(int) * 16 * JT * (8 / WO);
 }
 
 __global__ __launch_bounds__(256) void fus_rowmax_kernel(const float* __restrict__ x, int ldx, int m, int k,
@@ -285,10 +286,10 @@ __global__ __launch_bounds__(256) void fus_rowmax_kernel(const float* __restrict
     if (lane == 0) rmax[r] = v;
 }
 
-template <int WO, int ACT>
+template <int WO, int ACT, int JT = 4>
 __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a) {
-    constexpr int WT = 8 / WO, BM = 64 * WT;
-    constexpr int NA = 4 * WO * 128, NB = 4 * WT * 128;   // f16x8 fragments per stage
+    constexpr int WT = 8 / WO, BM = 16 * JT * WT, RU = BM / 64;   // RU: token rows per thread (8 threads a row)
+    constexpr int NA = 4 * WO * 128, NB = JT * WT * 128;   // f16x8 fragments per stage
     extern __shared__ __attribute__((aligned(16))) f16x8 sl_lds[];
     auto sA = [&](int st) { return sl_lds + st * (NA + NB); };
     auto sB = [&](int st) { return sl_lds + st * (NA + NB) + NA; };
@@ -300,10 +301,10 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
     const int g = tid & 7;
     const int ew = a.w[0];
     const f16x8* W = reinterpret_cast<const f16x8*>(a.w + 4);
-    int row[WT];
-    float sc[WT];
+    int row[RU];
+    float sc[RU];
 #pragma unroll
-    for (int u = 0; u < WT; ++u) {
+    for (int u = 0; u < RU; ++u) {
         const int r = (tid + SL_THREADS * u) >> 3;
         row[u] = m0 + r;
         const float mx = row[u] < a.m ? a.rmax[row[u]] : 0.f;
@@ -311,21 +312,21 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
         sc[u] = exp2i(14 - E);
         if (g == 0) eT[r] = E;
     }
-    auto load = [&](int c, f32x4 (&ra)[WO], f32x4 (&rb)[WT]) {
+    auto load = [&](int c, f32x4 (&ra)[WO], f32x4 (&rb)[RU]) {
 #pragma unroll
         for (int u = 0; u < WO; ++u) {
             const int idx = tid + SL_THREADS * u;
             ra[u] = ld4(reinterpret_cast<const float*>(W + ((size_t)(T0 + (idx >> 7)) * KC + c) * 128 + (idx & 127)));
         }
 #pragma unroll
-        for (int u = 0; u < WT; ++u)
+        for (int u = 0; u < RU; ++u)
             rb[u] = row[u] < a.m ? ld4(a.x + (size_t)row[u] * a.ldx + 32 * c + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    auto store = [&](int s, const f32x4 (&ra)[WO], const f32x4 (&rb)[WT]) {
+    auto store = [&](int s, const f32x4 (&ra)[WO], const f32x4 (&rb)[RU]) {
 #pragma unroll
         for (int u = 0; u < WO; ++u) sA(s)[tid + SL_THREADS * u] = __builtin_bit_cast(f16x8, ra[u]);
 #pragma unroll
-        for (int u = 0; u < WT; ++u) {
+        for (int u = 0; u < RU; ++u) {
 #pragma clang fp contract(off)
             const int r = (tid + SL_THREADS * u) >> 3, ln = 16 * (g & 3) + (r & 15), half = g >> 2;
             f16x4 hi, lo;
@@ -341,43 +342,75 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
         }
     };
     const int wo = wid % WO, wt = wid / WO;
-    f32x4 acc[4][4];
+    f32x4 acc[4][JT];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 ra[WO], rb[WT];
+        for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 ra[WO], rb[RU];
     load(0, ra, rb);
     store(0, ra, rb);
     __syncthreads();
     for (int c = 0; c < KC; ++c) {
         const int s = c & 1;
         if (c + 1 < KC) load(c + 1, ra, rb);
-        f16x8 bh[4], bl[4];
+        if constexpr (JT == 4) {
+            f16x8 bh[JT], bl[JT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            bh[j] = sB(s)[((4 * wt + j) * 2 + 0) * 64 + lane];
-            bl[j] = sB(s)[((4 * wt + j) * 2 + 1) * 64 + lane];
-        }
+            for (int j = 0; j < JT; ++j) {
+                bh[j] = sB(s)[((JT * wt + j) * 2 + 0) * 64 + lane];
+                bl[j] = sB(s)[((JT * wt + j) * 2 + 1) * 64 + lane];
+            }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const f16x8 ah = sA(s)[((4 * wo + i) * 2 + 0) * 64 + lane];
-            const f16x8 al = sA(s)[((4 * wo + i) * 2 + 1) * 64 + lane];
+            for (int i = 0; i < 4; ++i) {
+                const f16x8 ah = sA(s)[((4 * wo + i) * 2 + 0) * 64 + lane];
+                const f16x8 al = sA(s)[((4 * wo + i) * 2 + 1) * 64 + lane];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(al, bh[j], acc[i][j]);
+                for (int j = 0; j < JT; ++j) acc[i][j] = mfma_h(al, bh[j], acc[i][j]);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(ah, bl[j], acc[i][j]);
+                for (int j = 0; j < JT; ++j) acc[i][j] = mfma_h(ah, bl[j], acc[i][j]);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_h(ah, bh[j], acc[i][j]);
+                for (int j = 0; j < JT; ++j) acc[i][j] = mfma_h(ah, bh[j], acc[i][j]);
+            }
+        } else {
+            // the wave's four A tiles held for the chunk, the token tiles' planes read two at a time (the 8 x 4
+            // accumulators leave no room for all 16 B fragments); the same three products per tile, in order
+            f16x8 ah[4], al[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ah[i] = sA(s)[((4 * wo + i) * 2 + 0) * 64 + lane];
+                al[i] = sA(s)[((4 * wo + i) * 2 + 1) * 64 + lane];
+            }
+#pragma unroll
+            for (int j0 = 0; j0 < JT; j0 += 2) {
+                f16x8 bh[2], bl[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    bh[j] = sB(s)[((JT * wt + j0 + j) * 2 + 0) * 64 + lane];
+                    bl[j] = sB(s)[((JT * wt + j0 + j) * 2 + 1) * 64 + lane];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma_h(al[i], bh[j], acc[i][j0 + j]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma_h(ah[i], bl[j], acc[i][j0 + j]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma_h(ah[i], bh[j], acc[i][j0 + j]);
+            }
         }
         if (c + 1 < KC) store(s ^ 1, ra, rb);
         __syncthreads();
     }
     // epilogue: unscale (exact powers of two), bias, activation; the accumulator of tile (i, j) holds outputs
-    // 4q..4q+3 of output tile T0 + 4 wo + i for token (4 wt + j) * 16 + nn
+    // 4q..4q+3 of output tile T0 + 4 wo + i for token (JT wt + j) * 16 + nn
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int pc = (4 * wt + j) * 16 + nn, r = m0 + pc;
+    for (int j = 0; j < JT; ++j) {
+        const int pc = (JT * wt + j) * 16 + nn, r = m0 + pc;
         const float u = exp2i(eT[pc] - 14 - ew);
         float ym = 0.f;
 #pragma unroll
@@ -403,6 +436,17 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
     }
 }
 
+// 256-token workgroups (JT = 8) when they still give the chip at least two workgroups per CU; GENPOSE2_LSPLIT_JT=4
+// keeps the 128-token tiles (tuning)
+#ifndef SL_JT8_DEFAULT
+#define SL_JT8_DEFAULT 1
+#endif
+static bool sl_wide_tokens(int m, int npad) {
+    const char* env = getenv("GENPOSE2_LSPLIT_JT");
+    const bool on = env ? env[0] == '8' : SL_JT8_DEFAULT != 0;
+    return on && (long long)((m + 255) / 256) * (npad / 256) >= 512;
+}
+
 extern "C" size_t gp_linear_split_words(int n, int k) {
     if (n < 1 || k < 32) return 0;
     return 4 + (size_t)((n + 127) / 128 * 128) * k;
@@ -426,15 +470,19 @@ extern "C" int gp_linear_split(const float* x, int ldx, int m, int k, const int3
         return gp_check_launch("linear_split ymax memset");
     SplitLinArgs a{x, ldx, m, k, rmax, wpk, bias, n, y, ldy, reinterpret_cast<unsigned*>(ymax)};
     const int npad = (n + 127) / 128 * 128;
-#define GP_LSPLIT(WO)                                                                                              \
+#define GP_LSPLIT(WO, JT)                                                                                          \
     {                                                                                                          \
-        const dim3 grid(npad / (64 * WO), (m + 64 * (8 / WO) - 1) / (64 * (8 / WO)));                          \
-        if (act == 0) hipLaunchKernelGGL((linear_split_kernel<WO, 0>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
-        else if (act == 1) hipLaunchKernelGGL((linear_split_kernel<WO, 1>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
-        else if (act == 2) hipLaunchKernelGGL((linear_split_kernel<WO, 2>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
-        else hipLaunchKernelGGL((linear_split_kernel<WO, 3>), grid, dim3(SL_THREADS), sl_lds_bytes<WO>(), st, a); \
+        constexpr int BM = 16 * JT * (8 / WO);                                                                 \
+        const dim3 grid(npad / (64 * WO), (m + BM - 1) / BM);                                                  \
+        constexpr size_t lds = sl_lds_bytes<WO, JT>();                                                         \
+        if (act == 0) hipLaunchKernelGGL((linear_split_kernel<WO, 0, JT>), grid, dim3(SL_THREADS), lds, st, a); \
+        else if (act == 1) hipLaunchKernelGGL((linear_split_kernel<WO, 1, JT>), grid, dim3(SL_THREADS), lds, st, a); \
+        else if (act == 2) hipLaunchKernelGGL((linear_split_kernel<WO, 2, JT>), grid, dim3(SL_THREADS), lds, st, a); \
+        else hipLaunchKernelGGL((linear_split_kernel<WO, 3, JT>), grid, dim3(SL_THREADS), lds, st, a); \
     }
-    if (npad % 256 == 0) GP_LSPLIT(4) else GP_LSPLIT(2)
+    if (npad % 256 == 0 && sl_wide_tokens(m, npad)) GP_LSPLIT(4, 8)
+    else if (npad % 256 == 0) GP_LSPLIT(4, 4)
+    else GP_LSPLIT(2, 4)
 #undef GP_LSPLIT
     return gp_check_launch("linear_split_kernel");
 }
