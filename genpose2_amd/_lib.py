@@ -49,6 +49,9 @@ _SIGS: Dict[str, tuple] = {
     "gp_encoder_geometry": (c_int, [c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "gp_encoder_forward_geom": (c_int, [c_void_p, c_int64_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t,
                                         c_void_p, c_void_p]),
+    "gp_encoder_geometry_levels": (c_int, [c_void_p, c_int, c_int, c_void_p, c_size_t, c_int, c_int, c_void_p]),
+    "gp_encoder_forward_geom_levels": (c_int, [c_void_p, c_int64_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                               c_size_t, c_void_p, c_int, c_int, c_void_p]),
     "gp_sa_level": (c_int, [c_void_p, c_int64_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t,
                             c_void_p, c_void_p]),
     "gp_linear": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),

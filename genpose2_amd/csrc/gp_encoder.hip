@@ -1911,16 +1911,19 @@ extern "C" int gp_encoder_fps(const float* pts, int B, int N, void* workspace, s
 
 // The geometry of every level in one pass: the FPS chain of all four levels, then the ball lists of both
 // radii per level. Another encoder of the same points then skips all of it (gp_encoder_forward_geom).
-extern "C" int gp_encoder_geometry(const float* pts, int B, int N, void* workspace, size_t workspace_bytes,
-                                   hipStream_t st) {
+extern "C" int gp_encoder_geometry_levels(const float* pts, int B, int N, void* workspace, size_t workspace_bytes,
+                                          int first, int last, hipStream_t st) {
     const float dummy = 0.f;
     const int64_t tab = 0;
     int rc = enc_check(&dummy, &tab, pts, B, N, workspace, workspace_bytes);
     if (rc) return rc;
+    GP_REQUIRE(first >= 0 && first < last && last <= 4, "encoder_geometry_levels: levels [%d, %d) of 4", first, last);
     const EncCtx c = enc_ctx(nullptr, nullptr, pts, B, N, workspace);
-    rc = gp_launch_fps_chain(pts, B, 4, c.nin, c.mout, (int* const*)c.fidx, (float* const*)c.nxyz, st);
+    // levels first.. sample from level first-1's centroids (already in the workspace)
+    rc = gp_launch_fps_chain(first == 0 ? pts : c.nxyz[first - 1], B, last - first, c.nin + first, c.mout + first,
+                             (int* const*)c.fidx + first, (float* const*)c.nxyz + first, st);
     if (rc) return rc;
-    for (int l = 0; l < 4; ++l) {
+    for (int l = first; l < last; ++l) {
         const float* xyz_prev = l == 0 ? pts : c.nxyz[l - 1];
         rc = gp_launch_ball_query2(B, c.nin[l], kNpoint[l], kRadius[l][0], kRadius[l][1], kNs[0], kNs[1], c.nxyz[l],
                                    xyz_prev, reinterpret_cast<int*>(c.ws + c.L.ball[l][0]),
@@ -1932,20 +1935,33 @@ extern "C" int gp_encoder_geometry(const float* pts, int B, int N, void* workspa
 
 // gp_encoder_forward over geometry that gp_encoder_geometry left in `geometry` (a workspace of the same
 // (B, N) layout; it may be `workspace` itself): only the per-level MLPs run, their scratch in `workspace`.
-extern "C" int gp_encoder_forward_geom(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N,
-                                       const void* geometry, void* workspace, size_t workspace_bytes, float* feat,
-                                       hipStream_t st) {
+extern "C" int gp_encoder_geometry(const float* pts, int B, int N, void* workspace, size_t workspace_bytes,
+                                   hipStream_t st) {
+    return gp_encoder_geometry_levels(pts, B, N, workspace, workspace_bytes, 0, 4, st);
+}
+
+extern "C" int gp_encoder_forward_geom_levels(const float* wbuf, const int64_t* layer_off, const float* pts, int B,
+                                              int N, const void* geometry, void* workspace, size_t workspace_bytes,
+                                              float* feat, int first, int last, hipStream_t st) {
     int rc = enc_check(wbuf, layer_off, pts, B, N, workspace, workspace_bytes);
     if (rc) return rc;
     GP_REQUIRE(feat && geometry, "encoder_forward_geom: null feat or geometry");
+    GP_REQUIRE(first >= 0 && first < last && last <= 5, "encoder_forward_geom_levels: levels [%d, %d) of 5", first, last);
     const EncCtx c = enc_ctx(wbuf, layer_off, pts, B, N, workspace, const_cast<void*>(geometry));
-    for (int l = 0; l < 5; ++l) {
+    for (int l = first; l < last; ++l) {
         const float* fprev = l == 0 ? nullptr : reinterpret_cast<const float*>(c.ws + c.L.feat[l - 1]);
         float* out = l < 4 ? reinterpret_cast<float*>(c.ws + c.L.feat[l]) : feat;
         rc = run_sa_level(c, l, l == 0 ? 0 : kCout[l - 1], fprev, out, false, st);
         if (rc) return rc;
     }
     return GP_OK;
+}
+
+extern "C" int gp_encoder_forward_geom(const float* wbuf, const int64_t* layer_off, const float* pts, int B, int N,
+                                       const void* geometry, void* workspace, size_t workspace_bytes, float* feat,
+                                       hipStream_t st) {
+    return gp_encoder_forward_geom_levels(wbuf, layer_off, pts, B, N, geometry, workspace, workspace_bytes, feat, 0, 5,
+                                          st);
 }
 
 extern "C" int gp_sa_level(const float* wbuf, const int64_t* layer_off, int level, int c_prev, const float* pts, int B,

@@ -45,11 +45,13 @@ class EncoderGeometry:
     model recomputes geometry in that workspace (its next geometry() or forward() without a geometry), which
     forward(geometry=...) detects through the producer's generation counter; ``event`` marks its completion on
     the producing stream. Refilling the points tensor in place also invalidates it (not detectable: the key is
-    the tensor's address and shape)."""
+    the tensor's address and shape). ``event0`` (or None) marks level 0's geometry alone: levels 1-3 were
+    computed on a side stream after it, so a consumer can start level 0 before they are done."""
 
-    def __init__(self, ws: torch.Tensor, event, key, producer=None, gen: int = 0):
+    def __init__(self, ws: torch.Tensor, event, key, producer=None, gen: int = 0, event0=None):
         self.ws, self.event, self.key = ws, event, key   # key: (points tensor address, (B, N))
         self.producer, self.gen = producer, gen
+        self.event0 = event0
 
 
 class EncoderModel:
@@ -63,6 +65,9 @@ class EncoderModel:
         self._table = np.ascontiguousarray(offs, np.int64)     # [5][2][3][4] (gp_encoder_forward)
         self._ws: Optional[torch.Tensor] = None
         self._gen = 0   # bumped whenever this model writes geometry into its workspace
+        # geometry(): levels 1-3 of the FPS chain and ball lists on a side stream, beside level 0's MLPs
+        self.geometry_overlap = os.environ.get("GENPOSE2_GEOM_OVERLAP", "1") == "1"
+        self._geo_stream: Optional[torch.cuda.Stream] = None
         self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
 
     @property
@@ -109,11 +114,31 @@ class EncoderModel:
         B, N, _ = pts.shape
         ws = self.workspace(B, N)
         self._gen += 1
-        check(self.lib.gp_encoder_geometry(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()),
-                                           ws.numel(), ctypes.c_void_p(stream_handle(self.device))), "encoder_geometry")
+        cur = torch.cuda.current_stream(self.device)
+        if not self.geometry_overlap:
+            check(self.lib.gp_encoder_geometry(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()),
+                                               ws.numel(), ctypes.c_void_p(cur.cuda_stream)), "encoder_geometry")
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            return EncoderGeometry(ws, ev, key, self, self._gen)
+        # level 0 here; levels 1-3 (their FPS reads level 0's centroids) on the side stream after it
+        check(self.lib.gp_encoder_geometry_levels(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()),
+                                                  ws.numel(), 0, 1, ctypes.c_void_p(cur.cuda_stream)),
+              "encoder_geometry level 0")
+        ev0 = torch.cuda.Event()
+        ev0.record(cur)
+        if self._geo_stream is None:
+            self._geo_stream = torch.cuda.Stream(device=self.device)
+        side = self._geo_stream
+        side.wait_event(ev0)
+        check(self.lib.gp_encoder_geometry_levels(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()),
+                                                  ws.numel(), 1, 4, ctypes.c_void_p(side.cuda_stream)),
+              "encoder_geometry levels 1-3")
+        ws.record_stream(side)
+        pts.record_stream(side)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        return EncoderGeometry(ws, ev, key, self, self._gen)
+        ev.record(side)
+        return EncoderGeometry(ws, ev, key, self, self._gen, event0=ev0)
 
     def forward(self, pts: torch.Tensor, return_workspace: bool = False,
                 geometry: Optional["EncoderGeometry"] = None):
@@ -136,12 +161,17 @@ class EncoderModel:
                 raise ValueError("encoder geometry was computed for other points")
             if geometry.producer is not None and geometry.producer._gen != geometry.gen:
                 raise ValueError("encoder geometry is stale: its model encoded other points since")
-            torch.cuda.current_stream(self.device).wait_event(geometry.event)
-            check(self.lib.gp_encoder_forward_geom(
-                ctypes.c_void_p(self.wbuf.data_ptr()), self.offsets.ctypes.data_as(_lib.c_int64_p),
-                ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(geometry.ws.data_ptr()),
-                ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(feat.data_ptr()), st),
-                "encoder_forward_geom")
+            cur = torch.cuda.current_stream(self.device)
+            # level 0 may start once its own geometry is there (event0), levels 1-4 after all of it
+            spans = ((0, 1, geometry.event0), (1, 5, geometry.event)) if geometry.event0 is not None else \
+                ((0, 5, geometry.event),)
+            for first, last, ev in spans:
+                cur.wait_event(ev)
+                check(self.lib.gp_encoder_forward_geom_levels(
+                    ctypes.c_void_p(self.wbuf.data_ptr()), self.offsets.ctypes.data_as(_lib.c_int64_p),
+                    ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(geometry.ws.data_ptr()),
+                    ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(feat.data_ptr()), first, last, st),
+                    "encoder_forward_geom")
             if geometry.ws is not ws:
                 geometry.ws.record_stream(torch.cuda.current_stream(self.device))
         return (feat, ws) if return_workspace else feat

@@ -86,6 +86,17 @@ int gp_encoder_geometry(const float *pts, int b, int n, void *workspace, size_t 
 int gp_encoder_forward_geom(const float *wbuf, const int64_t *layer_off, const float *pts, int b, int n,
                             const void *geometry, void *workspace, size_t workspace_bytes, float *feat,
                             hipStream_t stream);
+/* The same two calls over a range of levels, so that level 0's MLPs can start while the FPS chain and ball
+ * lists of levels 1-3 are still being computed (on another stream): gp_encoder_geometry_levels fills the
+ * geometry of levels [first, last) (first > 0 reads level first-1's centroids from the workspace);
+ * gp_encoder_forward_geom_levels runs SA levels [first, last) of 5 (level l reads level l-1's features from
+ * `workspace`; level 4 writes `feat`). geometry_levels(0, 4) == gp_encoder_geometry and
+ * forward_geom_levels(0, 5) == gp_encoder_forward_geom; any split gives the same bits. */
+int gp_encoder_geometry_levels(const float *pts, int b, int n, void *workspace, size_t workspace_bytes,
+                               int first, int last, hipStream_t stream);
+int gp_encoder_forward_geom_levels(const float *wbuf, const int64_t *layer_off, const float *pts, int b, int n,
+                                   const void *geometry, void *workspace, size_t workspace_bytes, float *feat,
+                                   int first, int last, hipStream_t stream);
 /* Level-by-level form (the fused encoders, whose levels take features computed between levels):
  * gp_encoder_fps runs the FPS chain of all four levels into the workspace (fps idx + new_xyz, as
  * gp_encoder_workspace_layout places them); gp_sa_level then runs SA level `level`

@@ -140,9 +140,11 @@ def test_encoder_shared_geometry_bit_exact(N, score_agent):
     energy = PoseNet(GenPoseConfig(device=DEV, agent_type="energy")).eval()
     pts, _ = synthetic.make_batch(21, 10, N, n_unique_every=5)
     p = torch.from_numpy(pts).to(DEV)
-    for arith in ("split_f16", "f32"):
+    for arith, overlap in (("split_f16", True), ("split_f16", False), ("f32", True)):
         for a in (score_agent, energy):
             a.encoder.set_arith(arith)
+        # overlap: levels 1-3 of the geometry on a side stream while level 0's MLPs run (EncoderGeometry.event0)
+        score_agent.encoder.geometry_overlap = overlap
         ref_s, ws_s = score_agent.encoder.forward(p, return_workspace=True)
         lv_ref = [{k: (v.clone() if torch.is_tensor(v) else [x.clone() for x in v]) for k, v in d.items()
                    if k != "features"} for d in score_agent.encoder.levels(10, N, ws_s)]
@@ -152,7 +154,8 @@ def test_encoder_shared_geometry_bit_exact(N, score_agent):
         got_e = energy.encoder.forward(p, geometry=data["enc_geometry"])
         got_s = score_agent.encoder.forward(p, geometry=data["enc_geometry"])
         torch.cuda.synchronize()
-        assert torch.equal(got_s, ref_s) and torch.equal(got_e, ref_e), arith
+        assert (data["enc_geometry"].event0 is not None) == overlap
+        assert torch.equal(got_s, ref_s) and torch.equal(got_e, ref_e), (arith, overlap)
         for d0, d1 in zip(lv_ref, score_agent.encoder.levels(10, N, data["enc_geometry"].ws)):
             for k in d0:
                 if torch.is_tensor(d0[k]):
@@ -166,6 +169,7 @@ def test_encoder_shared_geometry_bit_exact(N, score_agent):
             energy.encoder.forward(p, geometry=data["enc_geometry"])
     for a in (score_agent, energy):
         a.encoder.set_arith("split_f16")
+    score_agent.encoder.geometry_overlap = True
 
 
 def test_encoder_batch_independence(score_agent):
