@@ -14,6 +14,57 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+// MODE 3: waves 0-3 only, NF independent f32 FMAs after every MFMA in the same instruction stream (can one wave
+// fill its own MFMA shadow with VALU work?)
+template <int NF>
+__global__ __launch_bounds__(512) void fill(float* out, long long* cyc, int n) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    f16x8 a, b;
+    for (int k = 0; k < 8; ++k) {
+        a[k] = (_Float16)(1.0f + lane * 1e-3f + k * 1e-2f);
+        b[k] = (_Float16)(0.5f - lane * 1e-3f + k * 1e-2f);
+    }
+    float sink = 0.f;
+    __builtin_amdgcn_s_barrier();
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    if (w < 4) {
+        f32x4 acc[8];
+        float v[16];
+        for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < 16; ++c) v[c] = lane * 1e-3f + c;
+        const float x = 1.0f + lane * 1e-6f, y = 0.999f;
+        for (int i = 0; i < n; ++i) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[j], 0, 0, 0);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) v[(j * NF + f) & 15] = __builtin_fmaf(v[(j * NF + f) & 15], x, y);
+            }
+        }
+        for (int j = 0; j < 8; ++j) sink += acc[j].x + acc[j].y + acc[j].z + acc[j].w;
+        for (int c = 0; c < 16; ++c) sink += v[c];
+    }
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) cyc[blockIdx.x * 8 + w] = t1 - t0;
+    out[blockIdx.x * 512 + threadIdx.x] = sink;
+}
+
+template <int NF>
+void run_fill(const char* name, float* out, long long* cyc, int n) {
+    const int nwg = 256;
+    std::vector<long long> h(nwg * 8);
+    for (int rep = 0; rep < 2; ++rep) {
+        hipLaunchKernelGGL((fill<NF>), dim3(nwg), dim3(512), 0, 0, out, cyc, n);
+        hipDeviceSynchronize();
+    }
+    hipMemcpy(h.data(), cyc, h.size() * 8, hipMemcpyDeviceToHost);
+    double m = 0;
+    for (int g = 0; g < nwg; ++g)
+        for (int w = 0; w < 4; ++w) m += h[g * 8 + w];
+    m /= nwg * 4;
+    printf("%-22s mfma waves %9.0f cyc (%5.2f / MFMA with %d f32 FMAs each)\n", name, m, m / (n * 8.0), NF);
+}
+
 template <int MODE, bool PK>
 __global__ __launch_bounds__(512) void mix(float* out, long long* cyc, int n) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -106,5 +157,10 @@ int main() {
     run<1, true>("pk_fma only", out, cyc, n, n);
     run<2, false>("split f32 fma", out, cyc, n, n);
     run<2, true>("split pk_fma", out, cyc, n, n);
+    run_fill<0>("fill 0", out, cyc, n);
+    run_fill<2>("fill 2", out, cyc, n);
+    run_fill<4>("fill 4", out, cyc, n);
+    run_fill<8>("fill 8", out, cyc, n);
+    run_fill<12>("fill 12", out, cyc, n);
     return 0;
 }
