@@ -254,6 +254,15 @@ extern "C" int gp_linear(const float* x, int ldx, int m, int k, const float* w, 
 // LDS stages of one 32-deep chunk, one barrier per chunk. JT = 8 (WO = 4): every A fragment read from LDS
 // feeds 8 token tiles instead of 4, so the LDS traffic per MFMA drops by a third.
 constexpr int SL_THREADS = 512;
+#ifndef SL_DMA
+#define SL_DMA 1   // A planes global -> LDS by global_load_lds_dwordx4 (0: through registers and ds_write)
+#endif
+// 16 bytes per lane from global memory straight into LDS at lds + 16 * lane (lds wave-uniform)
+__device__ __forceinline__ void lds_dma16(const void* src, void* lds) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+// every outstanding memory operation of the wave has completed (the LDS copies above included)
+__device__ __forceinline__ void wait_all_mem() { __builtin_amdgcn_s_waitcnt(0); }
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 struct SplitLinArgs {
     const float* x;
@@ -312,19 +321,32 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
         sc[u] = exp2i(14 - E);
         if (g == 0) eT[r] = E;
     }
-    auto load = [&](int c, f32x4 (&ra)[WO], f32x4 (&rb)[RU]) {
+    // A (the packed weight planes, stored as they are): SL_DMA copies them global -> LDS directly
+    // (global_load_lds_dwordx4: no registers, no ds_write; the wave's 64 lanes fill 1 KB at its LDS base)
+    auto load = [&](int c, int sdst, f32x4 (&ra)[WO], f32x4 (&rb)[RU]) {
 #pragma unroll
         for (int u = 0; u < WO; ++u) {
             const int idx = tid + SL_THREADS * u;
-            ra[u] = ld4(reinterpret_cast<const float*>(W + ((size_t)(T0 + (idx >> 7)) * KC + c) * 128 + (idx & 127)));
+            const f16x8* src = W + ((size_t)(T0 + (idx >> 7)) * KC + c) * 128 + (idx & 127);
+#if SL_DMA
+            lds_dma16(src, sA(sdst) + (idx & ~63));
+            (void)ra;
+#else
+            (void)sdst;
+            ra[u] = ld4(reinterpret_cast<const float*>(src));
+#endif
         }
 #pragma unroll
         for (int u = 0; u < RU; ++u)
             rb[u] = row[u] < a.m ? ld4(a.x + (size_t)row[u] * a.ldx + 32 * c + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
     };
     auto store = [&](int s, const f32x4 (&ra)[WO], const f32x4 (&rb)[RU]) {
+#if !SL_DMA
 #pragma unroll
         for (int u = 0; u < WO; ++u) sA(s)[tid + SL_THREADS * u] = __builtin_bit_cast(f16x8, ra[u]);
+#else
+        (void)ra;
+#endif
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
 #pragma clang fp contract(off)
@@ -348,12 +370,13 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
 #pragma unroll
         for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 ra[WO], rb[RU];
-    load(0, ra, rb);
+    load(0, 0, ra, rb);
     store(0, ra, rb);
+    if constexpr (SL_DMA) wait_all_mem();   // the direct-to-LDS copies have landed
     __syncthreads();
     for (int c = 0; c < KC; ++c) {
         const int s = c & 1;
-        if (c + 1 < KC) load(c + 1, ra, rb);
+        if (c + 1 < KC) load(c + 1, s ^ 1, ra, rb);
         if constexpr (JT == 4) {
             f16x8 bh[JT], bl[JT];
 #pragma unroll
@@ -404,6 +427,7 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
             }
         }
         if (c + 1 < KC) store(s ^ 1, ra, rb);
+        if constexpr (SL_DMA) wait_all_mem();
         __syncthreads();
     }
     // epilogue: unscale (exact powers of two), bias, activation; the accumulator of tile (i, j) holds outputs
