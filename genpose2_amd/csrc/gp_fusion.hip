@@ -297,7 +297,10 @@ __global__ __launch_bounds__(256) void fus_rowmax_kernel(const float* __restrict
 
 template <int WO, int ACT, int JT = 4>
 __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a) {
-    constexpr int WT = 8 / WO, BM = 16 * JT * WT, RU = BM / 64;   // RU: token rows per thread (8 threads a row)
+    // RU: (token row, k-group pair) items per thread. Item (row br, k-groups bq and bq + 4) fills one 16-byte
+    // B-fragment entry per plane, and a wave's 16-lane store phases cover 16 rows of one k-group: entries of
+    // distinct banks (8 threads a row writing 8-byte halves conflicted 4-way: 43 % of LDS cycles)
+    constexpr int WT = 8 / WO, BM = 16 * JT * WT, RU = BM / 128;
     constexpr int NA = 4 * WO * 128, NB = JT * WT * 128;   // f16x8 fragments per stage
     extern __shared__ __attribute__((aligned(16))) f16x8 sl_lds[];
     auto sA = [&](int st) { return sl_lds + st * (NA + NB); };
@@ -307,23 +310,24 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int m0 = blockIdx.y * BM, T0 = blockIdx.x * 4 * WO;
     const int KC = a.k >> 5;
-    const int g = tid & 7;
     const int ew = a.w[0];
     const f16x8* W = reinterpret_cast<const f16x8*>(a.w + 4);
-    int row[RU];
+    int row[RU], brow[RU], bq[RU];
     float sc[RU];
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-        const int r = (tid + SL_THREADS * u) >> 3;
-        row[u] = m0 + r;
+        const int idx = tid + SL_THREADS * u;
+        brow[u] = (idx & 15) + 16 * (idx >> 6);
+        bq[u] = (idx >> 4) & 3;
+        row[u] = m0 + brow[u];
         const float mx = row[u] < a.m ? a.rmax[row[u]] : 0.f;
         const int E = mx > 1e-30f ? ilog2f(mx) : -100;
         sc[u] = exp2i(14 - E);
-        if (g == 0) eT[r] = E;
+        if (bq[u] == 0) eT[brow[u]] = E;
     }
     // A (the packed weight planes, stored as they are): SL_DMA copies them global -> LDS directly
     // (global_load_lds_dwordx4: no registers, no ds_write; the wave's 64 lanes fill 1 KB at its LDS base)
-    auto load = [&](int c, int sdst, f32x4 (&ra)[WO], f32x4 (&rb)[RU]) {
+    auto load = [&](int c, int sdst, f32x4 (&ra)[WO], f32x4 (&rb)[2 * RU]) {
 #pragma unroll
         for (int u = 0; u < WO; ++u) {
             const int idx = tid + SL_THREADS * u;
@@ -337,10 +341,13 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
 #endif
         }
 #pragma unroll
-        for (int u = 0; u < RU; ++u)
-            rb[u] = row[u] < a.m ? ld4(a.x + (size_t)row[u] * a.ldx + 32 * c + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < RU; ++u) {
+            const float* xr = a.x + (size_t)row[u] * a.ldx + 32 * c + 4 * bq[u];
+            rb[2 * u] = row[u] < a.m ? ld4(xr) : f32x4{0.f, 0.f, 0.f, 0.f};
+            rb[2 * u + 1] = row[u] < a.m ? ld4(xr + 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
     };
-    auto store = [&](int s, const f32x4 (&ra)[WO], const f32x4 (&rb)[RU]) {
+    auto store = [&](int s, const f32x4 (&ra)[WO], const f32x4 (&rb)[2 * RU]) {
 #if !SL_DMA
 #pragma unroll
         for (int u = 0; u < WO; ++u) sA(s)[tid + SL_THREADS * u] = __builtin_bit_cast(f16x8, ra[u]);
@@ -350,17 +357,19 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
 #pragma clang fp contract(off)
-            const int r = (tid + SL_THREADS * u) >> 3, ln = 16 * (g & 3) + (r & 15), half = g >> 2;
-            f16x4 hi, lo;
+            const int r = brow[u], ln = 16 * bq[u] + (r & 15);
+            f16x8 hi, lo;   // k-groups bq (halves 0-3) and bq + 4 (halves 4-7)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float x = rb[u][j] * sc[u];
-                const _Float16 h = (_Float16)x;
-                hi[j] = h;
-                lo[j] = (_Float16)(x - (float)h);
-            }
-            reinterpret_cast<f16x4*>(&sB(s)[((r >> 4) * 2 + 0) * 64 + ln])[half] = hi;
-            reinterpret_cast<f16x4*>(&sB(s)[((r >> 4) * 2 + 1) * 64 + ln])[half] = lo;
+            for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float x = rb[2 * u + h2][j] * sc[u];
+                    const _Float16 h = (_Float16)x;
+                    hi[4 * h2 + j] = h;
+                    lo[4 * h2 + j] = (_Float16)(x - (float)h);
+                }
+            sB(s)[((r >> 4) * 2 + 0) * 64 + ln] = hi;
+            sB(s)[((r >> 4) * 2 + 1) * 64 + ln] = lo;
         }
     };
     const int wo = wid % WO, wt = wid / WO;
@@ -369,7 +378,7 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 ra[WO], rb[RU];
+    f32x4 ra[WO], rb[2 * RU];
     load(0, 0, ra, rb);
     store(0, ra, rb);
     if constexpr (SL_DMA) wait_all_mem();   // the direct-to-LDS copies have landed

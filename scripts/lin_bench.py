@@ -30,7 +30,10 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     rng = np.random.default_rng(0)
     out = []
+    only = os.environ.get("LIN_SHAPES")
     for name, m, k, n in SHAPES:
+        if only and name not in only.split(","):
+            continue
         x = torch.from_numpy(rng.normal(size=(m, k)).astype(np.float32)).to(DEV)
         w = (rng.normal(size=(n, k)) / np.sqrt(k)).astype(np.float32)
         wh = torch.from_numpy(pack_split_linear(w)).to(DEV)
