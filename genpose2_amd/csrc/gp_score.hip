@@ -230,8 +230,15 @@ __device__ __forceinline__ void pc_update_rows(const PCArgs& a, int i, const PCS
             x3[k] = mean[k] + gs * z2v[k];
         }
         gram_schmidt6_quad(x3, p, lane);
-        const float* cp = a.center + (size_t)(r / a.kper) * 3;
-        const float cen[3] = {ld1(cp), ld1(cp + 1), ld1(cp + 2)};
+        // the centre only where it is added (the trajectory, the last step): the loads are atomic (gp_common.h
+        // ld1), which the compiler does not drop when their values go unused
+        float cen[3] = {0.f, 0.f, 0.f};
+        if (a.xs || i == a.steps) {
+            const float* cp = a.center + (size_t)(r / a.kper) * 3;
+            cen[0] = ld1(cp);
+            cen[1] = ld1(cp + 1);
+            cen[2] = ld1(cp + 2);
+        }
         if (a.xs) {
             float* o = a.xs + ((size_t)r * a.steps + (i - 1)) * 9 + e0;
 #pragma unroll
