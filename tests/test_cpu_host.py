@@ -1,5 +1,6 @@
 """CPU-only tests of the host side: C-ABI exports, packing, SDE scalars, RK45 controller,
 DBSCAN restatement, aggregation, sharding (gloo, world_size 2). No HIP compute calls."""
+import ctypes
 import os
 import re
 import subprocess
@@ -139,6 +140,17 @@ def test_invalid_arguments_return_status_not_exit():
     assert rc == -1 and b"ball_query" in lib.gp_last_error()
     with pytest.raises(_lib.GenPoseHipError):
         _lib.check(lib.gp_furthest_point_sampling(1, 0, 1, None, None, None, None), "fps")
+    # round-5 entry points: argument checks run before any device work
+    assert lib.gp_encoder_geometry_levels(None, 1, 1024, None, 0, 0, 4, None) == -1
+    assert b"encoder" in lib.gp_last_error()
+    assert lib.gp_encoder_forward_geom_levels(None, None, None, 1, 1024, None, None, 0, None, 0, 5, None) == -1
+    assert lib.gp_img_encoder2(None, None, None, 1, 256, 384, None, None, None, 0.0, None, None, None, 0.0, 0.0,
+                               None, None, None, None, None, None, 0, None) == -1
+    assert b"img_encoder" in lib.gp_last_error()
+    buf = np.zeros(16, np.float32)   # non-null stand-ins: the level range is rejected before any launch
+    ptr = buf.ctypes.data_as(ctypes.c_void_p)
+    assert lib.gp_encoder_geometry_levels(ptr, 1, 1024, ptr, 1 << 40, 2, 1, None) == -1
+    assert b"levels [2, 1)" in lib.gp_last_error()
 
 
 def test_a_fragment_packing_layout():
