@@ -367,7 +367,11 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     SplitScalars hs = {};
     if constexpr (SPLIT) hs = load_split_scalars<WV>(a.w);   // in flight across the update
     PC_MARK(0);
+#ifndef PC_UPD_PRIO
+#define PC_UPD_PRIO 0   // tuning: issue priority of the update waves over the draw / staging waves during the update
+#endif
     if (wid < NT) {
+        if constexpr (PC_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(PC_UPD_PRIO);
         // ---- every load first and unconditional (rows clamped: a guarded load becomes a branch,
         //      and the compiler then drains the first batch before issuing the next): the
         //      grad-norm partials of step i-1, then this lane's elements of x, s and the two draws.
@@ -405,6 +409,7 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         }
         PC_MARK(9);
         pc_update_rows<NT, WV, PL>(a, i, prev, sm, obj, g, lane, r0, gacc, x3, sv, z1v, z2v, hs, true, trace_slot);
+        if constexpr (PC_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         PC_MARK(12);
     }
     if (i == a.steps) return;  // finalize launch: no score evaluation
