@@ -263,6 +263,20 @@ def load_rocprof(kernel, config, dino="none"):
     return None
 
 
+def rocprof_top(config, dino="none", n=4):
+    """The n kernels with the largest total time in the newest committed rocprofv3 --stats summary of a bench run of
+    `config` (DINO-pointwise runs: config<C>_pointwise_*), or None."""
+    import csv
+    for fn in rocprof_files(config, dino):
+        with open(fn) as f:
+            rows = sorted(csv.DictReader(f), key=lambda r: -float(r["TotalDurationNs"]))
+        return {"source": os.path.relpath(fn, REPO),
+                "kernels": [{"name": r["Name"].split("(")[0], "calls": int(r["Calls"]),
+                             "avg_us": float(r["AverageNs"]) / 1e3, "percent": float(r["Percentage"])}
+                            for r in rows[:n]]}
+    return None
+
+
 def load_traffic(rows, split, tile):
     """HBM(+Infinity Cache) bytes per pc_step launch from the newest committed PMC pass of the same
     kernel instantiation (tile width, arithmetic) and row count (profiles/**/pmc_pc_step*.json,
@@ -324,23 +338,49 @@ def time_ode_calls(args, cfg, data0, B, K, ws, dev):
     if ws > 1:
         import torch.distributed as dist
         dist.barrier()
+    from genpose2_amd import arch, ode as ode_mod
     nf = []
+    ode_mod.STAGE_EVENTS = []   # each attempt's six stage launches bracketed by HIP events on the launch stream
     t0 = time.perf_counter()
-    for _ in range(args.ode_calls):
-        agent.pred_func(dict(data0), repeat_num=K, T0=0.55)
-        nf.append(agent.last_nfev)
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
+    try:
+        for _ in range(args.ode_calls):
+            agent.pred_func(dict(data0), repeat_num=K, T0=0.55)
+            nf.append(agent.last_nfev)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        stage_ms = [a.elapsed_time(b) for a, b, _ in ode_mod.STAGE_EVENTS]
+        rows = {r for _, _, r in ode_mod.STAGE_EVENTS}
+    finally:
+        ode_mod.STAGE_EVENTS = None
     if ws > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     per = el / args.ode_calls
     nfev = float(np.mean(nf))
-    return {"metric": "pose candidate-RHS evaluations/sec (B objs x K cands x nfev, ODE sampler, T0=0.55)",
-            "value": B * K * ws * float(np.sum(nf)) / el, "unit": "pose-candidate-evals/s", "nfev": nfev,
-            "ms_per_call": per * 1e3, "poses_per_s": B * K * ws / per, "calls": args.ode_calls,
-            "workload": f"B={B} objects/GPU, K={K}: encoder + RK45 (rtol=atol=1e-5) + denoise per call"}
+    out = {"metric": "pose candidate-RHS evaluations/sec (B objs x K cands x nfev, ODE sampler, T0=0.55)",
+           "value": B * K * ws * float(np.sum(nf)) / el, "unit": "pose-candidate-evals/s", "nfev": nfev,
+           "ms_per_call": per * 1e3, "poses_per_s": B * K * ws / per, "calls": args.ode_calls,
+           "workload": f"B={B} objects/GPU, K={K}: encoder + RK45 (rtol=atol=1e-5) + denoise per call"}
+    if stage_ms and rows == {B * K}:
+        # the dominant kernel: ode_stage_kernel, six launches per attempted step (five stage derivatives, then the
+        # last stage with y_new and the error partials), each one score evaluation of every row
+        us = float(np.sum(stage_ms)) * 1e3 / (6 * len(stage_ms))
+        fl = B * K * arch.score_flops_per_candidate_step()
+        fast = agent.heads.arith == "f16x3"
+        peak = F16_PEAK_TFLOPS / 6 if fast else FP32_PEAK_TFLOPS
+        tile = int(_tile_rows(B * K, fast))
+        kname = f"void ode_stage_kernel<0, {3 if fast else 0}, {tile // 16}>"
+        out["roofline"] = {"bound": "mfma", "achieved": fl / us / 1e6, "peak": peak, "unit": "TFLOP/s",
+                           "frac": fl / us / 1e6 / peak, "kernel": kname.replace("<0,", "<MODE,"),
+                           "flop_per_launch": fl, "avg_launch_us": us, "attempts_timed": len(stage_ms),
+                           "stage_ms_per_call": float(np.sum(stage_ms)) / args.ode_calls}
+        rp = load_rocprof(kname, args.config)
+        if rp is not None:
+            rp["achieved"] = fl / (rp["avg_launch_us"] * 1e-6) / 1e12
+            rp["frac"] = rp["achieved"] / peak
+            out["roofline"]["rocprof"] = rp
+    return out
 
 
 def main():
@@ -383,6 +423,10 @@ def main():
     ap.add_argument("--f32-steps", type=int, default=5,
                     help="PC runs: also time this many steps with every GEMM in exact fp32 (heads and encoders; "
                          "GENPOSE2_HEAD_ARITH=f32 / GENPOSE2_ENC_ARITH=f32) and report them under 'f32_exact' (0: off)")
+    ap.add_argument("--pointwise-steps", type=int, default=5,
+                    help="Light-encoder PC runs of a full-pipeline config: also time this many steps of the shipped "
+                         "scripts' encoder (scripts/eval_single.sh: --dino pointwise) on the same shape and report them "
+                         "under 'pointwise' (0: off)")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     ndev = 0
@@ -411,23 +455,31 @@ def main():
 
     B, N, K, T = cfgd["B"], cfgd["N"], cfgd["K"], cfgd["T"]
     ode = args.sampler == "ode"
-    cfg = GenPoseConfig(device=str(dev), sampling_steps=None if ode else T, eval_repeat_num=K,
-                        noise_seed=1234 + rank, sampler_mode=[args.sampler], dino=args.dino)
-    score = PoseNet(cfg).eval()
-    broadcast_weights(score, ws)
-    energy = PoseNet(cfg.copy(agent_type="energy")).eval() if cfgd["energy"] else None
-    scale = PoseNet(cfg.copy(agent_type="scale")).eval() if cfgd["scale"] else None
-    for a in (energy, scale):
-        if a is not None:
-            broadcast_weights(a, ws)
-    pts, center = synthetic.make_batch(args.config, B, N, first_object=rank * B)
-    data0 = {"pts": torch.from_numpy(pts).to(dev), "pts_center": torch.from_numpy(center).to(dev)}
-    if args.dino == "pointwise":   # the DINOv3 backbone's layers [2, 6, 11] and roi pixels, synthetic
-        rng = np.random.Generator(np.random.PCG64(4242 + rank))
-        data0["dino_layers"] = [torch.from_numpy(rng.standard_normal((B, 256, 384), dtype=np.float32)).to(dev)
-                                for _ in range(3)]
-        data0["roi_xs"] = torch.from_numpy(rng.integers(0, 224, size=(B, N)).astype(np.int32)).to(dev)
-        data0["roi_ys"] = torch.from_numpy(rng.integers(0, 224, size=(B, N)).astype(np.int32)).to(dev)
+    from types import SimpleNamespace
+
+    def build_leg(dino):
+        """The agents of one pipeline (score, energy, scale as the config asks) and its synthetic objects in HBM."""
+        c = GenPoseConfig(device=str(dev), sampling_steps=None if ode else T, eval_repeat_num=K,
+                          noise_seed=1234 + rank, sampler_mode=[args.sampler], dino=dino)
+        sc = PoseNet(c).eval()
+        broadcast_weights(sc, ws)
+        en = PoseNet(c.copy(agent_type="energy")).eval() if cfgd["energy"] else None
+        sl = PoseNet(c.copy(agent_type="scale")).eval() if cfgd["scale"] else None
+        for a in (en, sl):
+            if a is not None:
+                broadcast_weights(a, ws)
+        pts, center = synthetic.make_batch(args.config, B, N, first_object=rank * B)
+        d0 = {"pts": torch.from_numpy(pts).to(dev), "pts_center": torch.from_numpy(center).to(dev)}
+        if dino == "pointwise":   # the DINOv3 backbone's layers [2, 6, 11] and roi pixels, synthetic
+            rng = np.random.Generator(np.random.PCG64(4242 + rank))
+            d0["dino_layers"] = [torch.from_numpy(rng.standard_normal((B, 256, 384), dtype=np.float32)).to(dev)
+                                 for _ in range(3)]
+            d0["roi_xs"] = torch.from_numpy(rng.integers(0, 224, size=(B, N)).astype(np.int32)).to(dev)
+            d0["roi_ys"] = torch.from_numpy(rng.integers(0, 224, size=(B, N)).astype(np.int32)).to(dev)
+        return SimpleNamespace(score=sc, energy=en, scale=sl, data0=d0, dino=dino, cfg=c)
+
+    main_leg = build_leg(args.dino)
+    cfg, score, energy, scale, data0 = main_leg.cfg, main_leg.score, main_leg.energy, main_leg.scale, main_leg.data0
 
     stream = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(device=dev)
@@ -443,8 +495,11 @@ def main():
         pending.append(d)
     nfevs = []
 
-    def one_step(record=False, last=False):
-        pipe = args.pipeline and not ode
+    def one_step(record=False, last=False, leg=None, evs=None):
+        leg = main_leg if leg is None else leg
+        evs = samp_ev if evs is None else evs
+        score, energy, scale, data0 = leg.score, leg.energy, leg.scale, leg.data0
+        pipe = args.pipeline and not ode and leg is main_leg
         if pipe:
             if not pending:          # first step of a run: nothing to overlap with yet
                 start_encode()
@@ -458,7 +513,7 @@ def main():
             # the energy encoder needs only the points: overlap it with the score sampler
             # (as genpose2_amd.runner.EvaluationPipeline does)
             edata = {k: data0[k] for k in ("pts", "pts_center", "dino_layers", "roi_xs", "roi_ys") if k in data0}
-            if args.share_geometry and not pipe and args.dino == "none":
+            if args.share_geometry and not pipe and leg.dino == "none":
                 score.encode_geometry(data)          # one geometry pass for both encoders of this batch
                 edata["enc_geometry"] = data["enc_geometry"]
 
@@ -500,7 +555,7 @@ def main():
             nfevs.append(score.last_nfev)
         if record and not ode:
             score.heads.pc_sample = orig
-            samp_ev.append((e0, e1))
+            evs.append((e0, e1))
         if energy is not None:
             if not args.energy_overlap:
                 energy.encode_func(edata)
@@ -514,6 +569,24 @@ def main():
             axes = torch.eye(3, device=dev).expand(B, 3, 3).contiguous()
             scale.pred_scale_func({"pts_feat": data["pts_feat"], "axes": axes})
         return pose
+
+    def timed_steps(n, leg=None, evs=None):
+        """n steps between a barrier + device synchronisation on both sides; the max over ranks (s)."""
+        torch.cuda.synchronize(dev)
+        if ws > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(n):
+            one_step(record=True, last=True, leg=leg, evs=evs)
+        torch.cuda.synchronize(dev)
+        if ws > 1:
+            dist.barrier()
+        el = time.perf_counter() - t1
+        if ws > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     for i in range(args.warmup):
         one_step(last=i == args.warmup - 1)
@@ -590,6 +663,27 @@ def main():
             rp32["achieved"] = fl / (rp32["avg_launch_us"] * 1e-6) / 1e12
             rp32["frac"] = rp32["achieved"] / FP32_PEAK_TFLOPS
             f32_info["roofline"]["rocprof"] = rp32
+    pw_info = None
+    if args.pointwise_steps > 0 and args.dino == "none" and cfgd["energy"] and not args.pipeline:
+        # the shipped scripts' configuration (--dino pointwise): ImgEncoder over synthetic DINOv3 layers, the patch
+        # gather and Pointnet2ClsMSGFus for both nets, the same sampler, energy and aggregation
+        pw = build_leg("pointwise")
+        pw_ev = []
+        for _ in range(2):
+            one_step(last=True, leg=pw, evs=[])
+        elp = timed_steps(args.pointwise_steps, leg=pw, evs=pw_ev)
+        pw_samp = float(np.mean([a.elapsed_time(b) for a, b in pw_ev]))
+        ms = elp / args.pointwise_steps * 1e3
+        pw_info = {"value": B * K * T * ws * args.pointwise_steps / elp, "unit": "pose-candidate-steps/s",
+                   "steps": args.pointwise_steps, "ms_per_step": ms, "sampler_ms_per_step": pw_samp,
+                   "non_sampler_ms_per_step": ms - pw_samp,
+                   "pc_step_avg_launch_us": pw_samp / (T + 1) * 1e3,
+                   "workload": f"config{args.config} shape with --dino pointwise (scripts/eval_single.sh): ImgEncoder over "
+                               f"synthetic DINOv3 layers (B, 256, 384) x 3, patch gather, Pointnet2ClsMSGFus for the score "
+                               f"and energy nets, PC sampler, energy, ranking/aggregation",
+                   "rocprof_top": rocprof_top(args.config, "pointwise")}
+        del pw
+        torch.cuda.empty_cache()
     units = B * K * T * ws * args.steps
     samp_ms = float(np.mean([a.elapsed_time(b) for a, b in samp_ev]))
     per_launch_s = samp_ms / 1e3 / (T + 1)
@@ -649,6 +743,8 @@ def main():
             out["f32_exact"] = f32_info
         if ode_info is not None:
             out["ode"] = ode_info
+        if pw_info is not None:
+            out["pointwise"] = pw_info
         if not args.no_cpu_baseline and args.dino == "none":
             threads = args.cpu_threads or cpu_threads_default()
             out["cpu_baseline"] = (cpu_baseline(cfgd, args.config, threads, args.cpu_sample_objects)

@@ -54,11 +54,16 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<
 
 // One 4-byte global load that the backend never merges with its neighbours (a relaxed workgroup-scope atomic
 // load: a plain global_load_dword, sc0, cached as usual). Three consecutive floats (coordinates, a pose
-// row's three entries) are read through it: merged, they become a global_load_dwordx3, and gfx950 returned a
-// stale second dword to a packed-FP32 instruction (v_pk_fma_f32 / v_pk_add_f32 reading the load's register
-// pair) in a few 16-lane groups per thousand launches when other processes' kernels shared the GPU -- the
-// level-0 projection then lost its y term (DESIGN (c); scripts/race_probe.py). tests/test_cpu_host.py checks
-// the library for any dwordx3 load feeding a packed-FP32 instruction.
+// row's three entries) are read through it. Observed, not explained: with a merged global_load_dwordx3 feeding
+// a packed-FP32 instruction (v_pk_fma_f32 reading the load's register pair), the level-0 projection lost its y
+// term in a few 16-lane groups per thousand launches, only while other processes' kernels shared the GPU; with
+// 4-byte loads it never did (A/B in DESIGN (c), scripts/race_probe.py). The hardware cause -- wave state lost
+// across a context switch between processes -- is a HYPOTHESIS that user code cannot confirm. The guard is
+// behavioural (race_probe.py) plus static (tests/test_cpu_host.py: no 12-byte loads, no vector loads from the
+// kernel-argument segment). Kernels that still stage data in LDS behind a barrier and were cleared only by
+// finite probes (0 differing repetitions), not by construction: the level-0 FPS chain (gp_fps.h), the SA
+// gathers (gp_encoder.hip), the relative-PE key coordinates (gp_fusion.hip mha_relpe_kernel) and the PC / ODE
+// trunks' activation planes (gp_head.h).
 __device__ __forceinline__ float ld1(const float* p) {
     return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }

@@ -10,9 +10,6 @@ constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
 #ifndef PC_WV1
 #define PC_WV1 8                 // waves per workgroup, 16-candidate PC tiles
 #endif
-#ifndef PC_WV2
-#define PC_WV2 4                 // waves per workgroup, 32-candidate PC tiles
-#endif
 #ifndef EVAL_WV
 #define EVAL_WV 8                // waves per workgroup, score/energy evaluation
 #endif
@@ -31,8 +28,8 @@ constexpr int KG_HID = HID / 16; // k-groups over a 256-wide activation
 
 
 // The thread id behind an opaque copy: per-lane values derived from it are computed where they are used and
-// cannot be hoisted out of an enclosing loop (the persistent PC sampler runs the trunk once per step; hoisted
-// lane addresses stayed live across every trunk and were spilled, their reloads draining the weight ring)
+// cannot be hoisted out of an enclosing loop (a trunk run once per loop iteration kept hoisted lane addresses
+// live across every trunk and spilled them, their reloads draining the weight ring)
 __device__ __forceinline__ int tid_x() {
     int t = threadIdx.x;
     asm volatile("" : "+v"(t));
@@ -46,8 +43,7 @@ template <int NT, int WV, int PL = 0>
 struct HeadSmem {
     // 64-candidate tiles (NT = 4) alias pose_encoder.2's output onto pose_encoder.0's (written after
     // a barrier that retires every read of act1), so one workgroup still fits the 160 KiB of a CU
-    // (also the f16x3 trunk of 4-wave workgroups: two of them share a CU, PC_PAIR)
-    static constexpr bool kAliasAct = NT >= 4 || (PL != 0 && WV <= 4);
+    static constexpr bool kAliasAct = NT >= 4;
     static constexpr int kAct = PL ? (HID / 32) * NT * PL * 64 : KG_HID * NT * 64;   // 16-byte entries
     float xin[NT * 16 * 16];           // input poses, [col][16] (9 used)
     f32x4 act1[kAct];                  // pose_encoder.0 output: [g][ct][lane] (fp32) / [chunk][ct][plane][lane]
@@ -372,7 +368,7 @@ __device__ __forceinline__ void stream_hk_step(__amdgpu_buffer_rsrc_t W, const i
 // on the critical path between the PC update and pose_encoder.0.
 // Also this wave's pose_encoder.0 A fragments and bias (output tiles 2 wid, 2 wid + 1 of an 8-wave
 // workgroup): loaded at kernel entry instead of being staged through LDS for every launch.
-constexpr int HSPLIT_WV = 8;   // waves per workgroup of the split-trunk kernels (the paired PC step: 4)
+constexpr int HSPLIT_WV = 8;   // waves per workgroup of the split-trunk kernels
 struct SplitScalars {
     float A0, B0, A2, B2;
     int ew2, ewh;

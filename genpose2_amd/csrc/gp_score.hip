@@ -23,18 +23,25 @@
 
 #include "gp_common.h"
 
-#include <cstring>
-#include <mutex>
-#include <vector>
 
-// Phase timestamps for tuning builds only (make EXTRA=-DPC_TRACE; read by scripts/pc_trace.py).
+// Phase timestamps for tuning builds only (make EXTRA=-DPC_TRACE; read by scripts/pc_trace.py). Per wave of the
+// first 256 workgroups, three launch slots (step parity; 2 = the finalize launch i = steps): slots 0..15
+// shader-clock stamps (s_memtime) of the marks, 16 / 17 the constant 100 MHz clock (s_memrealtime) at marks 0 / 8
+// (workgroup start / end on one chip-wide time base: s_memtime runs per XCD at the current shader clock), 18 the
+// HW_ID register | XCC_ID << 32.
 #ifdef PC_TRACE
-__device__ unsigned long long g_pc_trace[2 * 256 * 8 * 16];
+constexpr int PC_TR_SLOTS = 20;
+__device__ unsigned long long g_pc_trace[3 * 256 * 8 * PC_TR_SLOTS];
+#define PC_TR_AT(k) g_pc_trace[((trace_slot * 256 + blockIdx.x) * 8 + (threadIdx.x >> 6)) * PC_TR_SLOTS + (k)]
 #define PC_MARK(k)                                                                                       \
     do {                                                                                                 \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)                                                 \
-            g_pc_trace[((trace_slot * 256 + blockIdx.x) * 8 + (threadIdx.x >> 6)) * 16 + (k)] =          \
-                __builtin_amdgcn_s_memtime();                                                            \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) {                                               \
+            PC_TR_AT(k) = __builtin_amdgcn_s_memtime();                                                  \
+            if ((k) == 0 || (k) == 8) PC_TR_AT(16 + ((k) == 8)) = __builtin_amdgcn_s_memrealtime();      \
+            if ((k) == 0)                                                                                \
+                PC_TR_AT(18) = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) | \
+                               ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32); \
+        }                                                                                                \
     } while (0)
 extern "C" int gp_debug_pc_trace(unsigned long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pc_trace), sizeof(g_pc_trace)) == hipSuccess ? 0 : -1;
@@ -352,8 +359,7 @@ __device__ __forceinline__ float pc_score_norm(const PCArgs& a, const PCStep& cu
 // grad-norm reduction overlap), while the other waves make the next step's draws, stage the small
 // weights and issue their first weight-stream loads; one barrier (inside the trunk) joins them.
 template <int NT, int WV, int PL>   // PL 0: exact fp32 GEMMs, X3P: f16x3
-__global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(2))) void pc_step_kernel(PCArgs a, int i,
-                                                                                                PCStep cur, PCStep prev) {
+__global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCStep cur, PCStep prev) {
     constexpr int ROWS = NT * 16;
     static_assert(NT < WV, "at least one wave besides the update waves");
     __shared__ HeadSmem<NT, WV, PL> sm;
@@ -363,15 +369,11 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r0 = blockIdx.x * ROWS;
-    const int trace_slot = i & 1;
+    const int trace_slot = i == a.steps ? 2 : (i & 1);
     SplitScalars hs = {};
     if constexpr (SPLIT) hs = load_split_scalars<WV>(a.w);   // in flight across the update
     PC_MARK(0);
-#ifndef PC_UPD_PRIO
-#define PC_UPD_PRIO 0   // tuning: issue priority of the update waves over the draw / staging waves during the update
-#endif
     if (wid < NT) {
-        if constexpr (PC_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(PC_UPD_PRIO);
         // ---- every load first and unconditional (rows clamped: a guarded load becomes a branch,
         //      and the compiler then drains the first batch before issuing the next): the
         //      grad-norm partials of step i-1, then this lane's elements of x, s and the two draws.
@@ -409,7 +411,6 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         }
         PC_MARK(9);
         pc_update_rows<NT, WV, PL>(a, i, prev, sm, obj, g, lane, r0, gacc, x3, sv, z1v, z2v, hs, true, trace_slot);
-        if constexpr (PC_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         PC_MARK(12);
     }
     if (i == a.steps) return;  // finalize launch: no score evaluation
@@ -427,171 +428,6 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
                                               [&](int c, int o, float v) { a.s[(size_t)(r0 + c) * 9 + o] = v; });
     if (tid == 0) a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = t;
     PC_MARK(8);
-}
-
-// ============================================================================ persistent PC sampler
-// The whole T-step loop in one launch: each workgroup keeps its rows for every step, so x stays in the
-// update waves' registers, s and the next step's draws in LDS, the weight planes stay resident in each
-// XCD's L2 across steps (a kernel boundary writes back and invalidates it: 17.8 MB of fabric traffic per
-// launch for 0.92 MB of state), and the per-launch staging disappears. The grid-wide dependency of a
-// step -- grad_norm, the mean score norm over all rows (samplers.py:143) -- becomes an all-gather of one
-// 8-byte granule per workgroup {partial's bits, step tag}, stored write-through (agent-scope relaxed atomic:
-// global_store_dwordx2 sc1) by one lane after the workgroup's barrier and polled by every update wave
-// with sc1 loads (MI355X_MICROARCH.md, hand-off table row 1 with R2 granules: the payload travels inside
-// the polled word, so no ordering is needed). The granules are double-buffered by step parity: a workgroup
-// can only overwrite slot j&1 (step j+2) after every workgroup published step j+1, i.e. finished polling
-// step j. Every workgroup sums the same granules in the multi-launch kernel's order, so the two kernels
-// agree bit for bit. Requires every workgroup resident at once (gp_pc_sample checks nwg <= CUs; one
-// 64-candidate workgroup per CU by LDS); every wait is bounded: a workgroup that waits ~1 s sets the
-// status word, poisons its rows (NaN) and stops waiting, so a co-residency failure ends as an error and
-// never as a hang.
-struct PCPersist {
-    const float* tab;              // (steps, 5) step table
-    unsigned long long* gran;      // (2, nwg) granules, zero at launch
-    unsigned* cnt;                 // PC_SHARDS arrival counters, 128 B apart, zero at launch
-    int* status;                   // 0 ok; 1 a wait timed out
-};
-
-#ifndef PC_PERSIST_SPIN
-#define PC_PERSIST_SPIN (1u << 20)   // polls before a wait gives up (each ~1 us + 64 cycles of sleep)
-#endif
-
-// Arrival counters, one per XCD-sized shard (workgroup b counts on shard b % 8: the round-robin dealing puts
-// those workgroups on one XCD, so a shard's adds stay local -- for speed only, correctness does not depend on
-// placement), each on a 128-byte line of its own. A workgroup publishes step j's partial as its granule
-// (write-through store), waits for that store, then adds 1 to its shard: after step j, shard s holds
-// j * (workgroups in s). A waiting wave polls the 8 counters with 8 lanes (32 bytes a round instead of
-// every granule: polling all of them from 800 waves took ~3 TB/s of fabric from the weight streams), then
-// reads the granules once.
-constexpr int PC_SHARDS = 8;
-constexpr int PC_SHARD_STRIDE = 32;   // uint32 words per shard (128 B)
-
-__device__ __forceinline__ void pc_publish(unsigned long long* gran, unsigned* cnt, uint32_t tag, float partial) {
-    __hip_atomic_store(gran + blockIdx.x, ((unsigned long long)tag << 32) | __float_as_uint(partial), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the granule has landed before the arrival counts
-    __hip_atomic_fetch_add(cnt + (blockIdx.x % PC_SHARDS) * PC_SHARD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ float pc_gather_norms(const unsigned long long* gran, unsigned* cnt, int nwg, uint32_t tag,
-                                                 int lane, bool& timed_out, int* status) {
-    // arrivals first: lane s < 8 waits for shard s to reach tag * (its workgroup count)
-    const int s = lane < PC_SHARDS ? lane : 0;
-    const unsigned want = (unsigned)(nwg / PC_SHARDS + (s < nwg % PC_SHARDS ? 1 : 0)) * tag;
-    for (uint32_t spin = 0; !timed_out; ++spin) {
-        const unsigned have = __hip_atomic_load(cnt + s * PC_SHARD_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__all(have >= want)) break;
-        if (spin >= PC_PERSIST_SPIN) {
-            if (lane == 0) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            timed_out = true;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-    // then every granule once, in the multi-launch kernel's lane / index order; a stale tag (not expected
-    // once the counts are complete) is read again
-    float gacc = 0.f;
-    for (int t0 = 0; t0 < nwg; t0 += 512) {
-        float pv[8];
-        for (uint32_t spin = 0;; ++spin) {
-            bool ok = true;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const unsigned long long v = __hip_atomic_load(const_cast<unsigned long long*>(gran) + min(t0 + lane + 64 * u, nwg - 1),
-                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                pv[u] = __uint_as_float((uint32_t)v);
-                ok = ok && (uint32_t)(v >> 32) == tag;
-            }
-            if (__all(ok)) break;
-            if (timed_out || spin >= PC_PERSIST_SPIN) {
-                if (!timed_out && lane == 0) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                timed_out = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) gacc += t0 + lane + 64 * u < nwg ? pv[u] : 0.f;
-    }
-    return timed_out ? __builtin_nanf("") : gacc;
-}
-
-template <int NT, int WV, int PL>
-__global__ __launch_bounds__(WV * 64) void pc_persist_kernel(PCArgs a, PCPersist pp) {
-    constexpr int ROWS = NT * 16;
-    static_assert(NT < WV, "at least one wave besides the update waves");
-    __shared__ HeadSmem<NT, WV, PL> sm;
-    constexpr bool SPLIT = PL != 0;
-    __shared__ int obj[ROWS];
-    __shared__ float s_l[ROWS * 9];          // score of the last step, [row][9]
-    __shared__ float z_l[2][2][ROWS * 9];    // draws: [step parity][stream][row][9]
-    const PCArgs& a0 = a;
-    bool timed_out = false;
-    stage_small_weights<NT, WV, 0, !SPLIT>(a0.w, sm);   // once (published by the trunk's first barrier)
-    const int steps = a0.steps;
-    for (int i = 0; i <= steps; ++i) {
-        // every per-lane and per-wave value is derived again from a laundered thread id each step, so nothing
-        // is hoisted out of the loop and kept live (spilled) across the trunk
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const int lane = tid & 63;
-        const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-        const int r0 = blockIdx.x * ROWS;
-        const bool inj = a.z1 != nullptr;
-        const int p = lane & 3;
-        const int e0 = 3 * (p < 3 ? p : 0);
-        const int c_row = 16 * (wid < NT ? wid : 0) + (lane >> 2);              // update waves: this lane's row
-        const int trace_slot = i & 1;
-        PC_MARK(0);
-        SplitScalars hs = {};
-        if constexpr (SPLIT) hs = load_split_scalars(a.w);
-        if (wid < NT) {
-            PCStep prev = {};
-            if (i > 0) {
-                const float* tp = pp.tab + (size_t)(i - 1) * 5;
-                prev = PCStep{ld1(tp), ld1(tp + 1), ld1(tp + 2), ld1(tp + 3), ld1(tp + 4)};
-            }
-            // x: from the input at i = 0, then from xin, which holds the update's result for every valid row
-            // (the trunk only reads it), so no register carries it across the trunk
-            float x3[3], sv[3], z1v[3], z2v[3];
-            {
-                const int cc = min(c_row, ROWS - 1);
-                const size_t e = (size_t)min(r0 + c_row, a.rows - 1) * 9 + e0;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) x3[k] = i == 0 ? ld1(a.x + e + k) : sm.xin[cc * 16 + e0 + k];
-                const float* z1p = a.z1 + (size_t)(i > 0 ? i - 1 : 0) * a.rows * 9;
-                const float* z2p = a.z2 + (size_t)(i > 0 ? i - 1 : 0) * a.rows * 9;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    sv[k] = s_l[cc * 9 + e0 + k];
-                    z1v[k] = inj ? ld1(z1p + e + k) : z_l[(i - 1) & 1][0][cc * 9 + e0 + k];
-                    z2v[k] = inj ? ld1(z2p + e + k) : z_l[(i - 1) & 1][1][cc * 9 + e0 + k];
-                }
-            }
-            const float gacc = i > 0 ? pc_gather_norms(pp.gran + (size_t)((i - 1) & 1) * a.nwg, pp.cnt, a.nwg, (uint32_t)i,
-                                                       lane, timed_out, pp.status)
-                                     : 0.f;
-            PC_MARK(9);
-            pc_update_rows<NT, WV, PL>(a, i, prev, sm, obj, wid, lane, r0, gacc, x3, sv, z1v, z2v, hs, false, trace_slot);
-            PC_MARK(12);
-        }
-        if (i == steps) break;
-        const float* tc = pp.tab + (size_t)i * 5;
-        const PCStep cur = PCStep{ld1(tc), ld1(tc + 1), ld1(tc + 2), ld1(tc + 3), ld1(tc + 4)};
-        if (wid >= NT && !inj)
-            pc_make_draws<NT, WV>(a, i, r0, [&](int st, int c, int e, float v) { z_l[i & 1][st][c * 9 + e] = v; });
-        if constexpr (SPLIT)
-            head_trunk_x3<NT, WV, true>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot, hs);
-        else
-            head_trunk<NT, WV>(a.w, a.pobj, a.tproj + (size_t)i * 768, obj, sm, trace_slot);
-        PC_MARK(7);
-        const bool last = i == steps - 1;   // the last score also goes to the workspace's s, as per-step launches leave it
-        const float t = pc_score_norm<NT, WV, PL>(a, cur, sm, r0, wid, lane, [&](int c, int o, float v) {
-            s_l[c * 9 + o] = v;
-            if (last) a.s[(size_t)(r0 + c) * 9 + o] = v;
-        });
-        PC_MARK(8);
-        if (tid == 0) pc_publish(pp.gran + (size_t)(i & 1) * a.nwg, pp.cnt, (uint32_t)(i + 1), t);
-    }
 }
 
 // Device standard normals in the PC sampler's draw layout: out[r][c] = philox_normal4(seed, stream,
@@ -623,90 +459,9 @@ extern "C" size_t gp_pc_workspace_size(int rows) {
     return sizeof(float) * ((size_t)rows * 9 * 5 + 2 * ntiles) + 256;
 }
 
-// PC_PAIR: where the f16x3 path would take 64-candidate workgroups of 8 waves, take 32-candidate workgroups
-// of 4 waves instead, two per CU (pc_step_kernel<2, 4, X3P>: <= 256 VGPRs, ~68 KiB of LDS each). The two
-// workgroups on a CU run independently, so one's serial VALU phases (update, pose_encoder.0, epilogues) overlap
-// the other's MFMA stream (scripts/mix16_probe.hip: f32 VALU beside f16 MFMA leaves the MFMA rate unchanged),
-// at the price of streaming the GEMM weights once per 32 instead of 64 candidates. GENPOSE2_PC_PAIR=0/1
-// overrides the build default.
-#ifndef PC_PAIR_DEFAULT
-#define PC_PAIR_DEFAULT 0
-#endif
-static bool pc_pair(int rows, bool split) {
-    if (!split || head_pick_nt(rows, split) != 4) return false;
-    const char* env = getenv("GENPOSE2_PC_PAIR");
-    return env ? env[0] != '0' : PC_PAIR_DEFAULT != 0;
-}
-static int pc_pick_nt(int rows, bool split) { return pc_pair(rows, split) ? 2 : head_pick_nt(rows, split); }
-
-// The persistent sampler (pc_persist_kernel) runs when enabled (GENPOSE2_PC_PERSIST, default PC_PERSIST_DEFAULT),
-// when every workgroup fits on the device at once (nwg <= compute units: the grid-wide exchange waits for all of
-// them) and when its granules, status word and step table fit the workspace's draw region, which the persistent
-// kernel does not use (its draws stay in LDS). Fills pp and returns true then.
-#ifndef PC_PERSIST_DEFAULT
-#define PC_PERSIST_DEFAULT 0
-#endif
-// Pinned host staging for the persistent sampler's per-call upload of the step table: a slot is
-// written again only after the copy that read it has completed (its event), so the upload never depends on
-// how hipMemcpyAsync treats pageable memory.
-struct PinnedSlot {
-    char* host;
-    size_t bytes;
-    hipEvent_t ev;
-};
-static std::mutex g_stage_mu;
-static std::vector<PinnedSlot> g_stage;
-static int pinned_upload(void* dev, const void* a, size_t na, hipStream_t st) {
-    std::lock_guard<std::mutex> lk(g_stage_mu);
-    PinnedSlot* slot = nullptr;
-    for (auto& sl : g_stage)
-        if (sl.bytes >= na && hipEventQuery(sl.ev) == hipSuccess) {
-            slot = &sl;
-            break;
-        }
-    if (!slot) {
-        PinnedSlot sl{nullptr, std::max<size_t>(na, 64 << 10), nullptr};
-        if (hipHostMalloc(reinterpret_cast<void**>(&sl.host), sl.bytes, hipHostMallocDefault) != hipSuccess)
-            return gp_check_launch("pc_sample: pinned staging");
-        if (hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) {
-            (void)hipHostFree(sl.host);
-            return gp_check_launch("pc_sample: staging event");
-        }
-        g_stage.push_back(sl);
-        slot = &g_stage.back();
-    }
-    memcpy(slot->host, a, na);
-    if (hipMemcpyAsync(dev, slot->host, na, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipEventRecord(slot->ev, st) != hipSuccess)
-        return gp_check_launch("pc_sample: staging copy");
-    return GP_OK;
-}
-
-static int pc_device_cus() {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 0;
-    return n;
-}
-static constexpr size_t pc_sync_bytes() { return sizeof(unsigned) * PC_SHARDS * PC_SHARD_STRIDE + 128; }
-static bool pc_persist_layout(const PCArgs& a, int rows, int steps, PCPersist& pp) {
-    const char* env = getenv("GENPOSE2_PC_PERSIST");
-    const bool on = env ? env[0] != '0' : PC_PERSIST_DEFAULT != 0;
-    if (!on || a.nwg > pc_device_cus()) return false;
-    const uintptr_t base = ((uintptr_t)a.zbuf + 15) & ~(uintptr_t)15;
-    const size_t gran = ((sizeof(unsigned long long) * 2 * a.nwg + 127) & ~(size_t)127) + pc_sync_bytes();
-    const size_t need = gran + sizeof(float) * 5 * (size_t)steps;
-    if (base + need > (uintptr_t)(a.zbuf + (size_t)rows * 36)) return false;
-    pp.gran = reinterpret_cast<unsigned long long*>(base);
-    pp.cnt = reinterpret_cast<unsigned*>(base + gran - pc_sync_bytes());
-    pp.status = reinterpret_cast<int*>(pp.cnt + PC_SHARDS * PC_SHARD_STRIDE);
-    pp.tab = reinterpret_cast<const float*>(base + gran);
-    return true;
-}
-
 // Candidates per PC-step workgroup that gp_pc_sample picks for `rows` (split: head weights with
 // the f16 planes) -- lets callers size their accounting from the kernel's real tiling.
-extern "C" int gp_pc_tile_rows(int rows, int split) { return 16 * pc_pick_nt(rows, split != 0); }
+extern "C" int gp_pc_tile_rows(int rows, int split) { return 16 * head_pick_nt(rows, split != 0); }
 
 // cond_pc_sampler's time grid and VE SDE scalars (samplers.py:129-130, sde.py:15-27) as float32 rows
 // {t, sigma(t), g(t), dt, sqrt(dt)} -- the table genpose2_amd/sde.py forms with torch, for hosts
@@ -752,8 +507,7 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     GP_REQUIRE(workspace_bytes >= gp_pc_workspace_size(rows), "pc_sample: workspace too small");
     // split-f16 GEMMs when the packed planes are given (gp_head_weights), exact fp32 otherwise
     const bool split = w->pe2_h != nullptr;
-    const int nt = pc_pick_nt(rows, split);
-    const bool pair = pc_pair(rows, split);
+    const int nt = head_pick_nt(rows, split);
     GP_REQUIRE(!split || (w->h1p_h && w->hsc), "pc_sample: pe2_h, h1p_h and hsc must be given together");
     PCArgs a;
     a.w = *w;
@@ -776,26 +530,6 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     a.nwg = (rows + 16 * nt - 1) / (16 * nt);
     a.ls_coef = snr * 3.0f;  // snr * sqrt(pose_dim=9) in fp32 (0.48 rounds identically)
     const dim3 grid(a.nwg);
-    PCPersist pp;
-    if (!pair && pc_persist_layout(a, rows, steps, pp)) {
-        // one launch for the whole loop (pc_persist_kernel): the step table and zeroed granules in the workspace
-        if (hipMemsetAsync(pp.gran, 0, reinterpret_cast<const char*>(pp.tab) - reinterpret_cast<char*>(pp.gran), stream) !=
-            hipSuccess)
-            return gp_check_launch("pc_sample: persistent set-up");
-        const int rc = pinned_upload(const_cast<float*>(pp.tab), step_tab, sizeof(float) * 5 * steps, stream);
-        if (rc) return rc;
-        if (nt == 4)
-            hipLaunchKernelGGL((pc_persist_kernel<4, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, pp);
-        else if (nt == 2 && split)
-            hipLaunchKernelGGL((pc_persist_kernel<2, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, pp);
-        else if (nt == 2)
-            hipLaunchKernelGGL((pc_persist_kernel<2, PC_WV2, 0>), grid, dim3(PC_WV2 * 64), 0, stream, a, pp);
-        else if (split)
-            hipLaunchKernelGGL((pc_persist_kernel<1, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, pp);
-        else
-            hipLaunchKernelGGL((pc_persist_kernel<1, PC_WV1, 0>), grid, dim3(PC_WV1 * 64), 0, stream, a, pp);
-        return gp_check_launch("pc_persist_kernel");
-    }
     for (int i = 0; i <= steps; ++i) {
         PCStep cur = {}, prev = {};
         if (i < steps) cur = PCStep{step_tab[5 * i], step_tab[5 * i + 1], step_tab[5 * i + 2], step_tab[5 * i + 3],
@@ -804,12 +538,8 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
                                  step_tab[5 * (i - 1) + 3], step_tab[5 * (i - 1) + 4]};
         if (nt == 4)
             hipLaunchKernelGGL((pc_step_kernel<4, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
-        else if (pair)
-            hipLaunchKernelGGL((pc_step_kernel<2, 4, X3P>), grid, dim3(4 * 64), 0, stream, a, i, cur, prev);
-        else if (nt == 2 && split)
-            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else if (nt == 2)
-            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV2, 0>), grid, dim3(PC_WV2 * 64), 0, stream, a, i, cur, prev);
+            hipLaunchKernelGGL((pc_step_kernel<2, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else if (split)
             hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else

@@ -68,6 +68,9 @@ class EncoderModel:
         # geometry(): levels 1-3 of the FPS chain and ball lists on a side stream, beside level 0's MLPs
         self.geometry_overlap = os.environ.get("GENPOSE2_GEOM_OVERLAP", "1") == "1"
         self._geo_stream: Optional[torch.cuda.Stream] = None
+        # completion of the last side-stream geometry write into self._ws: every later write into the
+        # workspace (geometry() again, forward() without a geometry) is ordered after it on its stream
+        self._geo_event: Optional[torch.cuda.Event] = None
         self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
 
     @property
@@ -99,6 +102,11 @@ class EncoderModel:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
+    def _after_side_writes(self, cur) -> None:
+        """Order the current stream after this model's outstanding side-stream geometry writes."""
+        if self._geo_event is not None:
+            cur.wait_event(self._geo_event)
+
     @staticmethod
     def _xyz(pts: torch.Tensor) -> torch.Tensor:
         pts = require_device_tensor(pts, "pts")
@@ -115,6 +123,7 @@ class EncoderModel:
         ws = self.workspace(B, N)
         self._gen += 1
         cur = torch.cuda.current_stream(self.device)
+        self._after_side_writes(cur)
         if not self.geometry_overlap:
             check(self.lib.gp_encoder_geometry(ctypes.c_void_p(pts.data_ptr()), B, N, ctypes.c_void_p(ws.data_ptr()),
                                                ws.numel(), ctypes.c_void_p(cur.cuda_stream)), "encoder_geometry")
@@ -138,6 +147,7 @@ class EncoderModel:
         pts.record_stream(side)
         ev = torch.cuda.Event()
         ev.record(side)
+        self._geo_event = ev
         return EncoderGeometry(ws, ev, key, self, self._gen, event0=ev0)
 
     def forward(self, pts: torch.Tensor, return_workspace: bool = False,
@@ -149,6 +159,7 @@ class EncoderModel:
         B, N, _ = pts.shape
         feat = torch.empty((B, arch.PTS_FEAT_DIM), dtype=torch.float32, device=self.device)
         ws = self.workspace(B, N)
+        self._after_side_writes(torch.cuda.current_stream(self.device))
         st = ctypes.c_void_p(stream_handle(self.device))
         if geometry is None:
             self._gen += 1   # the self-contained pass rewrites the geometry in this workspace

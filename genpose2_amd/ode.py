@@ -414,6 +414,11 @@ def _side_resources(dev):
     return r
 
 
+# Measurement hook (bench.py): when a list, every attempt's six stage launches are bracketed by a pair of
+# timing events on the launch stream, appended as (start, end, rows); the final no-op attempt is not recorded.
+STAGE_EVENTS: Optional[list] = None
+
+
 def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.ndarray] = None,
                 max_attempts: int = 100000):
     """solve_ivp(..., method="RK45", t_eval) with the step controller on the device.
@@ -461,7 +466,14 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
         launch(n + 1, 1)                       # decides attempt n, prepares attempt n+1
         ev = torch.cuda.Event()
         ev.record(stream)
+        timing = STAGE_EVENTS is not None
+        if timing:
+            s0 = torch.cuda.Event(enable_timing=True)
+            s1 = torch.cuda.Event(enable_timing=True)
+            s0.record(stream)
         launch(n + 1, 2)                       # attempt n+1 (no-op if attempt n ended the solve)
+        if timing:
+            s1.record(stream)
         off = ((n + 2) & 1) * rec + _STATUS_OFF
         side.wait_event(ev)
         with torch.cuda.stream(side):
@@ -469,6 +481,8 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
         side.synchronize()
         if int(stat[0]) != 0:
             break
+        if timing:
+            STAGE_EVENTS.append((s0, s1, be.R))
         n += 1
         if n > max_attempts:
             raise RuntimeError("RK45: attempt limit reached")

@@ -129,6 +129,10 @@ def test_energy_rank_aggregate_r12800_vs_reference(arith):
     n_diff, bad = _rank_mismatches(e_np, idx, g["cl_energy64"], 2 * own.max())
     print(arith, "clustered: order positions differing from the reference", n_diff, "(not near-ties:", len(bad), ")")
     assert not bad, bad[:5]
+    if arith == "fast":
+        # the default arithmetic ranks the clustered set exactly as the reference does (the energy epilogue sums in
+        # torch-CPU's order, gp_score.hip head_eval_kernel); exact fp32 MFMA differs at near-ties only (checked above)
+        assert n_diff == 0, n_diff
     got = aggregate.aggregate_pose(pose, torch.from_numpy(g["cl_energy"]).to(DEV), 0.4, 1, 0.05, 0.1667,
                                    retain_num=keep)
     _check_agg(got.cpu().numpy(), g["cl_aggregated_c1"])

@@ -172,6 +172,30 @@ def test_encoder_shared_geometry_bit_exact(N, score_agent):
     score_agent.encoder.geometry_overlap = True
 
 
+def test_encoder_geometry_then_forward_unsynchronised(score_agent):
+    """The producer's own writes are ordered after its side-stream geometry (levels 1-3): geometry() followed at
+    once -- no synchronize, no consumer waiting on its event -- by a self-contained forward() of other points, and
+    by a second geometry(), leave the workspace and features exactly as an isolated forward() does."""
+    from genpose2_amd import synthetic
+    enc = score_agent.encoder
+    pts, _ = synthetic.make_batch(31, 64, 1024, n_unique_every=7)
+    other, _ = synthetic.make_batch(32, 64, 1024, n_unique_every=7)
+    p, o = torch.from_numpy(pts).to(DEV), torch.from_numpy(other).to(DEV)
+    ref_p = enc.forward(p).clone()
+    ref_o = enc.forward(o).clone()
+    torch.cuda.synchronize()
+    assert enc.geometry_overlap
+    for _ in range(3):
+        enc.geometry(p)
+        got_o = enc.forward(o)          # rewrites every level's geometry while the side stream may still run
+        enc.geometry(o)
+        enc.geometry(p)                 # a second geometry() over level 0 while levels 1-3 of the first run
+        g = enc.geometry(p)
+        got_p = enc.forward(p, geometry=g)
+        torch.cuda.synchronize()
+        assert torch.equal(got_o, ref_o) and torch.equal(got_p, ref_p)
+
+
 def test_encoder_batch_independence(score_agent):
     from genpose2_amd import synthetic
     pts, _ = synthetic.make_batch(5, 6, 1024, n_unique_every=4)
@@ -746,43 +770,6 @@ def test_pc_philox_equals_injected_draws(score_agent, B, K):
     z2 = torch.stack([device.randn(seed, 2 * j + 1, R, 9, DEV) for j in range(T)])
     res_i, q_i, xs_i = heads.pc_sample(pobj, tproj, tab, x0.clone(), K, center, z1=z1, z2=z2, want_xs=True)
     assert torch.equal(res_p, res_i) and torch.equal(q_p, q_i) and torch.equal(xs_p, xs_i)
-
-
-@pytest.mark.parametrize("arith", ["f16x3", "f32"])
-@pytest.mark.parametrize("B,K,inject", [(4, 8, False), (90, 50, True), (164, 50, False), (256, 50, False),
-                                        (256, 50, True)])
-def test_pc_persistent_equals_per_step_launches(score_agent, monkeypatch, B, K, inject, arith):
-    """The persistent sampler (one launch, grid-wide norm exchange through polled granules) against one launch
-    per step (the kernel boundary as the exchange): final poses, quaternions, the final state x and the whole
-    trajectory bit for bit, over every tile width (16 / 32 / 64 candidates, ragged last tiles), both GEMM
-    arithmetics, Philox and injected noise."""
-    from genpose2_amd import device, sde
-    T, seed = 12, 5
-    R = B * K
-    heads = score_agent.heads
-    heads.set_arith(arith)
-    try:
-        tab = sde.pc_step_table(T)
-        tproj = heads.time_proj(torch.from_numpy(tab[:, 0]).to(DEV))
-        g = torch.Generator(device=DEV).manual_seed(B)
-        pobj = heads.object_proj(torch.rand(B, 1024, device=DEV, generator=g))
-        center = torch.rand(B, 3, device=DEV, generator=g)
-        x0 = torch.randn(R, 9, device=DEV, generator=g) * 50
-        kw = {}
-        if inject:
-            kw = dict(z1=torch.randn(T, R, 9, device=DEV, generator=g), z2=torch.randn(T, R, 9, device=DEV, generator=g))
-        out = {}
-        for persist in ("0", "1"):
-            monkeypatch.setenv("GENPOSE2_PC_PERSIST", persist)
-            x = x0.clone()
-            res, q, xs = heads.pc_sample(pobj, tproj, tab, x, K, center, seed=seed, want_xs=True, **kw)
-            torch.cuda.synchronize()
-            out[persist] = (res, q, xs, x)
-        for name, a, b in zip(("res", "q", "xs", "x"), out["0"], out["1"]):
-            assert torch.isfinite(b).all(), name
-            assert torch.equal(a, b), f"{name}: max diff {(a - b).abs().max().item()}"
-    finally:
-        heads.set_arith("f16x3")
 
 
 # ---------------------------------------------------------------- stage hand-off (SURVEY 8f rank 4)
