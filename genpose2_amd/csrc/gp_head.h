@@ -853,6 +853,26 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
     float pv[SM::kRedV];
 #pragma unroll
     for (int v = 9 * NT; v < SM::kRedV; ++v) pv[v] = 0.f;
+#if X3_DIAG & 8
+    // timing diagnostic: one wave per SIMD runs head layer 1 for its own output tiles and its sibling's (same
+    // results), the sibling idles -- the single-wave stream rate inside the kernel
+    if (wid < WV / 2) {
+        head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
+        PC_MARK(13);
+        head_x3_head<1, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
+        PC_MARK(14);
+        head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
+        const int vw = wid + WV / 2;
+        int TV[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) TV[t] = vw * TPW + t;
+        stream_x3_step<0, DH, TPW, NT, DH>(WH, TV, act2h, lane, voff, ringh, acc2, cor2);
+        head_x3_init_load<0, NT, TPW>(RP, RT, vo, vw, lane, tpv, pov);
+        head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, vw, lane, ringh, tpv, pov, pv);
+        head_x3_head<1, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, vw, lane, ringh, tpv, pov, pv);
+        head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, vw, lane, ringh, tpv, pov, pv);
+    }
+#else
     head_x3_head<0, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
     if constexpr (X3_HEAD_BARRIER) __syncthreads();
     PC_MARK(13);
@@ -860,6 +880,7 @@ __device__ __forceinline__ void head_trunk_x3(const gp_head_weights& w, const fl
     if constexpr (X3_HEAD_BARRIER) __syncthreads();
     PC_MARK(14);
     head_x3_head<2, NT, WV, TPW, DH>(WH, act2h, RP, RT, vo, sm, uh, sh, wid, lane, ringh, tpv, pov, pv);
+#endif
     if constexpr (X3_PRIO) __builtin_amdgcn_s_setprio(0);
     PC_MARK(5);
     if constexpr ((3 * NT) % 4 != 0) {
@@ -1012,6 +1033,20 @@ __device__ __forceinline__ float dot_chains(const float* __restrict__ W, size_t 
     return p[0];
 }
 
+// HOIST64 (diagnostic builds): the hoisted head-1 rows' GEMMs (object block, t_encoder, t block) accumulated in
+// float64 and rounded once -- how far the order of those sums moves the T0=1 ODE path (tests/test_gpu_parity.py
+// test_ode_t1_calibrated_vs_float64). The Fourier embedding stays the reference's float32 computation.
+#ifndef HOIST64
+#define HOIST64 0
+#endif
+template <int N>
+__device__ __forceinline__ double dot_f64(const float* __restrict__ W, size_t stride, const float* x) {
+    double s = 0.0;   // each fp32 x fp32 product is exact in float64
+#pragma unroll 8
+    for (int c = 0; c < N; ++c) s = fma((double)W[(size_t)c * stride], (double)x[c], s);
+    return s;
+}
+
 __device__ __forceinline__ void time_row(const gp_head_weights& w, float t, float* emb, float* tf,
                                          float* __restrict__ out, int o0 = 0, int o1 = 768) {
     const int i = threadIdx.x;
@@ -1021,7 +1056,13 @@ __device__ __forceinline__ void time_row(const gp_head_weights& w, float t, floa
         emb[64 + i] = cosf(a);
     }
     __syncthreads();
+#if HOIST64
+    if (i < 128) tf[i] = fmaxf((float)(dot_f64<128>(w.te_w_t + i, 128, emb) + (double)w.te_b[i]), 0.f);
+    __syncthreads();
+    for (int o = o0 + i; o < o1; o += HT) out[o] = (float)dot_f64<128>(w.h1t_t + o, 768, tf);
+#else
     if (i < 128) tf[i] = fmaxf(dot_chains<128, 16>(w.te_w_t + i, 128, emb) + w.te_b[i], 0.f);
     __syncthreads();
     for (int o = o0 + i; o < o1; o += HT) out[o] = dot_chains<128, 16>(w.h1t_t + o, 768, tf);
+#endif
 }

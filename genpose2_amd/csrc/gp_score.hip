@@ -59,7 +59,11 @@ __global__ __launch_bounds__(HT) void object_proj_kernel(gp_head_weights w, cons
     for (int i = threadIdx.x; i < 1024; i += HT) sf[i] = feat[(size_t)b * 1024 + i];
     __syncthreads();
     const int o = blockIdx.x * HT + threadIdx.x;  // 0..767
+#if HOIST64
+    pobj[(size_t)b * 768 + o] = (float)(dot_f64<1024>(w.h1pts_t + o, 768, sf) + (double)w.h1_b[o]);
+#else
     pobj[(size_t)b * 768 + o] = dot_chains<1024, 32>(w.h1pts_t + o, 768, sf) + w.h1_b[o];
+#endif
 }
 
 extern "C" int gp_head_object_proj(const gp_head_weights* w, const float* pts_feat, int b, float* pobj,
