@@ -513,7 +513,7 @@ def main():
             # the energy encoder needs only the points: overlap it with the score sampler
             # (as genpose2_amd.runner.EvaluationPipeline does)
             edata = {k: data0[k] for k in ("pts", "pts_center", "dino_layers", "roi_xs", "roi_ys") if k in data0}
-            if args.share_geometry and not pipe and leg.dino == "none":
+            if args.share_geometry and not pipe:
                 score.encode_geometry(data)          # one geometry pass for both encoders of this batch
                 edata["enc_geometry"] = data["enc_geometry"]
 
@@ -719,8 +719,7 @@ def main():
                                    f"{', DINO-pointwise fused encoders' if args.dino == 'pointwise' else ''}",
                        "global_batch": B * ws, "seq_len": T, "parallelism": f"dp{ws} (object shards)",
                        "encoder_pipelined": bool(args.pipeline),
-                       "shared_geometry": bool(args.share_geometry and cfgd["energy"] and args.dino == "none"
-                                               and not args.pipeline),
+                       "shared_geometry": bool(args.share_geometry and cfgd["energy"] and not args.pipeline),
                        "energy_encoder": (["after the sampler", "beside the sampler", "beside the score encoder"]
                                           [args.energy_overlap] if cfgd["energy"] else None)},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",

@@ -54,6 +54,8 @@ _SIGS: Dict[str, tuple] = {
                                                c_size_t, c_void_p, c_int, c_int, c_void_p]),
     "gp_sa_level": (c_int, [c_void_p, c_int64_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t,
                             c_void_p, c_void_p]),
+    "gp_sa_level_geom": (c_int, [c_void_p, c_int64_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_size_t, c_void_p, c_void_p]),
     "gp_linear": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     "gp_linear_split_words": (c_size_t, [c_int, c_int]),
     "gp_linear_split": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int,

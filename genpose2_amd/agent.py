@@ -151,17 +151,16 @@ class PoseNet:
             if rgb is None:
                 feat = self.img_encoder.forward(self.dino_layers(data))
                 rgb = self.img_encoder.gather(feat, data["roi_xs"], data["roi_ys"])
-            return self.encoder.forward(data["pts"], rgb)
+            return self.encoder.forward(data["pts"], rgb, geometry=data.get("enc_geometry"))
         return self.encoder.forward(data["pts"], geometry=data.get("enc_geometry"))
 
     @torch.no_grad()
     def encode_geometry(self, data):
         """data["enc_geometry"]: FPS indices, centroids and ball lists of data["pts"] for every level, in
-        this agent's encoder workspace. Every Light-encoder agent that encodes the same points (the
-        ScoreNet and EnergyNet of one batch) then runs only its MLPs; valid until this agent encodes
-        again. No-op for the pointwise model (its levels run one by one)."""
-        if not self.pointwise:
-            data["enc_geometry"] = self.encoder.geometry(data["pts"])
+        this agent's encoder workspace. Every agent of the same encoder family (Light or DINO-pointwise) that
+        encodes the same points (the ScoreNet and EnergyNet of one batch) then runs only its MLPs; valid until
+        this agent encodes again."""
+        data["enc_geometry"] = self.encoder.geometry(data["pts"])
 
     @torch.no_grad()
     def encode_func(self, data):

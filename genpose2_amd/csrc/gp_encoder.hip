@@ -1964,15 +1964,34 @@ extern "C" int gp_encoder_forward_geom(const float* wbuf, const int64_t* layer_o
                                           st);
 }
 
-extern "C" int gp_sa_level(const float* wbuf, const int64_t* layer_off, int level, int c_prev, const float* pts, int B,
-                           int N, const float* feat_prev, void* workspace, size_t workspace_bytes, float* out,
-                           hipStream_t st) {
+static int sa_level_impl(const float* wbuf, const int64_t* layer_off, int level, int c_prev, const float* pts, int B,
+                         int N, const float* feat_prev, const void* geometry, void* workspace, size_t workspace_bytes,
+                         float* out, hipStream_t st) {
     int rc = enc_check(wbuf, layer_off, pts, B, N, workspace, workspace_bytes);
     if (rc) return rc;
     GP_REQUIRE(level >= 0 && level < 5 && out, "sa_level: level %d out of range or null out", level);
     GP_REQUIRE(level == 0 ? (c_prev % 16 == 0 && c_prev >= 0 && c_prev <= 1024) : c_prev == kCout[level - 1],
                "sa_level: level %d takes c_prev = %d (got %d)", level, level ? kCout[level - 1] : 0, c_prev);
     GP_REQUIRE(c_prev == 0 || feat_prev, "sa_level: c_prev %d needs feat_prev", c_prev);
-    const EncCtx c = enc_ctx(wbuf, layer_off, pts, B, N, workspace);
+    const EncCtx c = enc_ctx(wbuf, layer_off, pts, B, N, workspace, const_cast<void*>(geometry));
     return run_sa_level(c, level, c_prev, feat_prev, out, false, st);
+}
+
+extern "C" int gp_sa_level(const float* wbuf, const int64_t* layer_off, int level, int c_prev, const float* pts, int B,
+                           int N, const float* feat_prev, void* workspace, size_t workspace_bytes, float* out,
+                           hipStream_t st) {
+    return sa_level_impl(wbuf, layer_off, level, c_prev, pts, B, N, feat_prev, nullptr, workspace, workspace_bytes, out,
+                         st);
+}
+
+// gp_sa_level over the geometry gp_encoder_geometry left in `geometry` (FPS indices, centroids and both ball lists of
+// every level; it may be `workspace` itself): no ball query runs, the level's scratch goes to `workspace`. Two fused
+// encoders of the same points (the ScoreNet's and the EnergyNet's) then share one geometry pass, as the Light
+// encoders do (gp_encoder_forward_geom).
+extern "C" int gp_sa_level_geom(const float* wbuf, const int64_t* layer_off, int level, int c_prev, const float* pts,
+                                int B, int N, const float* feat_prev, const void* geometry, void* workspace,
+                                size_t workspace_bytes, float* out, hipStream_t st) {
+    GP_REQUIRE(geometry, "sa_level_geom: null geometry");
+    return sa_level_impl(wbuf, layer_off, level, c_prev, pts, B, N, feat_prev, geometry, workspace, workspace_bytes,
+                         out, st);
 }

@@ -30,7 +30,7 @@ import torch
 
 from . import _lib, arch, pack, weights
 from ._lib import check
-from .device import require_device_tensor, stream_handle
+from .device import EncoderGeometry, require_device_tensor, stream_handle
 
 _ACT = {"none": 0, "relu": 1, "sigmoid": 2, "gate_mix": 3}   # gate_mix: gp_linear_split only
 
@@ -123,6 +123,7 @@ class FusEncoderModel:
         self._bias: Optional[torch.Tensor] = None
         self._fws: Optional[torch.Tensor] = None
         self._rmax: Optional[torch.Tensor] = None
+        self._gen = 0   # bumped whenever this model writes geometry into its workspace
         self.fused_bias = os.environ.get("GENPOSE2_FUSED_RELPE", "1") == "1"
         self.set_arith(os.environ.get("GENPOSE2_ENC_ARITH", "split_f16"))
 
@@ -272,7 +273,30 @@ class FusEncoderModel:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def forward(self, pts: torch.Tensor, rgb_feat: torch.Tensor, return_levels: bool = False):
+    def geometry(self, pts: torch.Tensor) -> EncoderGeometry:
+        """FPS indices, centroids and both ball lists of every level (gp_encoder_geometry) into this model's
+        workspace, for this encoder and any other encoder of the same points (forward(geometry=...)): the ScoreNet
+        and EnergyNet fused encoders of one batch then share one geometry pass (the ball query then runs once per
+        level, not once per encoder and level). Valid until this model encodes again."""
+        key = (require_device_tensor(pts, "pts").data_ptr(), tuple(pts.shape[:2]))
+        pts = require_device_tensor(pts, "pts")
+        B, N, C = pts.shape
+        if C != 3:
+            pts = pts[..., :3].contiguous()
+        ws = self.workspace(B, N)
+        self._gen += 1
+        cur = torch.cuda.current_stream(self.device)
+        check(self.lib.gp_encoder_geometry(_vp(pts), B, N, _vp(ws), ws.numel(), ctypes.c_void_p(cur.cuda_stream)),
+              "encoder_geometry")
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        return EncoderGeometry(ws, ev, key, self, self._gen)
+
+    def forward(self, pts: torch.Tensor, rgb_feat: torch.Tensor, return_levels: bool = False,
+                geometry: Optional[EncoderGeometry] = None):
+        """geometry: from geometry() on the same points (this model's or another fused encoder's): the levels then
+        read its FPS indices, centroids and ball lists (gp_sa_level_geom) after the stream waits for it."""
+        key = (require_device_tensor(pts, "pts").data_ptr(), tuple(pts.shape[:2]))
         pts = require_device_tensor(pts, "pts")
         rgb_feat = require_device_tensor(rgb_feat, "rgb_feat")
         B, N, C = pts.shape
@@ -281,7 +305,19 @@ class FusEncoderModel:
         if tuple(rgb_feat.shape) != (B, N, arch.DINO_DIM):
             raise ValueError(f"rgb_feat must be ({B}, {N}, {arch.DINO_DIM}), got {tuple(rgb_feat.shape)}")
         ws = self.workspace(B, N)
-        check(self.lib.gp_encoder_fps(_vp(pts), B, N, _vp(ws), ws.numel(), self._s()), "encoder_fps")
+        if geometry is None:
+            self._gen += 1   # the self-contained pass rewrites the geometry in this workspace
+            check(self.lib.gp_encoder_fps(_vp(pts), B, N, _vp(ws), ws.numel(), self._s()), "encoder_fps")
+            geo = None
+        else:
+            if geometry.key != key:
+                raise ValueError("encoder geometry was computed for other points")
+            if geometry.producer is not None and geometry.producer._gen != geometry.gen:
+                raise ValueError("encoder geometry is stale: its model encoded other points since")
+            torch.cuda.current_stream(self.device).wait_event(geometry.event)
+            geo = geometry.ws
+            if geo is not ws:
+                geo.record_stream(torch.cuda.current_stream(self.device))
         off = np.zeros(25, np.int64)
         check(self.lib.gp_encoder_workspace_layout(B, N, off.ctypes.data_as(_lib.c_int64_p)))
         orig, feats = rgb_feat, rgb_feat
@@ -299,10 +335,16 @@ class FusEncoderModel:
             m = arch.NPOINTS[lv] if lv < 4 else 1
             cout = arch.level_out_channels(lv)
             sa = torch.empty((B, m, cout), dtype=torch.float32, device=self.device)
-            check(self.lib.gp_sa_level(_vp(self.wbuf), self.offsets.ctypes.data_as(_lib.c_int64_p), lv, feats.shape[2],
-                                       _vp(pts), B, N, _vp(feats), _vp(ws), ws.numel(), _vp(sa), self._s()),
-                  f"sa_level {lv}")
-            xyz = ws[off[lv * 5 + 1]:].view(torch.float32)[: B * m * 3].view(B, m, 3) if lv < 4 else None
+            if geo is None:
+                check(self.lib.gp_sa_level(_vp(self.wbuf), self.offsets.ctypes.data_as(_lib.c_int64_p), lv,
+                                           feats.shape[2], _vp(pts), B, N, _vp(feats), _vp(ws), ws.numel(), _vp(sa),
+                                           self._s()), f"sa_level {lv}")
+            else:
+                check(self.lib.gp_sa_level_geom(_vp(self.wbuf), self.offsets.ctypes.data_as(_lib.c_int64_p), lv,
+                                                feats.shape[2], _vp(pts), B, N, _vp(feats), _vp(geo), _vp(ws),
+                                                ws.numel(), _vp(sa), self._s()), f"sa_level_geom {lv}")
+            gsrc = ws if geo is None else geo
+            xyz = gsrc[off[lv * 5 + 1]:].view(torch.float32)[: B * m * 3].view(B, m, 3) if lv < 4 else None
             feats = self.transformer(lv, sa, xyz)
             rec.update(sa=sa, tf=feats)
             levels.append(rec)

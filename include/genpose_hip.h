@@ -110,6 +110,12 @@ int gp_encoder_fps(const float *pts, int b, int n, void *workspace, size_t works
 int gp_sa_level(const float *wbuf, const int64_t *layer_off, int level, int c_prev, const float *pts,
                 int b, int n, const float *feat_prev, void *workspace, size_t workspace_bytes,
                 float *out, hipStream_t stream);
+/* gp_sa_level over geometry that gp_encoder_geometry left in `geometry` (a workspace of the same (b, n) layout,
+ * possibly `workspace` itself): no ball query; the level's scratch goes to `workspace`. The ScoreNet and
+ * EnergyNet fused encoders of one batch share one geometry pass this way. Same bits as gp_sa_level. */
+int gp_sa_level_geom(const float *wbuf, const int64_t *layer_off, int level, int c_prev, const float *pts,
+                     int b, int n, const float *feat_prev, const void *geometry, void *workspace,
+                     size_t workspace_bytes, float *out, hipStream_t stream);
 
 /* ===================================================================== fused-encoder blocks
  * The DINO-pointwise encoder Pointnet2ClsMSGFus (pointnet2.py:255-388) between SA levels:

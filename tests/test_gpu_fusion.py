@@ -266,6 +266,43 @@ def test_sa_level_api_equals_encoder_forward():
     assert torch.equal(feat.reshape(5, -1), ref)
 
 
+def test_fus_encoder_shared_geometry_bit_exact(fus_sd):
+    """Two fused encoders (different weights) of the same points over ONE geometry pass -- the first model's
+    geometry() (gp_encoder_geometry), both through gp_sa_level_geom, the second on another stream -- equal each
+    model's self-contained forward (gp_encoder_fps + gp_sa_level, its own ball queries) bit for bit, every level;
+    geometry of other points or of a model that encoded again is refused."""
+    from genpose2_amd import synthetic, weights
+    from genpose2_amd.fus_encoder import FusEncoderModel
+    a = FusEncoderModel(fus_sd, torch.device(DEV))
+    b = FusEncoderModel(weights.synthetic_state_dict("energy_pointwise", seed=1), torch.device(DEV))
+    pts_np, _ = synthetic.make_batch(82, 6, 1024, n_unique_every=3)
+    p = torch.from_numpy(pts_np).to(DEV)
+    rgb = torch.randn(6, 1024, 384, device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    ref = {}
+    for name, m in (("a", a), ("b", b)):
+        out, lv = m.forward(p, rgb, return_levels=True)
+        ref[name] = (out.clone(), [{k: v.clone() for k, v in d.items()} for d in lv])
+    side = torch.cuda.Stream(device=DEV)
+    for _ in range(2):
+        g = a.geometry(p)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            got_b = b.forward(p, rgb, return_levels=True, geometry=g)
+        got_a = a.forward(p, rgb, return_levels=True, geometry=g)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        for name, got in (("a", got_a), ("b", got_b)):
+            assert torch.equal(got[0], ref[name][0]), name
+            for lv, (d0, d1) in enumerate(zip(ref[name][1], got[1])):
+                for k in d0:
+                    assert torch.equal(d0[k], d1[k]), (name, lv, k)
+    with pytest.raises(ValueError):
+        b.forward(p.clone(), rgb, geometry=g)   # other points
+    a.forward(p, rgb)                           # the producer encodes again: its geometry is rewritten
+    with pytest.raises(ValueError, match="stale"):
+        b.forward(p, rgb, geometry=g)
+
+
 # ---------------------------------------------------------------- whole encoder vs the reference
 def test_fus_encoder_vs_reference_golden(fus_model):
     import make_golden_fus as mf
