@@ -31,6 +31,18 @@ out = {"kernel": name, "rows": rows,
        "algorithmic_bytes_per_launch": rows * 72,
        "note": "fabric reads are dominated by each XCD's L2 re-fetching the streamed head weights (1.57 MB of f16x3 planes) once "
                "per launch (the kernel boundary invalidates L2); served from the 256 MB Infinity Cache"}
+if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+    # summed over every SIMD of the chip; the launch occupies ceil(rows / tile) CUs (one workgroup each)
+    tile = 64 if rows > 8192 else (32 if rows > 4096 else 16)
+    simds = 4 * min(256, -(-rows // tile))
+    out["mfma_busy_cycles_per_active_simd"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / simds
+    out["grbm_gui_active_per_xcd"] = m.get("GRBM_GUI_ACTIVE", 0) / 8
+    out["pmc_note"] = ("counters under --pmc stretch the launch (GRBM_GUI_ACTIVE per XCD is the profiled duration); "
+                       "divide the MFMA busy cycles by the un-profiled workgroup lifetime (scripts/pc_trace.py) for "
+                       "the MFMA utilisation")
+if "SQ_INSTS_VALU" in m:
+    out["valu_insts"] = m["SQ_INSTS_VALU"]
+    out["lds_bank_conflict_cycles"] = m.get("SQ_LDS_BANK_CONFLICT")
 if "TCC_HIT_sum" in m:
     out["tcc_hit_rate"] = m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
 if "TCP_TCC_READ_REQ_sum" in m:
