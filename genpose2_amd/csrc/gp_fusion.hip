@@ -257,6 +257,9 @@ constexpr int SL_THREADS = 512;
 #ifndef SL_DMA
 #define SL_DMA 1   // A planes global -> LDS by global_load_lds_dwordx4 (0: through registers and ds_write)
 #endif
+#ifndef SL_DIAG
+#define SL_DIAG 0     // timing diagnostics of linear_split_kernel's chunk loop (wrong results): see the loop
+#endif
 // 16 bytes per lane from global memory straight into LDS at lds + 16 * lane (lds wave-uniform)
 __device__ __forceinline__ void lds_dma16(const void* src, void* lds) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
@@ -385,7 +388,27 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
     __syncthreads();
     for (int c = 0; c < KC; ++c) {
         const int s = c & 1;
+#if SL_DIAG
+        // timing diagnostic (wrong results): bit 1 no x loads / split / B stores after chunk 0, bit 2 no weight
+        // copies after chunk 0, bit 4 no barrier wait on memory (the loop's vmcnt(0) dropped)
+        if (c + 1 < KC) {
+            if constexpr ((SL_DIAG & 2) == 0)
+#pragma unroll
+                for (int u = 0; u < WO; ++u) {
+                    const int idx = tid + SL_THREADS * u;
+                    lds_dma16(W + ((size_t)(T0 + (idx >> 7)) * KC + c + 1) * 128 + (idx & 127), sA(s ^ 1) + (idx & ~63));
+                }
+            if constexpr ((SL_DIAG & 1) == 0)
+#pragma unroll
+                for (int u = 0; u < RU; ++u) {
+                    const float* xr = a.x + (size_t)row[u] * a.ldx + 32 * (c + 1) + 4 * bq[u];
+                    rb[2 * u] = row[u] < a.m ? ld4(xr) : f32x4{0.f, 0.f, 0.f, 0.f};
+                    rb[2 * u + 1] = row[u] < a.m ? ld4(xr + 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+        }
+#else
         if (c + 1 < KC) load(c + 1, s ^ 1, ra, rb);
+#endif
         if constexpr (JT == 4) {
             f16x8 bh[JT], bl[JT];
 #pragma unroll
@@ -435,9 +458,15 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
                     for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma_h(ah[i], bh[j], acc[i][j0 + j]);
             }
         }
+#if SL_DIAG
+        if ((SL_DIAG & 1) == 0 && c + 1 < KC) store(s ^ 1, ra, rb);
+        if constexpr ((SL_DIAG & 4) == 0) wait_all_mem();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
         if (c + 1 < KC) store(s ^ 1, ra, rb);
         if constexpr (SL_DMA) wait_all_mem();
         __syncthreads();
+#endif
     }
     // epilogue: unscale (exact powers of two), bias, activation; the accumulator of tile (i, j) holds outputs
     // 4q..4q+3 of output tile T0 + 4 wo + i for token (JT wt + j) * 16 + nn
