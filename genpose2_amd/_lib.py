@@ -90,6 +90,10 @@ _SIGS: Dict[str, tuple] = {
     "gp_pc_sample": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                              c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_float, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_size_t, c_void_p]),
+    "gp_pc_global_partials": (c_int, [c_int, c_int, c_int, c_int]),
+    "gp_pc_sample_global": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                                    c_int, c_void_p, c_uint64, c_float, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                    c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "gp_pose_epilogue_f64": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "gp_ode_workspace_size": (c_size_t, [c_int]),
     "gp_ode_rhs": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_float, c_float, c_double, c_void_p, c_void_p,
@@ -133,6 +137,10 @@ _SIGS: Dict[str, tuple] = {
 
 EXPORTED = tuple(_SIGS)
 _lib = None
+
+
+# gp_pc_exchange_fn (genpose_hip.h): int (*)(void* ctx, int step, float* slot, int n, hipStream_t stream)
+PC_EXCHANGE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, c_void_p, c_int, c_void_p)
 
 
 def load(path: str = LIB_PATH):

@@ -52,6 +52,8 @@ class PoseNet:
         self.ode_host_control = False              # ODE: True runs the RK45 controller on the host
         self.ode_trace: Optional[list] = None      # ODE: a list receives [t, h, error norm] per step attempt
                                                    # (host controller)
+        self.global_batch = None                   # shard.GlobalBatch: this call is one shard of a global-batch
+                                                   # PC call (runner.ShardedEvaluationPipeline(global_batch=True))
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(self.cfg.noise_seed)
         self.weights_source = f"synthetic(seed={self.cfg.seed})"
@@ -217,7 +219,12 @@ class PoseNet:
         if mode == "pc":
             T = int(self.cfg.sampling_steps)
             tab, tproj = self._pc_table(T)
-            if rep_init is None:   # prior((R,9)) at T=1 (sde.py:30-34); init_x used as-is (samplers.py:128)
+            gb = self.global_batch
+            if rep_init is None and gb is not None:   # this shard's rows of the whole batch's prior draw
+                if self.noise_feed is not None:
+                    raise ValueError("global-batch sampling draws the prior itself (noise_feed not supported)")
+                x = (self._draw_prior(gb.total * K)[gb.lo * K:gb.hi * K] * sde.prior_sigma(arch.SDE_T)).contiguous()
+            elif rep_init is None:   # prior((R,9)) at T=1 (sde.py:30-34); init_x used as-is (samplers.py:128)
                 x = (self._draw_prior(R) * sde.prior_sigma(arch.SDE_T)).contiguous()
             else:
                 x = rep_init.to(torch.float32).contiguous().clone()
@@ -227,11 +234,15 @@ class PoseNet:
                 z2 = self.noise_feed.z2.to(self.device, torch.float32).contiguous()
             seed = (self.cfg.noise_seed * 1000003 + self._calls) & 0xFFFFFFFFFFFF
             want_xs = bool(return_process or self.cfg.save_video)
-            res, q, xs = self.heads.pc_sample(pobj, tproj, tab, x, K, center, z1, z2, seed=seed, want_xs=want_xs)
+            res, q, xs = self.heads.pc_sample(pobj, tproj, tab, x, K, center, z1, z2, seed=seed, want_xs=want_xs,
+                                              global_batch=gb)
             pred_pose = res.view(bs, K, -1)
             pred_q = q.view(bs, K, -1)
             in_process = xs.view(bs, K, T, -1) if xs is not None else None
         elif mode == "ode":
+            if self.global_batch is not None:
+                raise NotImplementedError("global-batch sampling is built for the PC sampler; the ODE sampler runs "
+                                          "per shard")
             pred_pose, pred_q, in_process = self._ode(pobj, center, bs, K, rep_init, T0,
                                                       bool(return_process or self.cfg.save_video))
         else:

@@ -178,7 +178,12 @@ struct PCArgs {
     const float* tproj;   // (T, 768)
     float* x;             // (R, 9) state
     float* s;             // (R, 9) score of the previous step
-    float* part;          // (2, nwg) per-workgroup sums of row score norms
+    float* part;          // (2, part_n) per-workgroup sums of row score norms; this call's workgroups write
+                          // entries [part_off, part_off + nwg) of a slot
+    int part_n, part_off; // entries summed for grad_norm (nwg / 0 for a call on its own rows; every shard's
+                          // workgroups in shard order for a global-batch call, gp_pc_sample_global)
+    int norm_rows;        // rows grad_norm averages over (rows, or the global batch's)
+    int row_off;          // global index of row 0 (the Philox draws' row counter)
     float* zbuf;          // (2 slots, 2 streams, R, 9) Philox draws: launch i writes step i's into slot
                           // i&1 while its wave 0 reads step i-1's from the other slot (no ordering
                           // between the waves of a workgroup is needed)
@@ -220,7 +225,7 @@ __device__ __forceinline__ void pc_update_rows(const PCArgs& a, int i, const PCS
     const int r = r0 + c;
     const bool upd = i > 0 && r < a.rows && p < 3;
     if (upd) {
-        const float gn = udiv(gacc, (float)a.rows);
+        const float gn = udiv(gacc, (float)a.norm_rows);
         const float ratio = udiv(a.ls_coef, gn);
         const float ls = 2.0f * (ratio * ratio);
         const float sq2ls = usqrt(2.0f * ls);
@@ -318,7 +323,7 @@ __device__ __forceinline__ void pc_make_draws(const PCArgs& a, int i, int r0, Ds
         const int c = e / 6, st = (e - c * 6) / 3, blk = e - c * 6 - st * 3;
         const int r = r0 + c;
         if (r < a.rows) {
-            const f32x4 v = philox_normal4(a.seed, (uint32_t)(st + 2 * i), (uint32_t)r, (uint32_t)blk);
+            const f32x4 v = philox_normal4(a.seed, (uint32_t)(st + 2 * i), (uint32_t)(a.row_off + r), (uint32_t)blk);
             dst(st, c, blk * 4 + 0, v.x);
             if (blk < 2) {
                 dst(st, c, blk * 4 + 1, v.y);
@@ -386,10 +391,10 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
         const float* zslot = a.zbuf + (size_t)((i - 1) & 1) * 2 * a.rows * 9;
         const float* z1p = inj ? a.z1 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : zslot;
         const float* z2p = inj ? a.z2 + ((size_t)(i > 0 ? i - 1 : 0) * a.rows) * 9 : zslot + (size_t)a.rows * 9;
-        const float* part = a.part + (size_t)((i - 1) & 1) * a.nwg;
+        const float* part = a.part + (size_t)((i - 1) & 1) * a.part_n;
         float pv[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) pv[u] = part[min(lane + 64 * u, a.nwg - 1)];
+        for (int u = 0; u < 8; ++u) pv[u] = part[min(lane + 64 * u, a.part_n - 1)];
         const int p = lane & 3;
         const int e0 = 3 * (p < 3 ? p : 0);
         float x3[3], sv[3], z1v[3], z2v[3];
@@ -406,12 +411,12 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
         // grad_norm = mean_r ||s_r|| over all rows of step i-1 (samplers.py:143); unused at i=0
         float gacc = 0.f;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) gacc += lane + 64 * u < a.nwg ? pv[u] : 0.f;
-        for (int t0 = 512; t0 < a.nwg; t0 += 512) {
+        for (int u = 0; u < 8; ++u) gacc += lane + 64 * u < a.part_n ? pv[u] : 0.f;
+        for (int t0 = 512; t0 < a.part_n; t0 += 512) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) pv[u] = part[min(t0 + lane + 64 * u, a.nwg - 1)];
+            for (int u = 0; u < 8; ++u) pv[u] = part[min(t0 + lane + 64 * u, a.part_n - 1)];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) gacc += t0 + lane + 64 * u < a.nwg ? pv[u] : 0.f;
+            for (int u = 0; u < 8; ++u) gacc += t0 + lane + 64 * u < a.part_n ? pv[u] : 0.f;
         }
         PC_MARK(9);
         pc_update_rows<NT, WV, PL>(a, i, prev, sm, obj, g, lane, r0, gacc, x3, sv, z1v, z2v, hs, true, trace_slot);
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(WV * 64) void pc_step_kernel(PCArgs a, int i, PCSte
     PC_MARK(7);
     const float t = pc_score_norm<NT, WV, PL>(a, cur, sm, r0, wid, lane,
                                               [&](int c, int o, float v) { a.s[(size_t)(r0 + c) * 9 + o] = v; });
-    if (tid == 0) a.part[(size_t)(i & 1) * a.nwg + blockIdx.x] = t;
+    if (tid == 0) a.part[(size_t)(i & 1) * a.part_n + a.part_off + blockIdx.x] = t;
     PC_MARK(8);
 }
 
@@ -500,10 +505,13 @@ extern "C" int gp_pc_step_table(int steps, float eps, float* out) {
     return GP_OK;
 }
 
-extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const float* tproj, const float* step_tab,
-                            int steps, float* x, int rows, int k, const float* pts_center, const float* z1,
-                            const float* z2, uint64_t seed, float snr, float* res, float* q, float* xs,
-                            void* workspace, size_t workspace_bytes, hipStream_t stream) {
+// The shared body of gp_pc_sample and gp_pc_sample_global: nt column tiles per workgroup, grad_norm over
+// part_n partials of `part` averaged over norm_rows, exchange (if any) after every scoring launch.
+static int pc_sample_impl(const gp_head_weights* w, const float* pobj, const float* tproj, const float* step_tab,
+                          int steps, float* x, int rows, int k, const float* pts_center, const float* z1,
+                          const float* z2, uint64_t seed, float snr, float* res, float* q, float* xs, void* workspace,
+                          size_t workspace_bytes, int nt, float* part, int part_n, int part_off, int norm_rows,
+                          int row_off, gp_pc_exchange_fn exchange, void* ctx, hipStream_t stream) {
     GP_REQUIRE(w && pobj && tproj && step_tab && x && pts_center && res && q && workspace,
                "pc_sample: null pointer");
     GP_REQUIRE(steps >= 2 && rows >= 1 && k >= 1, "pc_sample: need steps>=2, rows>=1, k>=1");
@@ -511,7 +519,6 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     GP_REQUIRE(workspace_bytes >= gp_pc_workspace_size(rows), "pc_sample: workspace too small");
     // split-f16 GEMMs when the packed planes are given (gp_head_weights), exact fp32 otherwise
     const bool split = w->pe2_h != nullptr;
-    const int nt = head_pick_nt(rows, split);
     GP_REQUIRE(!split || (w->h1p_h && w->hsc), "pc_sample: pe2_h, h1p_h and hsc must be given together");
     PCArgs a;
     a.w = *w;
@@ -519,8 +526,7 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     a.tproj = tproj;
     a.x = x;
     a.s = static_cast<float*>(workspace);
-    a.part = a.s + (size_t)rows * 9;
-    a.zbuf = a.part + 2 * (((size_t)rows + 15) / 16);
+    a.zbuf = a.s + (size_t)rows * 9 + 2 * (((size_t)rows + 15) / 16);
     a.z1 = z1;
     a.z2 = z2;
     a.seed = seed;
@@ -532,7 +538,14 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
     a.kper = k;
     a.steps = steps;
     a.nwg = (rows + 16 * nt - 1) / (16 * nt);
+    a.part = part != nullptr ? part : a.s + (size_t)rows * 9;
+    a.part_n = part != nullptr ? part_n : a.nwg;
+    a.part_off = part != nullptr ? part_off : 0;
+    a.norm_rows = norm_rows;
+    a.row_off = row_off;
     a.ls_coef = snr * 3.0f;  // snr * sqrt(pose_dim=9) in fp32 (0.48 rounds identically)
+    GP_REQUIRE(a.part_off >= 0 && a.part_off + a.nwg <= a.part_n, "pc_sample: partials [%d, %d) outside %d entries",
+               a.part_off, a.part_off + a.nwg, a.part_n);
     const dim3 grid(a.nwg);
     for (int i = 0; i <= steps; ++i) {
         PCStep cur = {}, prev = {};
@@ -548,8 +561,48 @@ extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const f
             hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, X3P>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
         else
             hipLaunchKernelGGL((pc_step_kernel<1, PC_WV1, 0>), grid, dim3(PC_WV1 * 64), 0, stream, a, i, cur, prev);
+        if (exchange != nullptr && i < steps) {   // launch i's partials -> every shard before launch i + 1 reads them
+            const int rc = gp_check_launch("pc_step_kernel");
+            if (rc) return rc;
+            GP_REQUIRE(exchange(ctx, i, a.part + (size_t)(i & 1) * a.part_n, a.part_n, stream) == 0,
+                       "pc_sample_global: the partials exchange of step %d failed", i);
+        }
     }
     return gp_check_launch("pc_step_kernel");
+}
+
+extern "C" int gp_pc_sample(const gp_head_weights* w, const float* pobj, const float* tproj, const float* step_tab,
+                            int steps, float* x, int rows, int k, const float* pts_center, const float* z1,
+                            const float* z2, uint64_t seed, float snr, float* res, float* q, float* xs,
+                            void* workspace, size_t workspace_bytes, hipStream_t stream) {
+    GP_REQUIRE(w != nullptr, "pc_sample: null pointer");
+    return pc_sample_impl(w, pobj, tproj, step_tab, steps, x, rows, k, pts_center, z1, z2, seed, snr, res, q, xs,
+                          workspace, workspace_bytes, head_pick_nt(rows, w->pe2_h != nullptr), nullptr, 0, 0, rows, 0,
+                          nullptr, nullptr, stream);
+}
+
+extern "C" int gp_pc_global_partials(int rows_total, int shard_rows_max, int shards, int split) {
+    if (rows_total < 1 || shard_rows_max < 1 || shards < 1) return 0;
+    const int tile = 16 * head_pick_nt(rows_total, split != 0);
+    return shards * ((shard_rows_max + tile - 1) / tile);
+}
+
+extern "C" int gp_pc_sample_global(const gp_head_weights* w, const float* pobj, const float* tproj,
+                                   const float* step_tab, int steps, float* x, int rows, int k,
+                                   const float* pts_center, uint64_t seed, float snr, float* res, float* q, float* xs,
+                                   int rows_total, int row_off, int shard, int shards, int shard_rows_max,
+                                   float* part, gp_pc_exchange_fn exchange, void* ctx, void* workspace,
+                                   size_t workspace_bytes, hipStream_t stream) {
+    GP_REQUIRE(w && part && exchange, "pc_sample_global: null pointer");
+    GP_REQUIRE(shards >= 1 && shard >= 0 && shard < shards && rows >= 1 && rows <= shard_rows_max &&
+                   row_off >= 0 && row_off + rows <= rows_total,
+               "pc_sample_global: shard %d of %d, rows [%d, %d) of %d (at most %d per shard)", shard, shards, row_off,
+               row_off + rows, rows_total, shard_rows_max);
+    const int nt = head_pick_nt(rows_total, w->pe2_h != nullptr);   // the tiling of one call on the whole batch
+    const int per = (shard_rows_max + 16 * nt - 1) / (16 * nt);
+    return pc_sample_impl(w, pobj, tproj, step_tab, steps, x, rows, k, pts_center, nullptr, nullptr, seed, snr, res, q,
+                          xs, workspace, workspace_bytes, nt, part, shards * per, shard * per, rows_total, row_off,
+                          exchange, ctx, stream);
 }
 
 // ============================================================================ ODE epilogue (fp64)

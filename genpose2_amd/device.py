@@ -269,7 +269,9 @@ class HeadModel:
         return out
 
     def pc_sample(self, pobj, tproj, step_tab: np.ndarray, x: torch.Tensor, k: int, pts_center: torch.Tensor,
-                  z1=None, z2=None, seed: int = 0, snr: float = arch.SNR, want_xs: bool = False):
+                  z1=None, z2=None, seed: int = 0, snr: float = arch.SNR, want_xs: bool = False, global_batch=None):
+        """gp_pc_sample; with ``global_batch`` (shard.GlobalBatch) gp_pc_sample_global: this rank's rows of one
+        call on the whole batch (grad_norm over every shard's rows, one partials all-gather per step)."""
         R = x.shape[0]
         T = step_tab.shape[0]
         need = int(self.lib.gp_pc_workspace_size(R))
@@ -279,6 +281,28 @@ class HeadModel:
         q = torch.empty((R, 7), dtype=torch.float32, device=self.device)
         xs = torch.empty((R, T, 9), dtype=torch.float32, device=self.device) if want_xs else None
         tab = np.ascontiguousarray(step_tab, np.float32)
+        if global_batch is not None:
+            from .shard import PartialsExchange
+            gb = global_batch
+            if z1 is not None or z2 is not None:
+                raise ValueError("global-batch sampling draws its noise on the device (z1 / z2 not supported)")
+            rows_total, rows_max = gb.total * k, gb.per_max * k
+            if R != (gb.hi - gb.lo) * k:
+                raise ValueError(f"global-batch shard: {R} rows for objects [{gb.lo}, {gb.hi}) x {k}")
+            n = int(self.lib.gp_pc_global_partials(rows_total, rows_max, gb.world, int(self.w.pe2_h is not None)))
+            part = torch.zeros(2 * n, dtype=torch.float32, device=self.device)
+            ex = PartialsExchange(part, n, gb)
+            rc = self.lib.gp_pc_sample_global(
+                ctypes.byref(self.w), ctypes.c_void_p(pobj.data_ptr()), ctypes.c_void_p(tproj.data_ptr()),
+                tab.ctypes.data_as(ctypes.c_void_p), T, ctypes.c_void_p(x.data_ptr()), R, k,
+                ctypes.c_void_p(pts_center.data_ptr()), ctypes.c_uint64(seed), ctypes.c_float(snr),
+                ctypes.c_void_p(res.data_ptr()), ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(_ptr(xs)),
+                rows_total, gb.lo * k, gb.rank, gb.world, rows_max, ctypes.c_void_p(part.data_ptr()), ex.fn, None,
+                ctypes.c_void_p(self._pc_ws.data_ptr()), self._pc_ws.numel(), self._s())
+            if ex.error is not None:
+                raise RuntimeError("pc_sample_global: partials exchange failed") from ex.error
+            check(rc, "pc_sample_global")
+            return res, q, xs
         check(self.lib.gp_pc_sample(
             ctypes.byref(self.w), ctypes.c_void_p(pobj.data_ptr()), ctypes.c_void_p(tproj.data_ptr()),
             tab.ctypes.data_as(ctypes.c_void_p), T, ctypes.c_void_p(x.data_ptr()), R, k,

@@ -107,11 +107,15 @@ class ShardedEvaluationPipeline:
     batch on every rank, processes the rank's contiguous object block (shard.shard_range) with no
     collective on the sampling path -- each shard is a reference call on its sub-batch -- and gathers
     pred_pose, pts_feat, energy, aggregated and length back in object order on every rank (dst=None)
-    or on ``dst`` only."""
+    or on ``dst`` only. ``global_batch=True`` (PC sampler) makes the shards one reference call on the
+    whole batch instead: the Langevin grad_norm over every shard's rows (one all-gather of the score-norm
+    partials per step, shard.GlobalBatch) and the prior and device noise drawn for the whole batch."""
 
-    def __init__(self, cfg: GenPoseConfig, with_energy: bool = True, with_scale: bool = False, src: int = 0):
+    def __init__(self, cfg: GenPoseConfig, with_energy: bool = True, with_scale: bool = False, src: int = 0,
+                 global_batch: bool = False):
         self.local = EvaluationPipeline(cfg, with_energy, with_scale)
         self.src = src
+        self.global_batch = global_batch
         self.sync_weights()
 
     def agents(self):
@@ -148,10 +152,15 @@ class ShardedEvaluationPipeline:
         total = int(batch["pts"].shape[0])
         lo, hi = shard.shard_range(total, dist.get_world_size(), dist.get_rank())
         K = self.local.cfg.eval_repeat_num
+        if self.global_batch:
+            self.local.score_agent.global_batch = shard.GlobalBatch.of(total)   # raises on an empty shard
         if hi > lo:
             # per-object tensors, and lists of them (the DINOv3 layers of --dino pointwise)
-            out = self.local.run({k: [t[lo:hi] for t in v] if isinstance(v, (list, tuple)) else v[lo:hi]
-                                  for k, v in batch.items()})
+            try:
+                out = self.local.run({k: [t[lo:hi] for t in v] if isinstance(v, (list, tuple)) else v[lo:hi]
+                                      for k, v in batch.items()})
+            finally:
+                self.local.score_agent.global_batch = None
         else:   # more ranks than objects: an empty shard still joins the gathers
             d = batch["pts"].device
             z = lambda *s: torch.zeros(s, dtype=torch.float32, device=d)  # noqa: E731

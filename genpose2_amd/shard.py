@@ -9,10 +9,15 @@ exchanges are:
 * once: the packed weights of every agent, broadcast from rank 0 (RCCL over xGMI; gloo on CPU);
 * per evaluated batch: the per-object outputs (pred_pose, energy, aggregated 4x4, lengths;
   about 4.5 MB at config 4) gathered to rank 0 or to every rank -- one all_gather per output
-  tensor, off the timed sampling loop.
+  tensor, off the timed sampling loop;
+* optional global-batch PC sampling (``GlobalBatch``): the shards together reproduce ONE
+  reference call on the whole batch -- the Langevin grad_norm averages every shard's rows -- at the
+  cost of one all-gather of the per-workgroup score-norm partials per step (a few hundred bytes,
+  latency-bound).
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
 from typing import Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
@@ -24,6 +29,64 @@ def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
     per = -(-total // world)
     lo = min(total, rank * per)
     return lo, min(total, lo + per)
+
+
+@dataclass
+class GlobalBatch:
+    """This rank's block of one global-batch call: objects [lo, hi) of ``total`` (shard_range), at most
+    ``per_max`` objects per shard, over the ranks of ``group`` (None: the default group)."""
+    total: int
+    lo: int
+    hi: int
+    per_max: int
+    rank: int
+    world: int
+    group: object = None
+
+    @staticmethod
+    def of(total: int, group=None) -> "GlobalBatch":
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        lo, hi = shard_range(total, world, rank)
+        if hi <= lo:
+            raise ValueError(f"global-batch sampling needs every shard non-empty ({total} objects over {world} ranks)")
+        return GlobalBatch(total, lo, hi, -(-total // world), rank, world, group)
+
+
+class PartialsExchange:
+    """gp_pc_sample_global's exchange callback over ``part`` (2 slots of ``n`` floats, ``n / world`` per
+    shard): after each scoring launch, every shard's chunk of the slot the launch wrote reaches every rank
+    before the next launch reads it. RCCL: an all-gather enqueued behind the launch on the current stream
+    (torch orders the next launch after it). gloo: through host copies (tests)."""
+
+    def __init__(self, part: torch.Tensor, n: int, gb: GlobalBatch):
+        import torch.distributed as dist
+        from . import _lib
+        self.part, self.n, self.gb = part, n, gb
+        self.per = n // gb.world
+        self.nccl = dist.get_backend(gb.group) == "nccl"
+        self.chunk = torch.empty(self.per, dtype=torch.float32, device=part.device)
+        self.error: Optional[BaseException] = None
+        self.fn = _lib.PC_EXCHANGE_FN(self._call)   # kept alive with the object
+
+    def _call(self, ctx, step, slot_ptr, n, stream) -> int:
+        import torch.distributed as dist
+        try:
+            base = (step & 1) * self.n
+            slot = self.part[base:base + self.n]
+            assert n == self.n and slot_ptr == slot.data_ptr(), "exchange: unexpected partials slot"
+            mine = slot[self.gb.rank * self.per:(self.gb.rank + 1) * self.per]
+            if self.nccl:
+                self.chunk.copy_(mine)
+                dist.all_gather_into_tensor(slot, self.chunk, group=self.gb.group)
+            else:
+                got = [torch.empty(self.per, dtype=torch.float32) for _ in range(self.gb.world)]
+                dist.all_gather(got, mine.cpu(), group=self.gb.group)
+                slot.copy_(torch.cat(got).to(slot.device))
+            return 0
+        except BaseException as e:   # noqa: BLE001 -- reported through the C return code, re-raised by the caller
+            self.error = e
+            return -1
 
 
 def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0) -> None:

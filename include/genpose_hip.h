@@ -250,6 +250,27 @@ int gp_pc_sample(const gp_head_weights *w, const float *pobj, const float *tproj
                  float snr, float *res, float *q, float *xs, void *workspace,
                  size_t workspace_bytes, hipStream_t stream);
 
+/* Global-batch PC sampling over shards (SURVEY 8e's optional mode; replaces nothing in the reference,
+ * whose single cond_pc_sampler call (samplers.py:113-177) couples every row of the batch through the
+ * Langevin grad_norm mean at :143-144). Each shard samples its contiguous block of rows
+ * [row_off, row_off + rows) of a batch of rows_total rows with the tiling one call on rows_total rows
+ * would use: its workgroups' partial sums of ||s_r|| go to entries [shard * per, shard * per + nwg) of
+ * `part` (2 x gp_pc_global_partials(...) floats, zero-filled by the caller, per = that count / shards),
+ * and after every scoring launch `exchange(ctx, step, slot, n, stream)` must make the slot's n entries
+ * hold every shard's partials (an all-gather of `per`-entry chunks, enqueued on `stream`) before the
+ * next launch reads them; grad_norm is their sum (in the fixed order) over rows_total, and the Philox
+ * draws are keyed by the global row. With every shard but the last holding shard_rows_max rows, a
+ * multiple of the tile (gp_pc_tile_rows(rows_total)), the result equals one gp_pc_sample call on the
+ * whole batch bit for bit. exchange returns 0 on success. */
+typedef int (*gp_pc_exchange_fn)(void *ctx, int step, float *slot, int n, hipStream_t stream);
+int gp_pc_global_partials(int rows_total, int shard_rows_max, int shards, int split);
+int gp_pc_sample_global(const gp_head_weights *w, const float *pobj, const float *tproj,
+                        const float *step_tab, int steps, float *x, int rows, int k,
+                        const float *pts_center, uint64_t seed, float snr, float *res, float *q,
+                        float *xs, int rows_total, int row_off, int shard, int shards,
+                        int shard_rows_max, float *part, gp_pc_exchange_fn exchange, void *ctx,
+                        void *workspace, size_t workspace_bytes, hipStream_t stream);
+
 /* The step table of cond_pc_sampler (samplers.py:129-130, sde.py:15-27) for hosts without Python:
  * out (HOST, steps x 5 fp32) = {t, sigma(t), g(t), dt, sqrt(dt)} with t = torch.linspace(1, eps,
  * steps) in float32 (bit-identical to torch's CPU rounding), sigma = f32(0.01) * 5000^t (power

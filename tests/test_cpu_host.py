@@ -743,3 +743,48 @@ def test_no_permlane_swap_in_mfma_hazard_window():
                 regs = _vregs(args[0])   # vdst
                 recent.append((0, regs))
     assert checked > 50, checked   # the trunks' row reductions were found
+
+
+def _exchange_worker(rank, world, port, out_dir, per):
+    import torch.distributed as dist
+    from genpose2_amd import shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        gb = shard.GlobalBatch.of(world * 3)
+        assert (gb.lo, gb.hi, gb.per_max, gb.rank, gb.world) == (3 * rank, 3 * rank + 3, 3, rank, world)
+        n = per * world
+        part = torch.full((2 * n,), -1.0)
+        ex = shard.PartialsExchange(part, n, gb)
+        for step in range(3):   # the sampler fills this rank's chunk of slot step & 1, then calls the exchange
+            base = (step & 1) * n
+            part[base + rank * per:base + (rank + 1) * per] = torch.arange(per, dtype=torch.float32) + 100 * rank + step
+            assert ex._call(None, step, part[base:].data_ptr(), n, None) == 0, ex.error
+            want = torch.cat([torch.arange(per, dtype=torch.float32) + 100 * r + step for r in range(world)])
+            assert torch.equal(part[base:base + n], want)
+        assert ex._call(None, 0, part.data_ptr() + 4, n, None) == -1 and ex.error is not None   # wrong slot
+        np.save(os.path.join(out_dir, f"ok_{rank}.npy"), np.array(True))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_global_batch_partials_exchange_gloo(tmp_path, world):
+    """Global-batch PC sampling's host side (shard.GlobalBatch, shard.PartialsExchange) over gloo: every
+    rank's chunk of the slot a scoring launch wrote reaches every rank in shard order, and an unexpected
+    slot pointer is reported as a failure (the C caller turns it into an error) instead of raising into C."""
+    import torch.multiprocessing as mp
+    port = 29700 + (os.getpid() + world) % 1000
+    mp.spawn(_exchange_worker, args=(world, port, str(tmp_path), 5), nprocs=world, join=True)
+    assert all(np.load(tmp_path / f"ok_{r}.npy") for r in range(world))
+
+
+def test_global_batch_rejects_empty_shards():
+    from genpose2_amd import shard
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{29690 + os.getpid() % 300}", rank=0, world_size=1)
+    try:
+        assert shard.GlobalBatch.of(4).per_max == 4
+        with pytest.raises(ValueError):
+            shard.GlobalBatch.of(0)
+    finally:
+        dist.destroy_process_group()

@@ -71,3 +71,46 @@ def test_two_ranks_mismatched_seeds_equal_rank0_weights(tmp_path, with_ckpt):
     for k in ("pred_pose", "pts_feat", "energy", "aggregated", "length"):
         want = torch.cat([getattr(p, k) for p in parts]).cpu().numpy()
         np.testing.assert_array_equal(np.load(tmp_path / f"{k}.npy"), want, err_msg=k)
+
+
+def _cfg_global(k):
+    from genpose2_amd.config import GenPoseConfig
+    return GenPoseConfig(device=DEV, sampling_steps=20, eval_repeat_num=k, noise_seed=4, seed=0)
+
+
+def _global_worker(rank, world, port, out_dir, total, k):
+    import torch.distributed as dist
+    from genpose2_amd.runner import ShardedEvaluationPipeline
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        pipe = ShardedEvaluationPipeline(_cfg_global(k), global_batch=True)
+        got = pipe.run(_batch(total))
+        # negative control: the default semantics (each shard a reference call on its sub-batch)
+        own = ShardedEvaluationPipeline(_cfg_global(k), with_energy=False).run(_batch(total))
+        if rank == 0:
+            for key in ("pred_pose", "energy", "aggregated"):
+                np.save(os.path.join(out_dir, f"{key}.npy"), getattr(got, key).cpu().numpy())
+            np.save(os.path.join(out_dir, "per_shard_pred_pose.npy"), own.pred_pose.cpu().numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total,k", [(6, 16), (5, 16), (132, 64)])
+def test_global_batch_two_ranks_equal_one_call(tmp_path, total, k):
+    """Global-batch PC sampling (ShardedEvaluationPipeline(global_batch=True), gp_pc_sample_global): two ranks
+    sharing cuda:0 over gloo, each sampling its block of objects with the Langevin grad_norm averaged over
+    BOTH shards' rows (one partials all-gather per step), the prior and the device noise drawn for the whole
+    batch, give bit for bit what ONE EvaluationPipeline call on the whole batch gives -- the reference's
+    single cond_pc_sampler call (samplers.py:143-144). Shards of whole tiles (16-row tiles; 64-row tiles at
+    132 x 64 rows) and a short last shard (5 objects: 3 + 2)."""
+    import torch.multiprocessing as mp
+    from genpose2_amd.runner import EvaluationPipeline
+    world = 2
+    port = 29400 + (os.getpid() + total) % 500
+    mp.spawn(_global_worker, args=(world, port, str(tmp_path), total, k), nprocs=world, join=True)
+    ref = EvaluationPipeline(_cfg_global(k)).run(_batch(total))
+    for key in ("pred_pose", "energy", "aggregated"):
+        np.testing.assert_array_equal(np.load(tmp_path / f"{key}.npy"), getattr(ref, key).cpu().numpy(), err_msg=key)
+    assert not np.array_equal(np.load(tmp_path / "per_shard_pred_pose.npy"), ref.pred_pose.cpu().numpy())
