@@ -227,7 +227,9 @@ def cpu_baseline(cfg, config_id, threads, sample_objects, reps=3):
             c = json.load(f)
         out["calibration_note"] = {"oracle_over_reference_time": round(c["oracle_over_reference"], 3),
                                    "threads": c["threads"], "source": os.path.relpath(cal, REPO),
-                                   "applied": False}
+                                   "applied": False,
+                                   # the reference's own CPU rate this ratio implies (value is not changed by it)
+                                   "reference_equivalent_value": out["value"] * c["oracle_over_reference"]}
         break
     return out
 
@@ -363,21 +365,28 @@ def time_ode_calls(args, cfg, data0, B, K, ws, dev):
            "ms_per_call": per * 1e3, "poses_per_s": B * K * ws / per, "calls": args.ode_calls,
            "workload": f"B={B} objects/GPU, K={K}: encoder + RK45 (rtol=atol=1e-5) + denoise per call"}
     if stage_ms and rows == {B * K}:
-        # the dominant kernel: ode_stage_kernel, six launches per attempted step (five stage derivatives, then the
-        # last stage with y_new and the error partials), each one score evaluation of every row
-        us = float(np.sum(stage_ms)) * 1e3 / (6 * len(stage_ms))
+        # the dominant kernel: one ode_attempt_kernel per attempted step (the six stage evaluations of every row back
+        # to back; GENPOSE2_ODE_FUSED=0: six ode_stage_kernel launches, five stage derivatives then the last stage
+        # with y_new and the error partials). The events bracket each attempt's launch(es).
+        att_us = float(np.sum(stage_ms)) * 1e3 / len(stage_ms)
         fl = B * K * arch.score_flops_per_candidate_step()
         fast = agent.heads.arith == "f16x3"
         peak = F16_PEAK_TFLOPS / 6 if fast else FP32_PEAK_TFLOPS
         tile = int(_tile_rows(B * K, fast))
-        kname = f"void ode_stage_kernel<0, {3 if fast else 0}, {tile // 16}>"
-        out["roofline"] = {"bound": "mfma", "achieved": fl / us / 1e6, "peak": peak, "unit": "TFLOP/s",
-                           "frac": fl / us / 1e6 / peak, "kernel": kname.replace("<0,", "<MODE,"),
-                           "flop_per_launch": fl, "avg_launch_us": us, "attempts_timed": len(stage_ms),
+        fused = os.environ.get("GENPOSE2_ODE_FUSED", "1")[:1] != "0"
+        if fused:
+            kname, flop_launch, us = f"void ode_attempt_kernel<{3 if fast else 0}, {tile // 16}>", 6 * fl, att_us
+            label = kname
+        else:
+            kname, flop_launch, us = f"void ode_stage_kernel<0, {3 if fast else 0}, {tile // 16}>", fl, att_us / 6
+            label = kname.replace("<0,", "<MODE,")
+        out["roofline"] = {"bound": "mfma", "achieved": flop_launch / us / 1e6, "peak": peak, "unit": "TFLOP/s",
+                           "frac": flop_launch / us / 1e6 / peak, "kernel": label, "flop_per_launch": flop_launch,
+                           "avg_launch_us": us, "us_per_stage_evaluation": att_us / 6, "attempts_timed": len(stage_ms),
                            "stage_ms_per_call": float(np.sum(stage_ms)) / args.ode_calls}
         rp = load_rocprof(kname, args.config)
         if rp is not None:
-            rp["achieved"] = fl / (rp["avg_launch_us"] * 1e-6) / 1e12
+            rp["achieved"] = flop_launch / (rp["avg_launch_us"] * 1e-6) / 1e12
             rp["frac"] = rp["achieved"] / peak
             out["roofline"]["rocprof"] = rp
     return out

@@ -2,14 +2,17 @@
 //
 // Reference: cond_ode_sampler (networks/gf_algorithms/samplers.py:180-258) hands the float64 state
 // to scipy solve_ivp(method="RK45") and pays a device->host and host->device copy per right-hand
-// side. Here every RK45 stage is one launch: the stage combination y + (sum_j a_j K_j) * h (fp64,
+// side. Here an RK45 stage is a fused kernel body: the stage combination y + (sum_j a_j K_j) * h (fp64,
 // scipy rk.py rk_step order) is formed in the prologue, cast to the fp32 pose the score model sees
 // (samplers.py:210), the head trunk evaluates the score, and the epilogue writes
 // K_s = -(0.5 g(t)^2) * score in fp64 (samplers.py:216). The last stage of an attempted step also
 // writes y_new and the per-workgroup sum of (err / scale)^2 of scipy's error estimator
 // (_estimate_error_norm, rk.py); ode_norm_kernel reduces it in a fixed order. The step
-// controller's scalars stay on the host (genpose2_amd/ode.py): one 8-byte read per attempt.
+// controller's scalars stay on the host (genpose2_amd/ode.py): one 8-byte read per attempt. The
+// device-controlled attempts (gp_ode_auto_attempt) run all six stages of an attempt in one launch
+// (ode_attempt_kernel); the host-controlled ones launch each stage (ode_stage_kernel).
 #include <cstddef>
+#include <cstdlib>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -62,43 +65,19 @@ struct OdeStageArgs {
     int stage;                   // 1..6
 };
 
-// MODE 0: stage derivative. MODE 1: last stage of an attempt (y_new, K_6, error partials).
-// NT column tiles of 16 candidates per workgroup (head_pick_nt: 32 / 64 candidates from 4097 / 8193 rows
-// with the split-f16 trunk, as the PC step).
-template <int MODE, int PL, int NT>   // PL 0: exact fp32 GEMMs, X3P: f16x3
-__global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a) {
+// One RK45 stage for the workgroup's rows. MODE 0: stage derivative. MODE 1: last stage of an attempt
+// (y_new, K_6, error partials). y_in = y + (sum_{j<nk} acoef_j K_j) h, K_out = coef * score(f32(y_in), t).
+template <int MODE, int PL, int NT>
+__device__ __forceinline__ void ode_stage_body(const OdeStageArgs& a, const double* y, const double* const* kin,
+                                               const double* acoef, int nk, double h, double coef, float sigma,
+                                               const float* tproj, double* kout, double* ynew,
+                                               HeadSmem<NT, EVAL_WV, PL>& sm, int* obj, double* y0s, double* y1s,
+                                               double* esq, const SplitScalars& hs) {
     constexpr int ROWS = 16 * NT;
     constexpr int NTH = EVAL_WV * 64;
-    __shared__ HeadSmem<NT, EVAL_WV, PL> sm;
     constexpr bool SPLIT = PL != 0;
-    __shared__ int obj[ROWS];
-    __shared__ double y0s[ROWS * 9], y1s[ROWS * 9], esq[NTH];
     const int tid = threadIdx.x;
     const int r0 = blockIdx.x * ROWS;
-    SplitScalars hs = {};
-    if constexpr (SPLIT) hs = load_split_scalars(a.w);
-    const double* y = a.y;
-    const double* kin[ODE_NK];
-#pragma unroll
-    for (int j = 0; j < ODE_NK; ++j) kin[j] = a.k[j];
-    double h = a.h, coef = a.coef;
-    float sigma = a.sigma;
-    const float* tproj = a.tproj;
-    double* kout = a.kout;
-    double* ynew = a.ynew;
-    if (a.ctl != nullptr) {   // device-controlled: skip when no attempt was prepared
-        const OdeCtl* c = a.ctl;
-        if (!c->active) return;
-        y = a.ybuf[c->yi];
-#pragma unroll
-        for (int j = 0; j < ODE_NK; ++j) kin[j] = a.kbuf[c->kidx[j]];
-        h = c->h;
-        coef = c->coef[a.stage - 1];
-        sigma = c->sig[a.stage - 1];
-        tproj = a.tproj6 + (size_t)(a.stage - 1) * 768;
-        kout = a.kbuf[c->kidx[a.stage]];
-        ynew = a.ybuf[c->yi ^ 1];
-    }
     stage_small_weights<NT, EVAL_WV, 0, !SPLIT>(a.w, sm);
     for (int i = tid; i < ROWS * 16; i += NTH) {
         const int c = i >> 4, j = i & 15;
@@ -109,9 +88,9 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
             const size_t e = (size_t)r * 9 + j;
             const double yv = y[e];
             double yi = yv;
-            if (a.nk > 0) {
-                double acc = kin[0][e] * a.a[0];
-                for (int s = 1; s < a.nk; ++s) acc = acc + kin[s][e] * a.a[s];
+            if (nk > 0) {
+                double acc = kin[0][e] * acoef[0];
+                for (int s = 1; s < nk; ++s) acc = acc + kin[s][e] * acoef[s];
                 yi = yv + acc * h;
             }
             xv = (float)yi;   // torch.tensor(x, dtype=torch.float32) (samplers.py:210)
@@ -165,6 +144,91 @@ __global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a)
             a.part[blockIdx.x] = t;
         }
     }
+}
+
+// MODE 0: stage derivative. MODE 1: last stage of an attempt (y_new, K_6, error partials).
+// NT column tiles of 16 candidates per workgroup (head_pick_nt: 32 / 64 candidates from 4097 / 8193 rows
+// with the split-f16 trunk, as the PC step).
+template <int MODE, int PL, int NT>   // PL 0: exact fp32 GEMMs, X3P: f16x3
+__global__ __launch_bounds__(EVAL_WV * 64) void ode_stage_kernel(OdeStageArgs a) {
+    constexpr int ROWS = 16 * NT;
+    constexpr int NTH = EVAL_WV * 64;
+    __shared__ HeadSmem<NT, EVAL_WV, PL> sm;
+    constexpr bool SPLIT = PL != 0;
+    __shared__ int obj[ROWS];
+    __shared__ double y0s[ROWS * 9], y1s[ROWS * 9], esq[NTH];
+    SplitScalars hs = {};
+    if constexpr (SPLIT) hs = load_split_scalars(a.w);
+    const double* y = a.y;
+    const double* kin[ODE_NK];
+#pragma unroll
+    for (int j = 0; j < ODE_NK; ++j) kin[j] = a.k[j];
+    double h = a.h, coef = a.coef;
+    float sigma = a.sigma;
+    const float* tproj = a.tproj;
+    double* kout = a.kout;
+    double* ynew = a.ynew;
+    if (a.ctl != nullptr) {   // device-controlled: skip when no attempt was prepared
+        const OdeCtl* c = a.ctl;
+        if (!c->active) return;
+        y = a.ybuf[c->yi];
+#pragma unroll
+        for (int j = 0; j < ODE_NK; ++j) kin[j] = a.kbuf[c->kidx[j]];
+        h = c->h;
+        coef = c->coef[a.stage - 1];
+        sigma = c->sig[a.stage - 1];
+        tproj = a.tproj6 + (size_t)(a.stage - 1) * 768;
+        kout = a.kbuf[c->kidx[a.stage]];
+        ynew = a.ybuf[c->yi ^ 1];
+    }
+    ode_stage_body<MODE, PL, NT>(a, y, kin, a.a, a.nk, h, coef, sigma, tproj, kout, ynew, sm, obj, y0s, y1s, esq, hs);
+}
+
+// A whole device-controlled attempt in one launch: the six stages run back to back in every workgroup
+// (a stage needs only its own rows' earlier stages, so no grid-wide step separates them -- only the
+// controller's accept / reject between attempts does). Stage s combines K_0..K_{s-1} with tableau row
+// A[s] (stage 6: B, y_new and the error partials), exactly as the six stage launches do: bit-identical,
+// without five kernel boundaries (each ~3 us of tail, boundary and refill at config 4). The K_s a stage
+// writes are read back by other threads of the workgroup after the stage's barrier (the workgroup-scope
+// release / acquire of __syncthreads orders the global stores before those loads).
+struct OdeTableau {
+    double A[36], B[6];
+};
+template <int PL, int NT>
+__global__ __launch_bounds__(EVAL_WV * 64) void ode_attempt_kernel(OdeStageArgs a, OdeTableau tb) {
+    constexpr int ROWS = 16 * NT;
+    constexpr int NTH = EVAL_WV * 64;
+    __shared__ HeadSmem<NT, EVAL_WV, PL> sm;
+    constexpr bool SPLIT = PL != 0;
+    __shared__ int obj[ROWS];
+    __shared__ double y0s[ROWS * 9], y1s[ROWS * 9], esq[NTH];
+    // the tableau and the K slots of this attempt in LDS: read per use (wave-uniform), not held in registers
+    // across the six stages
+    __shared__ double tab[42];
+    __shared__ const double* kin[ODE_NK];
+    const OdeCtl* c = a.ctl;
+    if (!c->active) return;
+    const int tid = threadIdx.x;
+    if (tid < 36) tab[tid] = tb.A[tid];
+    else if (tid < 42) tab[tid] = tb.B[tid - 36];
+    else if (tid < 42 + ODE_NK) kin[tid - 42] = a.kbuf[c->kidx[tid - 42]];
+    const double* y = a.ybuf[c->yi];
+    const double h = c->h;
+    __syncthreads();
+    for (int s = 1; s < 6; ++s) {
+        if (s > 1) __syncthreads();   // stage s-1's K stores and its reads of the staged weights are done
+        // per stage (L2-resident): held across the stages they would add to the trunk's register peak
+        SplitScalars hs = {};
+        if constexpr (SPLIT) hs = load_split_scalars(a.w);
+        ode_stage_body<0, PL, NT>(a, y, kin, tab + s * 6, s, h, c->coef[s - 1], c->sig[s - 1],
+                                  a.tproj6 + (size_t)(s - 1) * 768, const_cast<double*>(kin[s]), nullptr, sm, obj,
+                                  y0s, y1s, esq, hs);
+    }
+    __syncthreads();
+    SplitScalars hs = {};
+    if constexpr (SPLIT) hs = load_split_scalars(a.w);
+    ode_stage_body<1, PL, NT>(a, y, kin, tab + 36, 6, h, c->coef[5], c->sig[5], a.tproj6 + (size_t)5 * 768,
+                              const_cast<double*>(kin[6]), a.ybuf[c->yi ^ 1], sm, obj, y0s, y1s, esq, hs);
 }
 
 // Stage-kernel launch of `nt` column tiles per workgroup (1 for the exact-fp32 trunk).
@@ -617,6 +681,13 @@ __global__ __launch_bounds__(HT) void ode_control_kernel(gp_head_weights w, cons
     time_row(w, s.t32[blockIdx.x], emb, tf, tproj6 + (size_t)blockIdx.x * 768, blockIdx.y * PER, blockIdx.y * PER + PER);
 }
 
+// Device-controlled attempts as one fused launch (default) or six stage launches (GENPOSE2_ODE_FUSED=0: the
+// same bits; for A/B and the equality test).
+static bool ode_fused() {
+    const char* v = getenv("GENPOSE2_ODE_FUSED");
+    return v == nullptr || v[0] != '0';
+}
+
 // Workspace of the device-controlled path: ctl[2] | time rows (6 x 768 fp32) | error partials.
 static size_t auto_tproj_off() { return 2 * sizeof(OdeCtl); }
 static size_t auto_part_off() { return auto_tproj_off() + 6 * 768 * sizeof(float); }
@@ -664,6 +735,23 @@ extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, 
     a.ybuf[0] = y0;
     a.ybuf[1] = y1;
     for (int j = 0; j < ODE_NK; ++j) a.kbuf[j] = kslots[j];
+    if (ode_fused()) {   // one launch per attempt (ode_attempt_kernel)
+        OdeTableau tb;
+        for (int j = 0; j < 36; ++j) tb.A[j] = tableau_a[j];
+        for (int j = 0; j < 6; ++j) tb.B[j] = b[j];
+        for (int j = 0; j < ODE_NK; ++j) a.e[j] = e[j];
+        a.part = part;
+        const dim3 grid(nwg), blk(EVAL_WV * 64);
+        if (!w->pe2_h)
+            hipLaunchKernelGGL((ode_attempt_kernel<0, 1>), grid, blk, 0, stream, a, tb);
+        else if (nt == 4)
+            hipLaunchKernelGGL((ode_attempt_kernel<X3P, 4>), grid, blk, 0, stream, a, tb);
+        else if (nt == 2)
+            hipLaunchKernelGGL((ode_attempt_kernel<X3P, 2>), grid, blk, 0, stream, a, tb);
+        else
+            hipLaunchKernelGGL((ode_attempt_kernel<X3P, 1>), grid, blk, 0, stream, a, tb);
+        return gp_check_launch("ode_attempt_kernel");
+    }
     for (int s = 1; s < 6; ++s) {
         a.stage = s;
         a.nk = s;

@@ -509,6 +509,34 @@ def test_ode_device_controller_matches_host_controller(tag):
         assert np.abs(out[False][0] - out[True][0]).max() < 1e-4 * max(1.0, np.abs(out[True][0]).max())
 
 
+@pytest.mark.parametrize("case", ["t1_none", "ode_r4800", "ode_r12800"])
+def test_ode_fused_attempt_equals_stage_launches(case, monkeypatch):
+    """The device-controlled RK45 attempt as ONE launch (ode_attempt_kernel: the six stages back to back in
+    each workgroup, default) against six stage launches (GENPOSE2_ODE_FUSED=0): the same nfev and the same
+    bits, at 16-, 32- and 64-candidate tiles (R = 5, 4800, 12,800 rows; T0 = 1 is the case whose
+    accept/reject path follows last-bit differences)."""
+    import large_noise
+    from genpose2_amd.agent import NoiseFeed, PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    if case == "t1_none":
+        g = golden("ode")
+        pts, center, prior, K, T0 = (g["t1_none_pts"], g["t1_none_pts_center"], g["t1_none_prior"], 5, 1.0)
+    else:
+        _, _, B, K, _, T0, _ = large_noise.CASES[case]
+        pts, center, prior, _, _ = large_noise.inputs(case)
+    agent = PoseNet(GenPoseConfig(device=DEV, sampler_mode=["ode"], sampling_steps=None)).eval()
+    data = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("GENPOSE2_ODE_FUSED", fused)
+        agent.noise_feed = NoiseFeed(torch.from_numpy(prior))
+        pose, q = agent.pred_func(dict(data), repeat_num=K, T0=T0)
+        out[fused] = (pose.cpu().numpy(), q.cpu().numpy(), agent.last_nfev)
+    assert out["1"][2] == out["0"][2]
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+
+
 def test_ode_device_controller_full_size():
     """Config-2 shape (B=64, K=50, T0=0.55): device and host controllers agree on nfev, outputs are
     finite, rotations orthonormal."""
