@@ -124,6 +124,10 @@ _SIGS: Dict[str, tuple] = {
     "gp_img_encoder2": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
                                 c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gp_img_encoder3": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
+                                c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_size_t, c_void_p]),
+    "gp_img_encoder3_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
     "gp_img_geo_table": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "gp_gather_patch_points": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_void_p, c_void_p]),

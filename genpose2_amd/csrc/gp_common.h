@@ -12,6 +12,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // --------------------------------------------------------------- error plumbing (host)
 void gp_set_error(const char* fmt, ...);
 int gp_check_launch(const char* what);
+// the split linear with implicit im2col of a 3x3 conv (gp_fusion.hip; used by the image encoder, not part of the ABI)
+int gp_linear_split_conv3x3(const float* f, int b, int g, int d, const int32_t* wpk, const float* bias, int n,
+                            float* y, const float* rmax, hipStream_t st);
 
 #define GP_REQUIRE(cond, ...)                   \
     do {                                        \

@@ -277,6 +277,10 @@ struct SplitLinArgs {
     float* y;
     int ldy;
     unsigned* ymax;       // or null: per-row max |y| (bits of a float >= 0 order as unsigned: atomicMax)
+    // IM = 1 (implicit im2col of a 3x3 / pad 1 conv): x is the (objects, g*g pixels, d) feature map, row r = pixel
+    // (r / gg, r % gg) of object r / gg, k = 9 d in position-major order (k index = (ky * 3 + kx) * d + channel):
+    // chunk c reads the 32 channels (c % d32) * 32.. of neighbour c / d32 -- zeros outside the grid
+    int im_g, im_d32;
 };
 template <int WO, int JT = 4>
 constexpr size_t sl_lds_bytes() {
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(256) void fus_rowmax_kernel(const float* __restrict
     if (lane == 0) rmax[r] = v;
 }
 
-template <int WO, int ACT, int JT = 4>
+template <int WO, int ACT, int JT = 4, int IM = 0>
 __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a) {
     // RU: (token row, k-group pair) items per thread. Item (row br, k-groups bq and bq + 4) fills one 16-byte
     // B-fragment entry per plane, and a wave's 16-lane store phases cover 16 rows of one k-group: entries of
@@ -317,6 +321,7 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
     const f16x8* W = reinterpret_cast<const f16x8*>(a.w + 4);
     int row[RU], brow[RU], bq[RU];
     float sc[RU];
+    int py[RU], px[RU];   // IM: the row's pixel
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
         const int idx = tid + SL_THREADS * u;
@@ -327,7 +332,28 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
         const int E = mx > 1e-30f ? ilog2f(mx) : -100;
         sc[u] = exp2i(14 - E);
         if (bq[u] == 0) eT[brow[u]] = E;
+        if constexpr (IM) {
+            const int p = row[u] % (a.im_g * a.im_g);
+            py[u] = p / a.im_g;
+            px[u] = p - py[u] * a.im_g;
+        }
     }
+    // x of chunk c for item u: its two 16-byte k-groups (IM: the neighbour pixel's channels, zeros off the grid)
+    auto xload = [&](int c, int u, f32x4& v0, f32x4& v1) {
+        if constexpr (IM) {
+            const int k9 = c / a.im_d32, cc = c - k9 * a.im_d32;   // wave-uniform
+            const int dy = k9 / 3 - 1, dx = k9 - (k9 / 3) * 3 - 1;
+            const int yy = py[u] + dy, xx = px[u] + dx;
+            const bool in = row[u] < a.m && yy >= 0 && yy < a.im_g && xx >= 0 && xx < a.im_g;
+            const float* xr = a.x + (size_t)(in ? row[u] + dy * a.im_g + dx : 0) * a.ldx + 32 * cc + 4 * bq[u];
+            v0 = in ? ld4(xr) : f32x4{0.f, 0.f, 0.f, 0.f};
+            v1 = in ? ld4(xr + 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+            const float* xr = a.x + (size_t)row[u] * a.ldx + 32 * c + 4 * bq[u];
+            v0 = row[u] < a.m ? ld4(xr) : f32x4{0.f, 0.f, 0.f, 0.f};
+            v1 = row[u] < a.m ? ld4(xr + 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
     // A (the packed weight planes, stored as they are): SL_DMA copies them global -> LDS directly
     // (global_load_lds_dwordx4: no registers, no ds_write; the wave's 64 lanes fill 1 KB at its LDS base)
     auto load = [&](int c, int sdst, f32x4 (&ra)[WO], f32x4 (&rb)[2 * RU]) {
@@ -344,11 +370,7 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
 #endif
         }
 #pragma unroll
-        for (int u = 0; u < RU; ++u) {
-            const float* xr = a.x + (size_t)row[u] * a.ldx + 32 * c + 4 * bq[u];
-            rb[2 * u] = row[u] < a.m ? ld4(xr) : f32x4{0.f, 0.f, 0.f, 0.f};
-            rb[2 * u + 1] = row[u] < a.m ? ld4(xr + 16) : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+        for (int u = 0; u < RU; ++u) xload(c, u, rb[2 * u], rb[2 * u + 1]);
     };
     auto store = [&](int s, const f32x4 (&ra)[WO], const f32x4 (&rb)[2 * RU]) {
 #if !SL_DMA
@@ -400,11 +422,7 @@ __global__ __launch_bounds__(SL_THREADS) void linear_split_kernel(SplitLinArgs a
                 }
             if constexpr ((SL_DIAG & 1) == 0)
 #pragma unroll
-                for (int u = 0; u < RU; ++u) {
-                    const float* xr = a.x + (size_t)row[u] * a.ldx + 32 * (c + 1) + 4 * bq[u];
-                    rb[2 * u] = row[u] < a.m ? ld4(xr) : f32x4{0.f, 0.f, 0.f, 0.f};
-                    rb[2 * u + 1] = row[u] < a.m ? ld4(xr + 16) : f32x4{0.f, 0.f, 0.f, 0.f};
-                }
+                for (int u = 0; u < RU; ++u) xload(c + 1, u, rb[2 * u], rb[2 * u + 1]);
         }
 #else
         if (c + 1 < KC) load(c + 1, s ^ 1, ra, rb);
@@ -530,7 +548,7 @@ extern "C" int gp_linear_split(const float* x, int ldx, int m, int k, const int3
     }
     if (ymax && hipMemsetAsync(ymax, 0, sizeof(float) * (size_t)m, st) != hipSuccess)
         return gp_check_launch("linear_split ymax memset");
-    SplitLinArgs a{x, ldx, m, k, rmax, wpk, bias, n, y, ldy, reinterpret_cast<unsigned*>(ymax)};
+    SplitLinArgs a{x, ldx, m, k, rmax, wpk, bias, n, y, ldy, reinterpret_cast<unsigned*>(ymax), 0, 0};
     const int npad = (n + 127) / 128 * 128;
 #define GP_LSPLIT(WO, JT)                                                                                          \
     {                                                                                                          \
@@ -547,6 +565,33 @@ extern "C" int gp_linear_split(const float* x, int ldx, int m, int k, const int3
     else GP_LSPLIT(2, 4)
 #undef GP_LSPLIT
     return gp_check_launch("linear_split_kernel");
+}
+
+// relu(conv3x3(f) + bias) over every pixel of b objects of a g x g grid (stride 1, zero padding 1) as the split
+// linear with implicit im2col: f (b, g*g, d) pixel-major, wpk = pack_split_linear of the weight in position-major
+// order ((n, 3, 3, d) rows: k index (ky * 3 + kx) * d + channel), rmax[b * g * g] = max |x| over each pixel's im2col
+// row (its in-grid neighbours' channel maxima), y (b * g * g, n). No (b g^2, 9 d) column buffer is formed.
+int gp_linear_split_conv3x3(const float* f, int b, int g, int d, const int32_t* wpk, const float* bias, int n,
+                            float* y, const float* rmax, hipStream_t st) {
+    GP_REQUIRE(f && wpk && bias && y && rmax && b >= 0 && g >= 1, "conv3x3_split: bad arguments");
+    GP_REQUIRE(d % 32 == 0 && n >= 16 && n % 16 == 0, "conv3x3_split: d=%d (multiple of 32), n=%d (of 16)", d, n);
+    GP_REQUIRE(((uintptr_t)f | (uintptr_t)wpk | (uintptr_t)y | (uintptr_t)bias) % 16 == 0,
+               "conv3x3_split: pointers must be 16-byte aligned");
+    const int m = b * g * g, k = 9 * d;
+    if (!m) return GP_OK;
+    SplitLinArgs a{f, d, m, k, rmax, wpk, bias, n, y, n, nullptr, g, d / 32};
+    const int npad = (n + 127) / 128 * 128;
+#define GP_LSPLIT_IM(WO)                                                                                       \
+    {                                                                                                          \
+        constexpr int BM = 16 * 4 * (8 / WO);                                                                  \
+        const dim3 grid(npad / (64 * WO), (m + BM - 1) / BM);                                                  \
+        constexpr size_t lds = sl_lds_bytes<WO, 4>();                                                          \
+        hipLaunchKernelGGL((linear_split_kernel<WO, 1, 4, 1>), grid, dim3(SL_THREADS), lds, st, a);            \
+    }
+    if (npad % 256 == 0) GP_LSPLIT_IM(4)
+    else GP_LSPLIT_IM(2)
+#undef GP_LSPLIT_IM
+    return gp_check_launch("linear_split_kernel<im2col>");
 }
 
 // ============================================================================ residual + LayerNorm

@@ -73,6 +73,33 @@ __global__ __launch_bounds__(IE_THREADS) void imgenc_im2col_kernel(const float* 
     }
 }
 
+// Row maxima of the implicit im2col (gp_linear_split_conv3x3): pmax[t] = max |f[t][:]| per pixel (a wave per pixel),
+// then rmax[t] = the max of pmax over the pixel's in-grid 3x3 neighbourhood -- the max |x| of its im2col row (the
+// zero padding adds 0), bit for bit what a row max over the formed column buffer gives.
+__global__ __launch_bounds__(IE_THREADS) void imgenc_pixel_max_kernel(const float* __restrict__ f, int t, int d,
+                                                                      float* __restrict__ pmax) {
+    const int r = blockIdx.x * (IE_THREADS / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= t) return;
+    float v = 0.f;
+    for (int c = 4 * lane; c < d; c += 256) {
+        const f32x4 x = ld4(f + (size_t)r * d + c);
+        v = fmaxf(v, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    if (lane == 0) pmax[r] = v;
+}
+__global__ void imgenc_nbr_max_kernel(const float* __restrict__ pmax, int t, int g, float* __restrict__ rmax) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= t) return;
+    const int p = r % (g * g), y = p / g, x = p - y * g;
+    float v = 0.f;
+    for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx)
+            if (y + dy >= 0 && y + dy < g && x + dx >= 0 && x + dx < g) v = fmaxf(v, pmax[r + dy * g + dx]);
+    rmax[r] = v;
+}
+
 // edge[b][o] = (sum_p y[b][p][o], p in order) / np -- AdaptiveAvgPool2d(1)'s sequential sum (np = 256: the
 // division is exact scaling, as the reference's / kh / kw)
 __global__ void imgenc_pool_kernel(const float* __restrict__ y, int nb, int np, int co, float* __restrict__ edge) {
@@ -279,16 +306,17 @@ size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 struct ImgLayout {
     size_t h, fused, s, ft, o, col, ey, edge, rmax, total;
 };
-ImgLayout img_layout(int b, int np, int d) {
+// implicit: the split edge conv of gp_img_encoder3 (no column buffer; its output and pixel maxima for all objects)
+ImgLayout img_layout(int b, int np, int d, bool implicit = false) {
     ImgLayout L = {};
-    const int co = d / 4, hid = d / 2, chunk = b < IE_EDGE_CHUNK ? b : IE_EDGE_CHUNK;
+    const int co = d / 4, hid = d / 2, chunk = implicit ? b : (b < IE_EDGE_CHUNK ? b : IE_EDGE_CHUNK);
     size_t off = 0;
     L.h = off;     off += al256(sizeof(float) * 3 * (size_t)b * np * hid);
     L.fused = off; off += al256(sizeof(float) * (size_t)b * np * d);
     L.s = off;     off += al256(sizeof(float) * (size_t)b * np * np);
     L.ft = off;    off += al256(sizeof(float) * (size_t)b * np * d);
     L.o = off;     off += al256(sizeof(float) * (size_t)b * np * d);
-    L.col = off;   off += al256(sizeof(float) * (size_t)chunk * np * 9 * d);
+    L.col = off;   off += implicit ? al256(sizeof(float) * (size_t)b * np) : al256(sizeof(float) * (size_t)chunk * np * 9 * d);
     L.ey = off;    off += al256(sizeof(float) * (size_t)chunk * np * co);
     L.edge = off;  off += al256(sizeof(float) * (size_t)b * co);
     L.rmax = off;  off += al256(sizeof(float) * (size_t)b * np);   // split GEMMs: per-token row maxima
@@ -301,6 +329,10 @@ extern "C" size_t gp_img_encoder_workspace_size(int b, int np, int d) {
     return b >= 1 && np >= 1 && d >= 4 ? img_layout(b, np, d).total : 0;
 }
 
+extern "C" size_t gp_img_encoder3_workspace_size(int b, int np, int d, int split_conv) {
+    return b >= 1 && np >= 1 && d >= 4 ? img_layout(b, np, d, split_conv != 0).total : 0;
+}
+
 // y = relu(x W^T + b): split-f16 (gp_linear_split, the token linears' arithmetic: per-token power-of-two scaling,
 // three f16 products) when the weight planes are given, exact fp32 MFMA (gp_linear) otherwise
 static int img_linear_relu(const float* x, int m, int k, const float* w, const int32_t* wh, const float* bias, int n,
@@ -309,11 +341,12 @@ static int img_linear_relu(const float* x, int m, int k, const float* w, const i
     return gp_linear(x, k, m, k, w, bias, n, 1, y, n, st);
 }
 
-extern "C" int gp_img_encoder2(const float* l0, const float* l1, const float* l2, int b, int np, int d,
-                               const float* la_w1, const float* la_b1, const float* la_w2, float la_b2,
-                               const float* geo_table, const float* conv_w, const float* conv_b, float geo_gate,
-                               float edge_gate, const int32_t* la_w1_h, const int32_t* conv_w_h, float* out,
-                               float* layer_w, float* edge_out, void* workspace, size_t workspace_bytes, hipStream_t st) {
+// implicit: conv_w_h holds the position-major planes and the edge conv runs as gp_linear_split_conv3x3
+static int img_encoder_impl(const float* l0, const float* l1, const float* l2, int b, int np, int d,
+                            const float* la_w1, const float* la_b1, const float* la_w2, float la_b2,
+                            const float* geo_table, const float* conv_w, const float* conv_b, float geo_gate,
+                            float edge_gate, const int32_t* la_w1_h, const int32_t* conv_w_h, bool implicit, float* out,
+                            float* layer_w, float* edge_out, void* workspace, size_t workspace_bytes, hipStream_t st) {
     GP_REQUIRE(l0 && l1 && l2 && la_w1 && la_b1 && la_w2 && geo_table && conv_w && conv_b && out && workspace,
                "img_encoder: null pointer");
     GP_REQUIRE(b >= 0 && np >= 4 && d % 64 == 0, "img_encoder: need np >= 4 and d a multiple of 64 (d=%d)", d);
@@ -321,8 +354,10 @@ extern "C" int gp_img_encoder2(const float* l0, const float* l1, const float* l2
     while (g * g < np) ++g;
     GP_REQUIRE(g * g == np && np % 16 == 0, "img_encoder: np=%d must be a square grid with np %% 16 == 0", np);
     if (!b) return GP_OK;
-    const ImgLayout L = img_layout(b, np, d);
-    GP_REQUIRE(workspace_bytes >= L.total, "img_encoder: workspace too small (gp_img_encoder_workspace_size)");
+    implicit = implicit && conv_w_h != nullptr;
+    const ImgLayout L = img_layout(b, np, d, implicit);
+    GP_REQUIRE(workspace_bytes >= L.total, "img_encoder: workspace too small (gp_img_encoder%s_workspace_size)",
+               implicit ? "3" : "");
     char* ws = static_cast<char*>(workspace);
     float* h = reinterpret_cast<float*>(ws + L.h);
     float* fused = reinterpret_cast<float*>(ws + L.fused);
@@ -344,7 +379,20 @@ extern "C" int gp_img_encoder2(const float* l0, const float* l1, const float* l2
                        la_w2, la_b2, l0, l1, l2, T, d, fused, layer_w);
     if ((rc = gp_check_launch("imgenc_layer_fuse_kernel"))) return rc;
     // 2. edge branch: im2col GEMM + ReLU per chunk of objects, then the pixel mean
-    for (int c0 = 0; c0 < b; c0 += IE_EDGE_CHUNK) {
+    if (implicit) {   // the split GEMM gathers its column rows from the feature map itself
+        float* pmax = col;   // (b * np) pixel maxima in the implicit layout
+        hipLaunchKernelGGL(imgenc_pixel_max_kernel, dim3((T + 3) / 4), dim3(IE_THREADS), 0, st, (const float*)fused, T, d,
+                           pmax);
+        if ((rc = gp_check_launch("imgenc_pixel_max_kernel"))) return rc;
+        hipLaunchKernelGGL(imgenc_nbr_max_kernel, dim3((T + 255) / 256), dim3(256), 0, st, (const float*)pmax, T, g,
+                           rmax);
+        if ((rc = gp_check_launch("imgenc_nbr_max_kernel"))) return rc;
+        if ((rc = gp_linear_split_conv3x3(fused, b, g, d, conv_w_h, conv_b, co, ey, rmax, st))) return rc;
+        hipLaunchKernelGGL(imgenc_pool_kernel, dim3((b * co + 255) / 256), dim3(256), 0, st, (const float*)ey, b, np, co,
+                           edge);
+        if ((rc = gp_check_launch("imgenc_pool_kernel"))) return rc;
+    }
+    for (int c0 = 0; c0 < (implicit ? 0 : b); c0 += IE_EDGE_CHUNK) {
         const int nb = b - c0 < IE_EDGE_CHUNK ? b - c0 : IE_EDGE_CHUNK;
         hipLaunchKernelGGL(imgenc_im2col_kernel, dim3(nb * np), dim3(IE_THREADS), 0, st,
                            (const float*)(fused + (size_t)c0 * np * d), np, g, d, col);
@@ -371,6 +419,24 @@ extern "C" int gp_img_encoder2(const float* l0, const float* l1, const float* l2
                        st, (const float*)fused, (const float*)o, (const float*)edge, np, d, co, geo_gate, edge_gate, n,
                        out);
     return gp_check_launch("imgenc_combine_kernel");
+}
+
+extern "C" int gp_img_encoder2(const float* l0, const float* l1, const float* l2, int b, int np, int d,
+                               const float* la_w1, const float* la_b1, const float* la_w2, float la_b2,
+                               const float* geo_table, const float* conv_w, const float* conv_b, float geo_gate,
+                               float edge_gate, const int32_t* la_w1_h, const int32_t* conv_w_h, float* out,
+                               float* layer_w, float* edge_out, void* workspace, size_t workspace_bytes, hipStream_t st) {
+    return img_encoder_impl(l0, l1, l2, b, np, d, la_w1, la_b1, la_w2, la_b2, geo_table, conv_w, conv_b, geo_gate,
+                            edge_gate, la_w1_h, conv_w_h, false, out, layer_w, edge_out, workspace, workspace_bytes, st);
+}
+
+extern "C" int gp_img_encoder3(const float* l0, const float* l1, const float* l2, int b, int np, int d,
+                               const float* la_w1, const float* la_b1, const float* la_w2, float la_b2,
+                               const float* geo_table, const float* conv_w, const float* conv_b, float geo_gate,
+                               float edge_gate, const int32_t* la_w1_h, const int32_t* conv_w_hp, float* out,
+                               float* layer_w, float* edge_out, void* workspace, size_t workspace_bytes, hipStream_t st) {
+    return img_encoder_impl(l0, l1, l2, b, np, d, la_w1, la_b1, la_w2, la_b2, geo_table, conv_w, conv_b, geo_gate,
+                            edge_gate, la_w1_h, conv_w_hp, true, out, layer_w, edge_out, workspace, workspace_bytes, st);
 }
 
 extern "C" int gp_img_encoder(const float* l0, const float* l1, const float* l2, int b, int np, int d,

@@ -46,6 +46,9 @@ def pack_img_encoder(sd: weights.StateDict, prefix: str = "img_encoder") -> Dict
            "conv_w": g("edge_guide.0.weight"), "conv_b": g("edge_guide.0.bias")}
     out["la_w1_h"] = pack_split_linear(out["la_w1"])
     out["conv_w_h"] = pack_split_linear(out["conv_w"].reshape(out["conv_w"].shape[0], -1))
+    # position-major (k index (ky * 3 + kx) * d + channel) for gp_img_encoder3's implicit im2col GEMM
+    out["conv_w_hp"] = pack_split_linear(
+        np.ascontiguousarray(out["conv_w"].transpose(0, 2, 3, 1)).reshape(out["conv_w"].shape[0], -1))
     return out
 
 
@@ -96,20 +99,24 @@ class ImgEncoderModel:
         B, n, d = ls[0].shape
         if any(tuple(v.shape) != (B, n, d) for v in ls):
             raise ValueError("the three DINOv3 layers must have one shape (B, np, d)")
-        need = int(self.lib.gp_img_encoder_workspace_size(B, n, d))
+        split = self.arith == "split_f16"
+        # the edge conv's split GEMM with implicit im2col (gp_img_encoder3), or over a formed column buffer
+        # (gp_img_encoder2, GENPOSE2_IMG_IMPLICIT=0: same products, another summation order)
+        implicit = os.environ.get("GENPOSE2_IMG_IMPLICIT", "1")[:1] != "0"
+        need = int(self.lib.gp_img_encoder3_workspace_size(B, n, d, int(split)) if implicit
+                   else self.lib.gp_img_encoder_workspace_size(B, n, d))
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         out = torch.empty((B, n, d), dtype=torch.float32, device=self.device)
         lw = torch.empty((B, n, 3), dtype=torch.float32, device=self.device) if return_parts else None
         edge = torch.empty((B, d // 4), dtype=torch.float32, device=self.device) if return_parts else None
         b2, gg, eg = (float(v) for v in self.scalars)
-        split = self.arith == "split_f16"
-        check(self.lib.gp_img_encoder2(_vp(ls[0]), _vp(ls[1]), _vp(ls[2]), B, n, d, _vp(self.t["la_w1"]),
-                                       _vp(self.t["la_b1"]), _vp(self.t["la_w2"]), b2, _vp(self.t["geo_table"]),
-                                       _vp(self.t["conv_w"]), _vp(self.t["conv_b"]), gg, eg,
-                                       _vp(self.t["la_w1_h"] if split else None),
-                                       _vp(self.t["conv_w_h"] if split else None), _vp(out), _vp(lw),
-                                       _vp(edge), _vp(self._ws), self._ws.numel(), self._s()), "img_encoder")
+        fn = self.lib.gp_img_encoder3 if implicit else self.lib.gp_img_encoder2
+        conv_h = self.t["conv_w_hp" if implicit else "conv_w_h"]
+        check(fn(_vp(ls[0]), _vp(ls[1]), _vp(ls[2]), B, n, d, _vp(self.t["la_w1"]), _vp(self.t["la_b1"]),
+                 _vp(self.t["la_w2"]), b2, _vp(self.t["geo_table"]), _vp(self.t["conv_w"]), _vp(self.t["conv_b"]), gg,
+                 eg, _vp(self.t["la_w1_h"] if split else None), _vp(conv_h if split else None), _vp(out), _vp(lw),
+                 _vp(edge), _vp(self._ws), self._ws.numel(), self._s()), "img_encoder")
         if return_parts:
             return out, {"layer_w": lw, "edge": edge}
         return out

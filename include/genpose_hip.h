@@ -391,6 +391,19 @@ int gp_img_encoder2(const float *l0, const float *l1, const float *l2, int b, in
                     float edge_gate, const int32_t *la_w1_h, const int32_t *conv_w_h, float *out,
                     float *layer_w, float *edge_out, void *workspace, size_t workspace_bytes,
                     hipStream_t stream);
+/* gp_img_encoder2 with the edge conv's split-f16 GEMM gathering its im2col rows from the fused feature map
+ * itself (implicit GEMM: no (b np, 9d) column buffer, ~906 MB at b = 256, np = 256, d = 384). conv_w_hp are the
+ * planes of conv_w in POSITION-major order: fus_encoder.pack_split_linear of conv_w.permute(0, 2, 3, 1) as its
+ * (d/4, 9d) rows (k index (ky * 3 + kx) * d + channel). The products are the same, summed in that order: within
+ * rounding of gp_img_encoder2. conv_w_hp == NULL runs the edge conv in exact fp32 (as gp_img_encoder2 does).
+ * Workspace: gp_img_encoder3_workspace_size(b, np, d, conv_w_hp != NULL). */
+size_t gp_img_encoder3_workspace_size(int b, int np, int d, int split_conv);
+int gp_img_encoder3(const float *l0, const float *l1, const float *l2, int b, int np, int d,
+                    const float *la_w1, const float *la_b1, const float *la_w2, float la_b2,
+                    const float *geo_table, const float *conv_w, const float *conv_b, float geo_gate,
+                    float edge_gate, const int32_t *la_w1_h, const int32_t *conv_w_hp, float *out,
+                    float *layer_w, float *edge_out, void *workspace, size_t workspace_bytes,
+                    hipStream_t stream);
 /* HOST: the geometric attention's position table rel_pos_emb(rel_pos_idx).sum(-1) (img_encoder.py:
  * 68-76): table[i][j] = sum_k E[clamp((r_j - r_i + g - 1)(2g - 1) + (c_j - c_i + g - 1), 0, num_emb - 1)][k]
  * for patches i, j at (row, col) = (p / g, p % g). rel_pos_emb (num_emb, edim) host -> table (g^2, g^2)

@@ -391,6 +391,45 @@ def test_img_encoder_vs_reference_golden(tag, arith):
     assert rel(got[0, :64], g[f"{tag}_gather0"]) < 1e-5
 
 
+@pytest.mark.parametrize("B", [3, 40])
+def test_img_encoder_implicit_im2col_vs_column_buffer(B):
+    """gp_img_encoder3 (the edge conv's split GEMM gathering its im2col rows from the feature map, position-major
+    planes) against gp_img_encoder2 (the formed column buffer, channel-major planes): the same products, the same
+    per-row scaling (the row maxima are exact), summed in another order -- within 2e-6 of max|out| on the final
+    features and the edge weights; with NULL planes (exact fp32) both run the same kernels: bit-identical."""
+    import ctypes
+    import make_golden_img as mi
+    from genpose2_amd import _lib, weights
+    from genpose2_amd.img_encoder import ImgEncoderModel
+    lib = _lib.load()
+    model = ImgEncoderModel(weights.synthetic_state_dict("score_pointwise", seed=0), torch.device(DEV))
+    layers = [torch.from_numpy(v).to(DEV) for v in mi.dino_layers(B, 1.0, 77)]
+    n, d = layers[0].shape[1], layers[0].shape[2]
+    b2, gg, eg = (float(v) for v in model.scalars)
+    t = model.t
+    vp = lambda x: ctypes.c_void_p(None if x is None else x.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def run(fn, conv_planes, split_la):
+        need = max(int(lib.gp_img_encoder_workspace_size(B, n, d)), int(lib.gp_img_encoder3_workspace_size(B, n, d, 1)))
+        ws = torch.empty(need, dtype=torch.uint8, device=DEV)
+        out = torch.empty((B, n, d), device=DEV)
+        edge = torch.empty((B, d // 4), device=DEV)
+        _lib.check(fn(vp(layers[0]), vp(layers[1]), vp(layers[2]), B, n, d, vp(t["la_w1"]), vp(t["la_b1"]),
+                      vp(t["la_w2"]), b2, vp(t["geo_table"]), vp(t["conv_w"]), vp(t["conv_b"]), gg, eg,
+                      vp(t["la_w1_h"] if split_la else None), vp(conv_planes), vp(out), None, vp(edge), vp(ws),
+                      ws.numel(), st), "img_encoder")
+        return out.cpu().numpy(), edge.cpu().numpy()
+    o2, e2 = run(lib.gp_img_encoder2, t["conv_w_h"], True)
+    o3, e3 = run(lib.gp_img_encoder3, t["conv_w_hp"], True)
+    assert rel(o3, o2) < 2e-6 and rel(e3, e2) < 2e-6, (rel(o3, o2), rel(e3, e2))
+    assert not np.array_equal(e3, e2) or B < 4   # the implicit path ran (its K order rounds differently)
+    f2, g2 = run(lib.gp_img_encoder2, None, False)
+    f3, g3 = run(lib.gp_img_encoder3, None, False)
+    np.testing.assert_array_equal(f3, f2)
+    np.testing.assert_array_equal(g3, g2)
+
+
 class _Backbone:
     def __init__(self, layers):
         self.layers = layers
