@@ -233,3 +233,62 @@ def test_c_host_ode_sample_large_rows():
     ppose, _ = agent.pred_func({"pts": pts, "pts_center": center}, repeat_num=K, T0=T0)
     assert agent.last_nfev == nfev
     assert np.abs(ppose.cpu().numpy().reshape(-1, 9)[:, :6] - pose[:, :6]).max() < 1e-4
+
+
+def test_c_host_pc_sample_global_one_shard_and_exchange_failure():
+    """gp_pc_sample_global through the C ABI: one shard of a one-shard batch (the exchange callback is called
+    after every scoring launch with the slot the launch wrote, and has nothing to gather) gives gp_pc_sample's
+    bits; a callback that fails ends the call with an error instead of sampling on."""
+    from genpose2_amd import _lib, weights
+    B, K, T, N = 4, 64, 12, 1024
+    lib, h = _pack(0, weights.synthetic_state_dict("score"))
+    try:
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        from genpose2_amd import synthetic
+        pts, center = synthetic.make_batch(3, B, N)
+        pts, center = torch.from_numpy(pts).to(DEV), torch.from_numpy(center).to(DEV)
+        hw, pobj = _handle_features(lib, h, pts, B, N, s)
+        tab = np.zeros((T, 5), np.float32)
+        _lib.check(lib.gp_pc_step_table(T, ctypes.c_float(1e-5), tab.ctypes.data_as(ctypes.c_void_p)))
+        tproj = torch.empty(T, 768, device=DEV)
+        _lib.check(lib.gp_head_time_proj(hw, _vp(torch.from_numpy(np.ascontiguousarray(tab[:, 0])).to(DEV)), T,
+                                         _vp(tproj), s))
+        R = B * K
+        x0 = torch.randn(R, 9, device=DEV, generator=torch.Generator(DEV).manual_seed(5)) * 50.0
+        pws = torch.empty(int(lib.gp_pc_workspace_size(R)), dtype=torch.uint8, device=DEV)
+
+        def plain():
+            x, res, q = x0.clone(), torch.empty(R, 9, device=DEV), torch.empty(R, 7, device=DEV)
+            _lib.check(lib.gp_pc_sample(hw, _vp(pobj), _vp(tproj), tab.ctypes.data_as(ctypes.c_void_p), T, _vp(x), R, K,
+                                        _vp(center), None, None, ctypes.c_uint64(9), ctypes.c_float(0.16), _vp(res),
+                                        _vp(q), None, _vp(pws), pws.numel(), s), "pc_sample")
+            return res
+
+        n = int(lib.gp_pc_global_partials(R, R, 1, 1))
+        part = torch.zeros(2 * n, device=DEV)
+        calls = []
+
+        def run_global(fail_at=None):
+            def cb(ctx, step, slot, nn, stream):
+                calls.append((step, slot - part.data_ptr(), nn))
+                return -1 if step == fail_at else 0
+            fn = _lib.PC_EXCHANGE_FN(cb)
+            x, res, q = x0.clone(), torch.empty(R, 9, device=DEV), torch.empty(R, 7, device=DEV)
+            rc = lib.gp_pc_sample_global(hw, _vp(pobj), _vp(tproj), tab.ctypes.data_as(ctypes.c_void_p), T, _vp(x), R,
+                                         K, _vp(center), ctypes.c_uint64(9), ctypes.c_float(0.16), _vp(res), _vp(q),
+                                         None, R, 0, 0, 1, R, _vp(part), fn, None, _vp(pws), pws.numel(), s)
+            return rc, res
+        ref = plain()
+        rc, got = run_global()
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+        assert [c[0] for c in calls] == list(range(T)) and all(c[2] == n for c in calls)
+        assert [c[1] for c in calls] == [4 * n * (i & 1) for i in range(T)]   # slot i & 1 of the partials
+        calls.clear()
+        rc, _ = run_global(fail_at=3)
+        torch.cuda.synchronize()
+        assert rc != 0 and [c[0] for c in calls] == [0, 1, 2, 3]
+        assert "exchange" in lib.gp_last_error().decode()
+    finally:
+        lib.gp_weights_free(h)
