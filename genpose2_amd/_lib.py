@@ -112,6 +112,9 @@ _SIGS: Dict[str, tuple] = {
     "gp_ode_auto_attempt": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_int, c_int, c_double, c_double, c_double,
                                     c_double, c_double, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p]),
+    "gp_ode_auto_attempt_hs": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_int, c_int, c_double, c_double, c_double,
+                                    c_double, c_double, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p]),
     "gp_pc_step_table": (c_int, [c_int, c_float, c_void_p]),
     "gp_ode_sample_workspace_size": (c_size_t, [c_int]),
     "gp_ode_sample": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_int, c_int, c_double, c_double,

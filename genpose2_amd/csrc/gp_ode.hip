@@ -11,6 +11,7 @@
 // controller's scalars stay on the host (genpose2_amd/ode.py): one 8-byte read per attempt. The
 // device-controlled attempts (gp_ode_auto_attempt) run all six stages of an attempt in one launch
 // (ode_attempt_kernel); the host-controlled ones launch each stage (ode_stage_kernel).
+#include <chrono>
 #include <cstddef>
 #include <cstdlib>
 #include <mutex>
@@ -605,9 +606,12 @@ struct OdeConsts {
 
 #define ODE_CTL_CHUNKS 8   // workgroups per stage time row (768 / 8 outputs each)
 
+// hstat (optional, host-mapped memory): word n & 3 receives 4 n + (status + 1) once attempt n is decided and prepared,
+// so a host can follow the solve without an event and a copy between the control and the stage launches
 __global__ __launch_bounds__(HT) void ode_control_kernel(gp_head_weights w, const OdeCtl* __restrict__ cin,
                                                          OdeCtl* __restrict__ cout, const double* __restrict__ part,
-                                                         int decide, OdeConsts k, float* __restrict__ tproj6) {
+                                                         int decide, OdeConsts k, float* __restrict__ tproj6,
+                                                         int* __restrict__ hstat, int n) {
 #pragma clang fp contract(off)
     __shared__ double red[4];
     __shared__ OdeCtl s;
@@ -661,7 +665,13 @@ __global__ __launch_bounds__(HT) void ode_control_kernel(gp_head_weights w, cons
     }
     __syncthreads();
     if (!s.active) {
-        if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) *cout = s;
+        if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+            *cout = s;
+            if (hstat != nullptr) {
+                __threadfence_system();
+                reinterpret_cast<volatile int*>(hstat)[n & 3] = 4 * n + s.status + 1;
+            }
+        }
         return;
     }
     // stage times t + c_s h (s = 1..5) and t + h, one thread each (rk.py rk_step)
@@ -675,7 +685,13 @@ __global__ __launch_bounds__(HT) void ode_control_kernel(gp_head_weights w, cons
         s.coef[tid] = -(0.5 * (g * g));
     }
     __syncthreads();
-    if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) *cout = s;
+    if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+        *cout = s;
+        if (hstat != nullptr) {
+            __threadfence_system();
+            reinterpret_cast<volatile int*>(hstat)[n & 3] = 4 * n + s.status + 1;
+        }
+    }
     // time row slice of stage blockIdx.x: outputs [chunk * 96, chunk * 96 + 96)
     constexpr int PER = 768 / ODE_CTL_CHUNKS;
     time_row(w, s.t32[blockIdx.x], emb, tf, tproj6 + (size_t)blockIdx.x * 768, blockIdx.y * PER, blockIdx.y * PER + PER);
@@ -698,12 +714,11 @@ extern "C" size_t gp_ode_auto_workspace_size(int rows) {
     return auto_part_off() + sizeof(double) * (((size_t)rows + 15) / 16) + 256;
 }
 
-extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, int n, int what,
-                                   double t_bound, double direction, double rtol, double atol, double sig_min,
-                                   double base, double diff_scale, double* y0, double* y1,
-                                   double* const* kslots, const double* tableau_a, const double* b,
-                                   const double* e, int rows, int k, void* workspace, size_t workspace_bytes,
-                                   hipStream_t stream) {
+static int ode_auto_attempt_impl(const gp_head_weights* w, const float* pobj, int n, int what, double t_bound,
+                                 double direction, double rtol, double atol, double sig_min, double base,
+                                 double diff_scale, double* y0, double* y1, double* const* kslots,
+                                 const double* tableau_a, const double* b, const double* e, int rows, int k,
+                                 void* workspace, size_t workspace_bytes, int* hstat, hipStream_t stream) {
     GP_REQUIRE(w && pobj && y0 && y1 && kslots && tableau_a && b && e && workspace && rows >= 1 && k >= 1 && n >= 0,
                "ode_auto_attempt: bad arguments");
     GP_REQUIRE(workspace_bytes >= gp_ode_auto_workspace_size(rows), "ode_auto_attempt: workspace too small");
@@ -719,7 +734,7 @@ extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, 
     GP_REQUIRE(what >= 1 && what <= 3, "ode_auto_attempt: what must be 1 (control), 2 (stages) or 3 (both)");
     if (what & 1) {
         hipLaunchKernelGGL(ode_control_kernel, dim3(6, ODE_CTL_CHUNKS), dim3(HT), 0, stream, *w, (const OdeCtl*)cin,
-                           cout, (const double*)part, n > 0 ? 1 : 0, kc, tproj6);
+                           cout, (const double*)part, n > 0 ? 1 : 0, kc, tproj6, hstat, n);
         const int rc = gp_check_launch("ode_control_kernel");
         if (rc || !(what & 2)) return rc;
     }
@@ -765,6 +780,27 @@ extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, 
     a.part = part;
     ode_launch_stage<1>(a, nt, stream);
     return gp_check_launch("ode_stage_kernel<auto>");
+}
+
+extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, int n, int what,
+                                   double t_bound, double direction, double rtol, double atol, double sig_min,
+                                   double base, double diff_scale, double* y0, double* y1,
+                                   double* const* kslots, const double* tableau_a, const double* b,
+                                   const double* e, int rows, int k, void* workspace, size_t workspace_bytes,
+                                   hipStream_t stream) {
+    return ode_auto_attempt_impl(w, pobj, n, what, t_bound, direction, rtol, atol, sig_min, base, diff_scale, y0, y1,
+                                 kslots, tableau_a, b, e, rows, k, workspace, workspace_bytes, nullptr, stream);
+}
+
+extern "C" int gp_ode_auto_attempt_hs(const gp_head_weights* w, const float* pobj, int n, int what,
+                                      double t_bound, double direction, double rtol, double atol, double sig_min,
+                                      double base, double diff_scale, double* y0, double* y1,
+                                      double* const* kslots, const double* tableau_a, const double* b,
+                                      const double* e, int rows, int k, void* workspace, size_t workspace_bytes,
+                                      int* host_status, hipStream_t stream) {
+    GP_REQUIRE(host_status != nullptr, "ode_auto_attempt_hs: null status words");
+    return ode_auto_attempt_impl(w, pobj, n, what, t_bound, direction, rtol, atol, sig_min, base, diff_scale, y0, y1,
+                                 kslots, tableau_a, b, e, rows, k, workspace, workspace_bytes, host_status, stream);
 }
 
 // ============================================================================ whole sampler (C hosts)
@@ -953,26 +989,55 @@ extern "C" int gp_ode_sample(const gp_head_weights* w, const float* pobj, const 
         return gp_ode_auto_attempt(w, pobj, a, what, tf, dir, rtol, atol, kSigMin, kBase, dscale, y[0], y[1], K,
                                    kA6, kB6, kE7, rows, k, aws, aws_b, stream);
     };
-    if ((rc = launch(0, 3))) return rc;
     const int rec = (int)sizeof(OdeCtl);
     const int stat_off = (int)offsetof(OdeCtl, status);
     int a = 0;
-    for (;; ++a) {
-        GP_REQUIRE(a < 100000, "ode_sample: attempt limit reached");
-        if ((rc = launch(a + 1, 1))) return rc;   // decides attempt a, prepares a + 1
-        const char* src = static_cast<const char*>(aws) + ((a + 2) & 1) * rec + stat_off;
-        status.pending = true;
-        GP_REQUIRE(hipMemcpyAsync(status.r.pinned, src, 4, hipMemcpyDeviceToHost, stream) == hipSuccess &&
-                       hipEventRecord(status.r.ev, stream) == hipSuccess, "ode_sample: status read");
-        if ((rc = launch(a + 1, 2))) return rc;   // attempt a + 1 (a no-op once the solve has ended)
-        GP_REQUIRE(hipEventSynchronize(status.r.ev) == hipSuccess, "ode_sample: status wait");
-        status.pending = false;
-        if (*status.r.pinned != 0) break;
+    int* hs_dev = nullptr;   // the pinned words as the device addresses them, if it can
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&hs_dev), status.r.pinned, 0) != hipSuccess) {
+        hs_dev = nullptr;
+        (void)hipGetLastError();
+    }
+    if (hs_dev != nullptr) {
+        // polled: the control kernel of attempt n writes 4 n + (status + 1) into pinned word n & 3; nothing sits
+        // between a control launch and its stage launch (gp_ode_auto_attempt_hs)
+        volatile int* hv = status.r.pinned;
+        for (int i = 0; i < 4; ++i) hv[i] = -1;
+        auto launch_hs = [&](int n) {
+            return gp_ode_auto_attempt_hs(w, pobj, n, 3, tf, dir, rtol, atol, kSigMin, kBase, dscale, y[0], y[1], K,
+                                          kA6, kB6, kE7, rows, k, aws, aws_b, hs_dev, stream);
+        };
+        status.pending = true;   // the device writes the words until the stream drains
+        if ((rc = launch_hs(0))) return rc;
+        for (;; ++a) {
+            GP_REQUIRE(a < 100000, "ode_sample: attempt limit reached");
+            if ((rc = launch_hs(a + 1))) return rc;   // decides attempt a, prepares and runs a + 1
+            const int want = a + 1;
+            const auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+            int v;
+            while (((v = hv[want & 3]) >> 2) != want)
+                GP_REQUIRE(std::chrono::steady_clock::now() < t_end, "ode_sample: no status from attempt %d", want);
+            if ((v & 3) - 1 != 0) break;
+        }
+    } else {
+        if ((rc = launch(0, 3))) return rc;
+        for (;; ++a) {
+            GP_REQUIRE(a < 100000, "ode_sample: attempt limit reached");
+            if ((rc = launch(a + 1, 1))) return rc;   // decides attempt a, prepares a + 1
+            const char* src = static_cast<const char*>(aws) + ((a + 2) & 1) * rec + stat_off;
+            status.pending = true;
+            GP_REQUIRE(hipMemcpyAsync(status.r.pinned, src, 4, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                           hipEventRecord(status.r.ev, stream) == hipSuccess, "ode_sample: status read");
+            if ((rc = launch(a + 1, 2))) return rc;   // attempt a + 1 (a no-op once the solve has ended)
+            GP_REQUIRE(hipEventSynchronize(status.r.ev) == hipSuccess, "ode_sample: status wait");
+            status.pending = false;
+            if (*status.r.pinned != 0) break;
+        }
     }
     OdeCtl c;
     GP_REQUIRE(hipMemcpyAsync(&c, static_cast<const char*>(aws) + ((a + 2) & 1) * rec, sizeof(OdeCtl),
                               hipMemcpyDeviceToHost, stream) == hipSuccess &&
                    hipStreamSynchronize(stream) == hipSuccess, "ode_sample: final record");
+    status.pending = false;
     if (status_out) *status_out = c.status;
     if (nfev_out) *nfev_out = c.nfev;
     GP_REQUIRE(!(c.status < 0 && steps > 0),

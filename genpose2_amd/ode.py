@@ -19,6 +19,8 @@ CPU tests to hold the controller to ``solve_ivp`` exactly).
 from __future__ import annotations
 
 import ctypes
+import os
+import time
 import warnings
 from typing import List, Optional, Tuple
 
@@ -419,6 +421,106 @@ def _side_resources(dev):
 STAGE_EVENTS: Optional[list] = None
 
 
+def _attempts_evented(launch, ws, rec, stream, side, stat, be, max_attempts: int) -> int:
+    """The attempt loop with an event after each control launch and a 4-byte status copy on a side stream
+    (GENPOSE2_ODE_ZC=0). Returns the index n of the attempt whose successor's control ended the solve."""
+    launch(0, 3)
+    n = 0
+    while True:
+        launch(n + 1, 1)                       # decides attempt n, prepares attempt n+1
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        timing = STAGE_EVENTS is not None
+        if timing:
+            s0 = torch.cuda.Event(enable_timing=True)
+            s1 = torch.cuda.Event(enable_timing=True)
+            s0.record(stream)
+        launch(n + 1, 2)                       # attempt n+1 (no-op if attempt n ended the solve)
+        if timing:
+            s1.record(stream)
+        off = ((n + 2) & 1) * rec + _STATUS_OFF
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            stat.copy_(ws[off:off + 4].view(torch.int32), non_blocking=True)
+        side.synchronize()
+        if int(stat[0]) != 0:
+            return n
+        if timing:
+            STAGE_EVENTS.append((s0, s1, be.R))
+        n += 1
+        if n > max_attempts:
+            raise RuntimeError("RK45: attempt limit reached")
+
+
+_HSTAT = {}
+_HIP = None
+
+
+def _host_status_words(dev):
+    """4 pinned int32 words the device can write (hipHostGetDevicePointer checks that the pinned allocation is
+    mapped for the device; None if not, and the caller keeps the evented loop), with the device-side address."""
+    global _HIP
+    r = _HSTAT.get(dev)
+    if r is None:
+        h = torch.full((4,), -1, dtype=torch.int32).pin_memory()
+        dp = ctypes.c_void_p()
+        try:
+            if _HIP is None:
+                _HIP = ctypes.CDLL("libamdhip64.so")
+            rc = _HIP.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(h.data_ptr()), 0)
+        except OSError:
+            rc = -1
+        r = (h, dp.value) if rc == 0 and dp.value else (None, None)
+        _HSTAT[dev] = r
+    return r
+
+
+def _attempts_polled(lib, be, args, stream, max_attempts: int, timeout_s: float = 60.0) -> int:
+    """The attempt loop with nothing between a control launch and its stage launch: the control kernel of
+    attempt n writes 4 n + (status + 1) into word n & 3 of a host-mapped pinned buffer (gp_ode_auto_attempt_hs),
+    and the host, one attempt ahead, polls that word. Same launches, same order, same bits as the evented loop."""
+    h, hdev = _host_status_words(be.dev)
+    hv = h.numpy()
+    hv[:] = -1
+    hp = ctypes.c_void_p(hdev)
+    w, pobj = ctypes.byref(be.h.w), ctypes.c_void_p(be.pobj.data_ptr())
+    a = args[:-1]
+
+    def launch(n, what):
+        check(lib.gp_ode_auto_attempt_hs(w, pobj, n, what, *a, hp, args[-1]), "ode_auto_attempt")
+
+    timing = STAGE_EVENTS is not None
+
+    def attempt(n):
+        if not timing:
+            launch(n, 3)
+            return None
+        launch(n, 1)
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record(stream)
+        launch(n, 2)
+        s1.record(stream)
+        return s0, s1
+
+    attempt(0)
+    n = 0
+    while True:
+        evs = attempt(n + 1)                   # control n+1 decides attempt n and prepares n+1; then attempt n+1
+        want = n + 1
+        t_end = time.monotonic() + timeout_s
+        while (int(hv[want & 3]) >> 2) != want:
+            if time.monotonic() > t_end:
+                raise RuntimeError(f"RK45: no status from the control kernel of attempt {want} in {timeout_s} s")
+        status = (int(hv[want & 3]) & 3) - 1
+        if status != 0:
+            return n
+        if evs is not None:
+            STAGE_EVENTS.append((evs[0], evs[1], be.R))
+        n += 1
+        if n > max_attempts:
+            raise RuntimeError("RK45: attempt limit reached")
+
+
 def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.ndarray] = None,
                 max_attempts: int = 100000):
     """solve_ivp(..., method="RK45", t_eval) with the step controller on the device.
@@ -460,33 +562,12 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
         check(lib.gp_ode_auto_attempt(ctypes.byref(be.h.w), ctypes.c_void_p(be.pobj.data_ptr()), n, what, *args),
               "ode_auto_attempt")
 
-    launch(0, 3)
-    n = 0
-    while True:
-        launch(n + 1, 1)                       # decides attempt n, prepares attempt n+1
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        timing = STAGE_EVENTS is not None
-        if timing:
-            s0 = torch.cuda.Event(enable_timing=True)
-            s1 = torch.cuda.Event(enable_timing=True)
-            s0.record(stream)
-        launch(n + 1, 2)                       # attempt n+1 (no-op if attempt n ended the solve)
-        if timing:
-            s1.record(stream)
-        off = ((n + 2) & 1) * rec + _STATUS_OFF
-        side.wait_event(ev)
-        with torch.cuda.stream(side):
-            stat.copy_(ws[off:off + 4].view(torch.int32), non_blocking=True)
-        side.synchronize()
-        if int(stat[0]) != 0:
-            break
-        if timing:
-            STAGE_EVENTS.append((s0, s1, be.R))
-        n += 1
-        if n > max_attempts:
-            raise RuntimeError("RK45: attempt limit reached")
+    if os.environ.get("GENPOSE2_ODE_ZC", "1")[:1] != "0" and _host_status_words(dev)[0] is not None:
+        n = _attempts_polled(lib, be, args, stream, max_attempts)
+    else:
+        n = _attempts_evented(launch, ws, rec, stream, side, stat, be, max_attempts)
     last = ((n + 2) & 1) * rec
+
     ctl = OdeCtl.from_buffer_copy(bytes(ws[last:last + rec].cpu().numpy()))
     if ctl.status < 0:
         warnings.warn("RK45: required step size is less than spacing between numbers.")

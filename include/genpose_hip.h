@@ -343,6 +343,16 @@ int gp_ode_auto_attempt(const gp_head_weights *w, const float *pobj, int n, int 
                         double *const *kslots, const double *tableau_a, const double *b,
                         const double *e, int rows, int k, void *workspace, size_t workspace_bytes,
                         hipStream_t stream);
+/* gp_ode_auto_attempt whose control kernel also reports to the host without a copy: host_status (4 ints of
+ * host memory the device can write, e.g. hipHostMalloc'd) word n & 3 becomes 4 n + (status + 1) once attempt n
+ * is decided and prepared, so the host can keep attempts enqueued and poll, with no event or copy between a
+ * control launch and its stage launch. */
+int gp_ode_auto_attempt_hs(const gp_head_weights *w, const float *pobj, int n, int what,
+                           double t_bound, double direction, double rtol, double atol,
+                           double sig_min, double base, double diff_scale, double *y0, double *y1,
+                           double *const *kslots, const double *tableau_a, const double *b,
+                           const double *e, int rows, int k, void *workspace, size_t workspace_bytes,
+                           int *host_status, hipStream_t stream);
 /* The whole ODE sampler in one call (cond_ode_sampler, samplers.py:180-258, with scipy solve_ivp
  * RK45, samplers.py:226-234) for hosts without Python: x0 (R,9) fp32 device = the prior sample
  * [+ init_x] at T0; select_initial_step on the host from two RHS norms, then device-controlled
