@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 import time
 import warnings
 from typing import List, Optional, Tuple
@@ -452,34 +453,43 @@ def _attempts_evented(launch, ws, rec, stream, side, stat, be, max_attempts: int
             raise RuntimeError("RK45: attempt limit reached")
 
 
-_HSTAT = {}
+_HSTAT_FREE = {}            # device -> free (pinned words, device address) pairs
+_HSTAT_LOCK = threading.Lock()
 _HIP = None
 
 
 def _host_status_words(dev):
-    """4 pinned int32 words the device can write (hipHostGetDevicePointer checks that the pinned allocation is
-    mapped for the device; None if not, and the caller keeps the evented loop), with the device-side address."""
+    """Lease 4 pinned int32 words the device can write, with their device-side address (hipHostGetDevicePointer
+    checks that the pinned allocation is mapped for the device), or (None, None) if it cannot (the caller then
+    keeps the evented loop). One lease per solve: concurrent solves on one device never share the words. Return
+    it with _release_status_words."""
     global _HIP
-    r = _HSTAT.get(dev)
-    if r is None:
-        h = torch.full((4,), -1, dtype=torch.int32).pin_memory()
-        dp = ctypes.c_void_p()
-        try:
-            if _HIP is None:
-                _HIP = ctypes.CDLL("libamdhip64.so")
-            rc = _HIP.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(h.data_ptr()), 0)
-        except OSError:
-            rc = -1
-        r = (h, dp.value) if rc == 0 and dp.value else (None, None)
-        _HSTAT[dev] = r
-    return r
+    with _HSTAT_LOCK:
+        free = _HSTAT_FREE.setdefault(dev, [])
+        if free:
+            return free.pop()
+    h = torch.full((4,), -1, dtype=torch.int32).pin_memory()
+    dp = ctypes.c_void_p()
+    try:
+        if _HIP is None:
+            _HIP = ctypes.CDLL("libamdhip64.so")
+        rc = _HIP.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(h.data_ptr()), 0)
+    except OSError:
+        rc = -1
+    return (h, dp.value) if rc == 0 and dp.value else (None, None)
 
 
-def _attempts_polled(lib, be, args, stream, max_attempts: int, timeout_s: float = 60.0) -> int:
+def _release_status_words(dev, lease) -> None:
+    if lease[0] is not None:
+        with _HSTAT_LOCK:
+            _HSTAT_FREE.setdefault(dev, []).append(lease)
+
+
+def _attempts_polled(lib, be, args, stream, lease, max_attempts: int, timeout_s: float = 60.0) -> int:
     """The attempt loop with nothing between a control launch and its stage launch: the control kernel of
     attempt n writes 4 n + (status + 1) into word n & 3 of a host-mapped pinned buffer (gp_ode_auto_attempt_hs),
     and the host, one attempt ahead, polls that word. Same launches, same order, same bits as the evented loop."""
-    h, hdev = _host_status_words(be.dev)
+    h, hdev = lease
     hv = h.numpy()
     hv[:] = -1
     hp = ctypes.c_void_p(hdev)
@@ -562,10 +572,17 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
         check(lib.gp_ode_auto_attempt(ctypes.byref(be.h.w), ctypes.c_void_p(be.pobj.data_ptr()), n, what, *args),
               "ode_auto_attempt")
 
-    if os.environ.get("GENPOSE2_ODE_ZC", "1")[:1] != "0" and _host_status_words(dev)[0] is not None:
-        n = _attempts_polled(lib, be, args, stream, max_attempts)
-    else:
-        n = _attempts_evented(launch, ws, rec, stream, side, stat, be, max_attempts)
+    lease = _host_status_words(dev) if os.environ.get("GENPOSE2_ODE_ZC", "1")[:1] != "0" else (None, None)
+    try:
+        if lease[0] is not None:
+            n = _attempts_polled(lib, be, args, stream, lease, max_attempts)
+        else:
+            n = _attempts_evented(launch, ws, rec, stream, side, stat, be, max_attempts)
+    finally:
+        # the device may still write the words (the speculative next control) until the stream drains
+        if lease[0] is not None:
+            stream.synchronize()
+        _release_status_words(dev, lease)
     last = ((n + 2) & 1) * rec
 
     ctl = OdeCtl.from_buffer_copy(bytes(ws[last:last + rec].cpu().numpy()))
