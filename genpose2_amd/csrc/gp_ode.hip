@@ -283,7 +283,39 @@ __global__ __launch_bounds__(1024) void ode_init_norms_kernel(const double* __re
 #pragma clang fp contract(off)
     __shared__ double r0[16], r1[16];
     double s0 = 0.0, s1 = 0.0;
-    for (long long i = threadIdx.x; i < n; i += 1024) {
+    // each thread's elements i = tid + 1024 j in increasing j, as one load per step would add them; the loads of
+    // IL consecutive steps are issued together (a load per dependent add waited a full memory round trip each:
+    // 76 -> 42 us per call at R = 12,800; the rest is the fp64 divisions of one workgroup)
+    constexpr int IL = 8;
+    long long i0 = threadIdx.x;
+    for (; i0 + 1024LL * (IL - 1) < n; i0 += 1024LL * IL) {
+        double yv[IL], fa[IL], fb[IL];
+#pragma unroll
+        for (int j = 0; j < IL; ++j) {
+            yv[j] = y0[i0 + 1024LL * j];
+            fa[j] = f0[i0 + 1024LL * j];
+        }
+        if (f1 != nullptr) {
+#pragma unroll
+            for (int j = 0; j < IL; ++j) fb[j] = f1[i0 + 1024LL * j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < IL; ++j) fb[j] = 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < IL; ++j) {
+            const double sc = atol + fabs(yv[j]) * rtol;
+            if (f1 == nullptr) {
+                const double u = yv[j] / sc, v = fa[j] / sc;
+                s0 += u * u;
+                s1 += v * v;
+            } else {
+                const double v = (fb[j] - fa[j]) / sc;
+                s0 += v * v;
+            }
+        }
+    }
+    for (long long i = i0; i < n; i += 1024) {
         const double sc = atol + fabs(y0[i]) * rtol;
         if (f1 == nullptr) {
             const double u = y0[i] / sc, v = f0[i] / sc;
@@ -359,7 +391,8 @@ __global__ __launch_bounds__(256) void ode_dense_kernel(OdeDenseArgs a) {
 
 // Final denoise (samplers.py:240-249) + epilogue: grad = score(float(x), eps) in fp32,
 // mean_x = x + (0 - g^2 grad) * c (fp32 product, fp64 sum), then GS of [:6], + pts_center, quaternion
-// (posenet_agent.py:554-556). Writes pose (R,9) fp64 and q (R,7) fp64.
+// (posenet_agent.py:554-556). Writes pose (R,9) fp64 and q (R,7) fp64. The score runs on the stage kernels'
+// trunk and tile (f16x3, 64 candidates per workgroup at R >= 8193; exact fp32 without the f16 planes).
 struct OdeDenoiseArgs {
     gp_head_weights w;
     const float* pobj;
@@ -374,35 +407,43 @@ struct OdeDenoiseArgs {
     int rows, kper;
 };
 
+template <int PL, int NT>   // PL 0: exact fp32 trunk, X3P: f16x3 (the stage kernels' arithmetic)
 __global__ __launch_bounds__(EVAL_WV * 64) void ode_denoise_kernel(OdeDenoiseArgs a) {
-    __shared__ HeadSmem<1, EVAL_WV> sm;
-    __shared__ int obj[16];
-    __shared__ double xm[16 * 9];
+    constexpr int ROWS = 16 * NT;
+    constexpr int NTH = EVAL_WV * 64;
+    __shared__ HeadSmem<NT, EVAL_WV, PL> sm;
+    __shared__ int obj[ROWS];
+    __shared__ double xm[ROWS * 9];
     const int tid = threadIdx.x;
-    const int r0 = blockIdx.x * 16;
-    stage_small_weights<1, EVAL_WV>(a.w, sm);
-    for (int i = tid; i < 256; i += EVAL_WV * 64) {
+    const int r0 = blockIdx.x * ROWS;
+    SplitScalars hs = {};
+    if constexpr (PL != 0) hs = load_split_scalars(a.w);
+    stage_small_weights<NT, EVAL_WV, 0, PL == 0>(a.w, sm);
+    for (int i = tid; i < ROWS * 16; i += NTH) {
         const int c = i >> 4, j = i & 15;
         const int r = r0 + c;
         sm.xin[i] = (r < a.rows && j < 9) ? (float)a.x[(size_t)r * 9 + j] : 0.f;
     }
-    if (tid < 16) {
+    if (tid < ROWS) {
         const int r = r0 + tid;
         obj[tid] = (r < a.rows ? r : a.rows - 1) / a.kper;
     }
-    head_trunk<1, EVAL_WV>(a.w, a.pobj, a.tproj, obj, sm);
-    if (tid < 144) {
+    if constexpr (PL != 0)
+        head_trunk_x3<NT, EVAL_WV>(a.w, a.pobj, a.tproj, obj, sm, 0, hs);
+    else
+        head_trunk<NT, EVAL_WV>(a.w, a.pobj, a.tproj, obj, sm);
+    for (int e9 = tid; e9 < ROWS * 9; e9 += NTH) {
 #pragma clang fp contract(off)
-        const int c = tid / 9, o = tid - c * 9;
+        const int c = e9 / 9, o = e9 - c * 9;
         const int r = r0 + c;
         if (r < a.rows) {
             const float grad = fdiv(head_out(sm, c, o), fadd(a.sigma, 1e-7f));
             const float drift = 0.0f - a.g2 * grad;
-            xm[tid] = a.x[(size_t)r * 9 + o] + (double)(drift * a.step);
+            xm[e9] = a.x[(size_t)r * 9 + o] + (double)(drift * a.step);
         }
     }
     __syncthreads();
-    if (tid < 16 && r0 + tid < a.rows) {
+    if (tid < ROWS && r0 + tid < a.rows) {
         const int r = r0 + tid;
         double v[9], qq[4];
 #pragma unroll
@@ -584,7 +625,17 @@ extern "C" int gp_ode_denoise(const gp_head_weights* w, const float* pobj, float
     a.q = q;
     a.rows = rows;
     a.kper = k;
-    hipLaunchKernelGGL(ode_denoise_kernel, dim3((rows + 15) / 16), dim3(EVAL_WV * 64), 0, stream, a);
+    // the stage kernels' trunk and tile (exact fp32 without the f16 planes)
+    const int nt = ode_nt(w, rows);
+    const dim3 grid((rows + 16 * nt - 1) / (16 * nt)), blk(EVAL_WV * 64);
+    if (!w->pe2_h)
+        hipLaunchKernelGGL((ode_denoise_kernel<0, 1>), grid, blk, 0, stream, a);
+    else if (nt == 4)
+        hipLaunchKernelGGL((ode_denoise_kernel<X3P, 4>), grid, blk, 0, stream, a);
+    else if (nt == 2)
+        hipLaunchKernelGGL((ode_denoise_kernel<X3P, 2>), grid, blk, 0, stream, a);
+    else
+        hipLaunchKernelGGL((ode_denoise_kernel<X3P, 1>), grid, blk, 0, stream, a);
     return gp_check_launch("ode_denoise_kernel");
 }
 
