@@ -52,6 +52,7 @@ class PoseNet:
         self.ode_host_control = False              # ODE: True runs the RK45 controller on the host
         self.ode_trace: Optional[list] = None      # ODE: a list receives [t, h, error norm] per step attempt
                                                    # (host controller)
+        self._denoise_scalars = {}                 # ODE: (eps, steps) -> the denoise step's scalars
         self.global_batch = None                   # shard.GlobalBatch: this call is one shard of a global-batch
                                                    # PC call (runner.ShardedEvaluationPipeline(global_batch=True))
         self._gen = torch.Generator(device=self.device)
@@ -290,11 +291,17 @@ class PoseNet:
                 raise IndexError("RK45 failed before collecting any t_eval point (res.y is empty)")
             x = ys[-1]
         self.last_nfev = nfev
-        # denoise with the PC predictor step (samplers.py:240-249), GS, + pts_center, quaternion
-        t32, sig, _ = time_scalars(eps)
-        vec_eps = torch.full((1,), eps, dtype=torch.float32)
-        g2 = float(sde.diffusion(vec_eps).to(torch.float32) ** 2)
-        step = float(np.float32((1 - eps) / (1000 if steps is None else steps)))
+        # denoise with the PC predictor step (samplers.py:240-249), GS, + pts_center, quaternion; its scalars depend
+        # on eps and the step count only (formed once: the torch CPU ops sat between the solve and the denoise)
+        key = (eps, steps)
+        sc = self._denoise_scalars.get(key)
+        if sc is None:
+            t32, sig, _ = time_scalars(eps)
+            vec_eps = torch.full((1,), eps, dtype=torch.float32)
+            g2 = float(sde.diffusion(vec_eps).to(torch.float32) ** 2)
+            step = float(np.float32((1 - eps) / (1000 if steps is None else steps)))
+            sc = self._denoise_scalars[key] = (t32, sig, g2, step)
+        t32, sig, g2, step = sc
         pose, q = self.heads.ode_denoise(pobj, t32, sig, g2, step, x, K, center, be.ws)
         in_process = None
         if want_process:
