@@ -170,6 +170,10 @@ class PoseNet:
         """posenet_agent.py:385-387: data["pts_feat"] (no rgb branch with dino 'none')."""
         data["pts_feat"] = self._encode(data)
         data["rgb_feat"] = None
+        if self.cfg.agent_type == "energy":
+            # get_energy(extract_feature=False)'s object projection formed here, on the encoder's stream
+            # (the runner runs it beside the score sampler), keyed by the feature tensor it came from
+            data["_energy_pobj"] = (data["pts_feat"], self.heads.object_proj(data["pts_feat"]))
 
     @staticmethod
     def per_object_energy_t(bs: int) -> torch.Tensor:
@@ -326,7 +330,8 @@ class PoseNet:
         R = bs * K
         feat = self._encode(data) if extract_feature else dev.require_device_tensor(data["pts_feat"], "pts_feat")
         self.pts_feature = True
-        pobj = self.heads.object_proj(feat)
+        pre = data.get("_energy_pobj") if not extract_feature else None
+        pobj = pre[1] if pre is not None and pre[0] is feat else self.heads.object_proj(feat)
         pose = pose_samples.to(self.device).reshape(R, -1).to(torch.float32).clone()
         center = dev.require_device_tensor(data["pts_center"], "pts_center")
         pose[:, -3:] -= center.unsqueeze(1).repeat(1, K, 1).view(R, -1)

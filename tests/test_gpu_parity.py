@@ -651,6 +651,28 @@ def test_energy_per_object_t_batched():
         assert rel(e[b:b + 1], eb.numpy()) < 1e-6
 
 
+def test_energy_after_encode_func_equals_extracting_call():
+    """encode_func forms the energy net's object projection with the features (the runner runs it beside the
+    score sampler); get_energy(extract_feature=False) on that dict equals the extracting call bit for bit, and
+    a replaced pts_feat is not paired with the stale projection."""
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    g = golden("pipeline")
+    e_agent = PoseNet(GenPoseConfig(device=DEV, agent_type="energy")).eval()
+    pts, center = torch.from_numpy(g["pts"]).to(DEV), torch.from_numpy(g["pts_center"]).to(DEV)
+    pose = torch.from_numpy(g["pred_pose"]).to(DEV)
+    e_ref = e_agent.get_energy({"pts": pts, "pts_center": center}, pose, T=1e-5, mode="test")
+    data = {"pts": pts, "pts_center": center}
+    e_agent.encode_func(data)
+    assert "_energy_pobj" in data
+    assert torch.equal(e_agent.get_energy(data, pose, T=1e-5, mode="test", extract_feature=False), e_ref)
+    data["pts_feat"] = data["pts_feat"].flip(0).contiguous()
+    e_flip = e_agent.get_energy(data, pose, T=1e-5, mode="test", extract_feature=False)
+    plain = {"pts_feat": data["pts_feat"], "pts_center": center}
+    assert torch.equal(e_flip, e_agent.get_energy(plain, pose, T=1e-5, mode="test", extract_feature=False))
+    assert not torch.equal(e_flip, e_ref)
+
+
 def test_runner_pipeline_smoke():
     from genpose2_amd import synthetic
     from genpose2_amd.config import GenPoseConfig
