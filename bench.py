@@ -574,6 +574,8 @@ def main():
                 energy.encode_func(edata)
             stream.wait_stream(side)
             edata["pts_feat"].record_stream(stream)
+            if "_energy_pobj" in edata:
+                edata["_energy_pobj"][1].record_stream(stream)
             e = energy.get_energy(edata, pose, T=1e-5, extract_feature=False)
             agg = aggregate.aggregate_pose(pose, e)
             if scale is not None:

@@ -115,6 +115,14 @@ _SIGS: Dict[str, tuple] = {
     "gp_ode_auto_attempt_hs": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_int, c_int, c_double, c_double, c_double,
                                     c_double, c_double, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p]),
+    "gp_ode_global_partials": (c_int, [c_int, c_int, c_int, c_int]),
+    "gp_ode_global_workspace_size": (c_size_t, [c_int]),
+    "gp_ode_auto_partials_offset": (c_size_t, []),
+    "gp_ode_auto_attempt_global": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_int, c_int, c_double, c_double,
+                                           c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                           c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
+                                           c_void_p]),
     "gp_pc_step_table": (c_int, [c_int, c_float, c_void_p]),
     "gp_ode_sample_workspace_size": (c_size_t, [c_int]),
     "gp_ode_sample": (c_int, [ctypes.POINTER(HeadWeights), c_void_p, c_void_p, c_int, c_int, c_double, c_double,
@@ -148,6 +156,7 @@ _lib = None
 
 # gp_pc_exchange_fn (genpose_hip.h): int (*)(void* ctx, int step, float* slot, int n, hipStream_t stream)
 PC_EXCHANGE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, c_void_p, c_int, c_void_p)
+ODE_EXCHANGE_FN = PC_EXCHANGE_FN   # gp_ode_exchange_fn: the same C signature with an fp64 partials pointer
 
 
 def load(path: str = LIB_PATH):

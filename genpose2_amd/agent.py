@@ -17,7 +17,7 @@ import torch
 
 from . import aggregate, arch, device as dev, sde, weights
 from .config import GenPoseConfig
-from .ode import DeviceRk45, rk45_device, rk45_drive, time_scalars
+from .ode import DeviceRk45, GlobalDeviceRk45, rk45_device, rk45_drive, time_scalars
 
 
 def _as_config(cfg) -> GenPoseConfig:
@@ -54,7 +54,7 @@ class PoseNet:
                                                    # (host controller)
         self._denoise_scalars = {}                 # ODE: (eps, steps) -> the denoise step's scalars
         self.global_batch = None                   # shard.GlobalBatch: this call is one shard of a global-batch
-                                                   # PC call (runner.ShardedEvaluationPipeline(global_batch=True))
+                                                   # PC / ODE call (runner.ShardedEvaluationPipeline(global_batch=True))
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(self.cfg.noise_seed)
         self.weights_source = f"synthetic(seed={self.cfg.seed})"
@@ -245,9 +245,6 @@ class PoseNet:
             pred_q = q.view(bs, K, -1)
             in_process = xs.view(bs, K, T, -1) if xs is not None else None
         elif mode == "ode":
-            if self.global_batch is not None:
-                raise NotImplementedError("global-batch sampling is built for the PC sampler; the ODE sampler runs "
-                                          "per shard")
             pred_pose, pred_q, in_process = self._ode(pobj, center, bs, K, rep_init, T0,
                                                       bool(return_process or self.cfg.save_video))
         else:
@@ -272,28 +269,47 @@ class PoseNet:
         T0 = arch.SDE_T if T0 is None else float(T0)
         eps = arch.SAMPLING_EPS
         steps = self.cfg.sampling_steps
-        x0 = self._draw_prior(R) * sde.prior_sigma(T0)
+        gb = self.global_batch
+        if gb is None:
+            x0 = self._draw_prior(R) * sde.prior_sigma(T0)
+        else:   # this shard's rows of the whole batch's prior draw
+            if want_process or self.ode_host_control or self.ode_trace is not None:
+                raise NotImplementedError("global-batch ODE sampling runs the device step controller only "
+                                          "(no return_process / save_video, host control or trace)")
+            if self.noise_feed is not None:
+                raise ValueError("global-batch sampling draws the prior itself (noise_feed not supported)")
+            x0 = self._draw_prior(gb.total * K)[gb.lo * K:gb.hi * K] * sde.prior_sigma(T0)
         if rep_init is not None:
             x0 = rep_init.to(torch.float32) + x0
-        be = DeviceRk45(self.heads, pobj, x0.to(self.device), K)
         t_eval = None if steps is None else np.linspace(T0, eps, steps)
-        if want_process or self.ode_host_control or self.ode_trace is not None:
-            # every solve_ivp output is kept: host-side controller, one error norm read per attempt
-            _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process, trace=self.ode_trace)
-        else:
-            # default: the step controller runs on the device (no host round trip per attempt)
+        if gb is not None:
+            # one solve on the whole batch: the error norms over every shard's rows (GlobalDeviceRk45)
+            be = GlobalDeviceRk45(self.heads, pobj, x0.to(self.device), K, gb)
             x, nfev, status = rk45_device(be, T0, eps, t_eval=t_eval)
-        if status < 0 and t_eval is not None and not want_process:
-            # failed solve (step below spacing): solve_ivp returns the t_eval points collected so far and
-            # cond_ode_sampler continues from res.y[:, -1]; only the host restatement keeps them all
+            if status < 0 and t_eval is not None:
+                raise RuntimeError("global-batch RK45 failed (step size below the spacing of t) with t_eval set: the "
+                                   "t_eval outputs collected before the failure need the host controller")
+        else:
             be = DeviceRk45(self.heads, pobj, x0.to(self.device), K)
-            _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=True)
-            want_process = False
-        if want_process or self.ode_host_control or self.ode_trace is not None or (status < 0 and t_eval is not None):
-            ys = be.outputs()                  # (n_t or 1, R*9) fp64
-            if ys.shape[0] == 0:               # res.y[:, -1] of an empty solve_ivp result
-                raise IndexError("RK45 failed before collecting any t_eval point (res.y is empty)")
-            x = ys[-1]
+            if want_process or self.ode_host_control or self.ode_trace is not None:
+                # every solve_ivp output is kept: host-side controller, one error norm read per attempt
+                _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=want_process,
+                                             trace=self.ode_trace)
+            else:
+                # default: the step controller runs on the device (no host round trip per attempt)
+                x, nfev, status = rk45_device(be, T0, eps, t_eval=t_eval)
+            if status < 0 and t_eval is not None and not want_process:
+                # failed solve (step below spacing): solve_ivp returns the t_eval points collected so far and
+                # cond_ode_sampler continues from res.y[:, -1]; only the host restatement keeps them all
+                be = DeviceRk45(self.heads, pobj, x0.to(self.device), K)
+                _, nfev, status = rk45_drive(be, T0, eps, t_eval=t_eval, keep_all=True)
+                want_process = False
+            if (want_process or self.ode_host_control or self.ode_trace is not None
+                    or (status < 0 and t_eval is not None)):
+                ys = be.outputs()                  # (n_t or 1, R*9) fp64
+                if ys.shape[0] == 0:               # res.y[:, -1] of an empty solve_ivp result
+                    raise IndexError("RK45 failed before collecting any t_eval point (res.y is empty)")
+                x = ys[-1]
         self.last_nfev = nfev
         # denoise with the PC predictor step (samplers.py:240-249), GS, + pts_center, quaternion; its scalars depend
         # on eps and the step count only (formed once: the torch CPU ops sat between the solve and the denoise)

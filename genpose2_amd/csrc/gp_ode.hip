@@ -57,6 +57,8 @@ struct OdeStageArgs {
     double e[ODE_NK];            // error weights over K_0..K_6 (K_6 = this stage)
     double rtol, atol;
     double* part;                // (nwg) sum over the workgroup's elements of (err/scale)^2
+    int part_off;                // index of this launch's first partial (global-batch shards: the single call's
+                                 // workgroup index of this shard's first row tile; 0 otherwise)
     int rows, kper;
     // device-controlled attempts: state, time rows and buffers resolved from ctl
     const OdeCtl* ctl;           // null for host-controlled calls
@@ -142,7 +144,7 @@ __device__ __forceinline__ void ode_stage_body(const OdeStageArgs& a, const doub
         if (tid == 0) {
             double t = 0.0;
             for (int v = 0; v < EVAL_WV; ++v) t += esq[v];
-            a.part[blockIdx.x] = t;
+            a.part[a.part_off + blockIdx.x] = t;
         }
     }
 }
@@ -765,21 +767,39 @@ extern "C" size_t gp_ode_auto_workspace_size(int rows) {
     return auto_part_off() + sizeof(double) * (((size_t)rows + 15) / 16) + 256;
 }
 
+// A global-batch shard of one RK45 solve on the whole batch: the tiling of the single call (nt from rows_total), this
+// shard's partials at part_off of part_n, the error norm over every shard's partials and rows_total * 9 elements,
+// and after each attempt an exchange that brings every shard's partials to every rank before the next control.
+struct OdeGlobal {
+    int rows_total, part_n, part_off;
+    gp_ode_exchange_fn exchange;
+    void* ctx;
+};
+
+static size_t ode_auto_ws_bytes(int part_n) { return auto_part_off() + sizeof(double) * (size_t)part_n + 256; }
+
 static int ode_auto_attempt_impl(const gp_head_weights* w, const float* pobj, int n, int what, double t_bound,
                                  double direction, double rtol, double atol, double sig_min, double base,
                                  double diff_scale, double* y0, double* y1, double* const* kslots,
                                  const double* tableau_a, const double* b, const double* e, int rows, int k,
-                                 void* workspace, size_t workspace_bytes, int* hstat, hipStream_t stream) {
+                                 const OdeGlobal* g, void* workspace, size_t workspace_bytes, int* hstat,
+                                 hipStream_t stream) {
     GP_REQUIRE(w && pobj && y0 && y1 && kslots && tableau_a && b && e && workspace && rows >= 1 && k >= 1 && n >= 0,
                "ode_auto_attempt: bad arguments");
-    GP_REQUIRE(workspace_bytes >= gp_ode_auto_workspace_size(rows), "ode_auto_attempt: workspace too small");
     for (int j = 0; j < ODE_NK; ++j) GP_REQUIRE(kslots[j] != nullptr, "ode_auto_attempt: null K slot");
     char* ws = static_cast<char*>(workspace);
     OdeCtl* ctl = reinterpret_cast<OdeCtl*>(ws);
     float* tproj6 = reinterpret_cast<float*>(ws + auto_tproj_off());
     double* part = reinterpret_cast<double*>(ws + auto_part_off());
-    const int nwg = ode_nwg(w, rows), nt = ode_nt(w, rows);
-    OdeConsts kc = {t_bound, direction, rtol, atol, sig_min, base, diff_scale, (double)rows * 9.0, nwg};
+    const int nt = ode_nt(w, g ? g->rows_total : rows);
+    const int nwg = (rows + 16 * nt - 1) / (16 * nt);   // this call's workgroups
+    const int part_n = g ? g->part_n : nwg;
+    GP_REQUIRE(!g || (g->part_off >= 0 && g->part_off + nwg <= part_n),
+               "ode_auto_attempt: shard partials [%d, %d) outside %d", g ? g->part_off : 0, g ? g->part_off + nwg : 0,
+               part_n);
+    GP_REQUIRE(workspace_bytes >= ode_auto_ws_bytes(part_n), "ode_auto_attempt: workspace too small");
+    OdeConsts kc = {t_bound, direction, rtol, atol, sig_min, base, diff_scale,
+                    (double)(g ? g->rows_total : rows) * 9.0, part_n};
     OdeCtl* cin = ctl + (n & 1);
     OdeCtl* cout = ctl + ((n + 1) & 1);
     GP_REQUIRE(what >= 1 && what <= 3, "ode_auto_attempt: what must be 1 (control), 2 (stages) or 3 (both)");
@@ -794,6 +814,7 @@ static int ode_auto_attempt_impl(const gp_head_weights* w, const float* pobj, in
     a.pobj = pobj;
     a.rows = rows;
     a.kper = k;
+    a.part_off = g ? g->part_off : 0;
     a.rtol = rtol;
     a.atol = atol;
     a.ctl = cout;
@@ -816,7 +837,11 @@ static int ode_auto_attempt_impl(const gp_head_weights* w, const float* pobj, in
             hipLaunchKernelGGL((ode_attempt_kernel<X3P, 2>), grid, blk, 0, stream, a, tb);
         else
             hipLaunchKernelGGL((ode_attempt_kernel<X3P, 1>), grid, blk, 0, stream, a, tb);
-        return gp_check_launch("ode_attempt_kernel");
+        const int rc = gp_check_launch("ode_attempt_kernel");
+        if (rc || !g) return rc;
+        GP_REQUIRE(g->exchange(g->ctx, n, part, part_n, stream) == 0, "ode_auto_attempt: partials exchange of attempt %d",
+                   n);
+        return GP_OK;
     }
     for (int s = 1; s < 6; ++s) {
         a.stage = s;
@@ -830,7 +855,10 @@ static int ode_auto_attempt_impl(const gp_head_weights* w, const float* pobj, in
     for (int j = 0; j < ODE_NK; ++j) a.e[j] = e[j];
     a.part = part;
     ode_launch_stage<1>(a, nt, stream);
-    return gp_check_launch("ode_stage_kernel<auto>");
+    const int rc = gp_check_launch("ode_stage_kernel<auto>");
+    if (rc || !g) return rc;
+    GP_REQUIRE(g->exchange(g->ctx, n, part, part_n, stream) == 0, "ode_auto_attempt: partials exchange of attempt %d", n);
+    return GP_OK;
 }
 
 extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, int n, int what,
@@ -840,7 +868,7 @@ extern "C" int gp_ode_auto_attempt(const gp_head_weights* w, const float* pobj, 
                                    const double* e, int rows, int k, void* workspace, size_t workspace_bytes,
                                    hipStream_t stream) {
     return ode_auto_attempt_impl(w, pobj, n, what, t_bound, direction, rtol, atol, sig_min, base, diff_scale, y0, y1,
-                                 kslots, tableau_a, b, e, rows, k, workspace, workspace_bytes, nullptr, stream);
+                                 kslots, tableau_a, b, e, rows, k, nullptr, workspace, workspace_bytes, nullptr, stream);
 }
 
 extern "C" int gp_ode_auto_attempt_hs(const gp_head_weights* w, const float* pobj, int n, int what,
@@ -851,7 +879,38 @@ extern "C" int gp_ode_auto_attempt_hs(const gp_head_weights* w, const float* pob
                                       int* host_status, hipStream_t stream) {
     GP_REQUIRE(host_status != nullptr, "ode_auto_attempt_hs: null status words");
     return ode_auto_attempt_impl(w, pobj, n, what, t_bound, direction, rtol, atol, sig_min, base, diff_scale, y0, y1,
-                                 kslots, tableau_a, b, e, rows, k, workspace, workspace_bytes, host_status, stream);
+                                 kslots, tableau_a, b, e, rows, k, nullptr, workspace, workspace_bytes, host_status,
+                                 stream);
+}
+
+extern "C" int gp_ode_global_partials(int rows_total, int shard_rows_max, int shards, int split) {
+    if (rows_total < 1 || shard_rows_max < 1 || shards < 1) return 0;
+    const int tile = 16 * head_pick_nt(rows_total, split != 0);
+    return shards * ((shard_rows_max + tile - 1) / tile);
+}
+
+extern "C" size_t gp_ode_global_workspace_size(int part_n) { return part_n >= 1 ? ode_auto_ws_bytes(part_n) : 0; }
+
+extern "C" size_t gp_ode_auto_partials_offset(void) { return auto_part_off(); }
+
+extern "C" int gp_ode_auto_attempt_global(const gp_head_weights* w, const float* pobj, int n, int what,
+                                          double t_bound, double direction, double rtol, double atol, double sig_min,
+                                          double base, double diff_scale, double* y0, double* y1,
+                                          double* const* kslots, const double* tableau_a, const double* b,
+                                          const double* e, int rows, int k, int rows_total, int row_off, int shard,
+                                          int shards, int shard_rows_max, gp_ode_exchange_fn exchange, void* ctx,
+                                          void* workspace, size_t workspace_bytes, int* host_status,
+                                          hipStream_t stream) {
+    GP_REQUIRE(w && exchange, "ode_auto_attempt_global: null pointer");
+    GP_REQUIRE(shards >= 1 && shard >= 0 && shard < shards && rows >= 1 && rows <= shard_rows_max && row_off >= 0 &&
+                   row_off + rows <= rows_total,
+               "ode_auto_attempt_global: shard %d of %d, rows [%d, %d) of %d (at most %d per shard)", shard, shards,
+               row_off, row_off + rows, rows_total, shard_rows_max);
+    const int tile = 16 * ode_nt(w, rows_total);
+    const int per = (shard_rows_max + tile - 1) / tile;
+    OdeGlobal g = {rows_total, shards * per, shard * per, exchange, ctx};
+    return ode_auto_attempt_impl(w, pobj, n, what, t_bound, direction, rtol, atol, sig_min, base, diff_scale, y0, y1,
+                                 kslots, tableau_a, b, e, rows, k, &g, workspace, workspace_bytes, host_status, stream);
 }
 
 // ============================================================================ whole sampler (C hosts)

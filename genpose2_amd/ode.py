@@ -394,6 +394,50 @@ class DeviceRk45:
         return torch.stack(self.ys, 0)
 
 
+class GlobalDeviceRk45(DeviceRk45):
+    """DeviceRk45 for one shard of a global-batch solve (shard.GlobalBatch ``gb``: this rank holds the rows of
+    objects [gb.lo, gb.hi), K each, of one solve_ivp call on the whole batch). select_initial_step's norms are
+    taken over the WHOLE batch's y0, f0 and f1 (each shard's rows all-gathered: the same vectors and the same
+    summation order as one call), and rk45_device drives the attempts through gp_ode_auto_attempt_global (the
+    error norm over every shard's partials)."""
+
+    def __init__(self, heads, pobj: torch.Tensor, y0: torch.Tensor, k: int, gb, rtol: float = 1e-5,
+                 atol: float = 1e-5):
+        super().__init__(heads, pobj, y0, k, rtol, atol)
+        if self.R != (gb.hi - gb.lo) * self.k:
+            raise ValueError(f"global-batch shard: {self.R} rows for objects [{gb.lo}, {gb.hi}) x {self.k}")
+        self.gb = gb
+        self.n_total = gb.total * self.k * arch.POSE_DIM
+        self._y_full = self._f0_full = None
+
+    def _full(self, v: torch.Tensor) -> torch.Tensor:
+        from . import shard
+        return shard.gather_shard_rows(v.view(self.R, arch.POSE_DIM), self.gb, self.k).reshape(-1).contiguous()
+
+    def set_t_eval(self, t_eval, direction, keep_all):
+        raise NotImplementedError("global-batch RK45 keeps only the final output (rk45_device)")
+
+    def init_norms(self):
+        self._y_full, self._f0_full = self._full(self.y), self._full(self.K[0])
+        check(self.lib.gp_ode_init_norms(ctypes.c_void_p(self._y_full.data_ptr()),
+                                         ctypes.c_void_p(self._f0_full.data_ptr()), None, self.n_total, self.atol,
+                                         self.rtol, ctypes.c_void_p(self.scal.data_ptr()), self._s()), "ode_init_norms")
+        v = self.scal[:2].cpu().numpy()
+        return v[0], v[1]
+
+    def diff_norm(self):
+        f1 = self._full(self.f1)
+        check(self.lib.gp_ode_init_norms(ctypes.c_void_p(self._y_full.data_ptr()),
+                                         ctypes.c_void_p(self._f0_full.data_ptr()), ctypes.c_void_p(f1.data_ptr()),
+                                         self.n_total, self.atol, self.rtol, ctypes.c_void_p(self.scal.data_ptr()),
+                                         self._s()), "ode_init_norms")
+        self._y_full = self._f0_full = None
+        return self.scal[2:3].cpu().numpy()[0]
+
+    def attempt(self, t, h):
+        raise NotImplementedError("global-batch RK45 runs the device controller (rk45_device)")
+
+
 # ============================================================================ device-controlled driver
 class OdeCtl(ctypes.Structure):
     """Host mirror of the device controller record (gp_ode.hip OdeCtl)."""
@@ -485,7 +529,7 @@ def _release_status_words(dev, lease) -> None:
             _HSTAT_FREE.setdefault(dev, []).append(lease)
 
 
-def _attempts_polled(lib, be, args, stream, lease, max_attempts: int, timeout_s: float = 60.0) -> int:
+def _attempts_polled(call, be, stream, lease, max_attempts: int, timeout_s: float = 60.0) -> int:
     """The attempt loop with nothing between a control launch and its stage launch: the control kernel of
     attempt n writes 4 n + (status + 1) into word n & 3 of a host-mapped pinned buffer (gp_ode_auto_attempt_hs),
     and the host, one attempt ahead, polls that word. Same launches, same order, same bits as the evented loop."""
@@ -493,11 +537,9 @@ def _attempts_polled(lib, be, args, stream, lease, max_attempts: int, timeout_s:
     hv = h.numpy()
     hv[:] = -1
     hp = ctypes.c_void_p(hdev)
-    w, pobj = ctypes.byref(be.h.w), ctypes.c_void_p(be.pobj.data_ptr())
-    a = args[:-1]
 
     def launch(n, what):
-        check(lib.gp_ode_auto_attempt_hs(w, pobj, n, what, *a, hp, args[-1]), "ode_auto_attempt")
+        call(n, what, hp)
 
     timing = STAGE_EVENTS is not None
 
@@ -552,7 +594,22 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
             raise ValueError("Values in `t_eval` are not within `t_span`.")
     h_abs, nfev = initial_step(be, t0, tf, direction)
     dev = be.dev
-    ws = torch.empty(int(lib.gp_ode_auto_workspace_size(be.R)), dtype=torch.uint8, device=dev)
+    gb = be.gb if isinstance(be, GlobalDeviceRk45) else None
+    ex = None
+    nbytes = int(lib.gp_ode_auto_workspace_size(be.R))
+    if gb is not None:
+        from .shard import PartialsExchange
+        rows_total, rows_max = gb.total * be.k, gb.per_max * be.k
+        part_n = int(lib.gp_ode_global_partials(rows_total, rows_max, gb.world, int(be.h.w.pe2_h is not None)))
+        nbytes = max(nbytes, int(lib.gp_ode_global_workspace_size(part_n)))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    if gb is not None:
+        # every shard's partials, zero where a short last shard has no workgroup (their sum's fixed order is the
+        # single call's)
+        off = int(lib.gp_ode_auto_partials_offset())
+        part = ws[off:off + 8 * part_n].view(torch.float64)
+        part.zero_()
+        ex = PartialsExchange(part, part_n, gb)
     rec = ctypes.sizeof(OdeCtl)
     c0 = OdeCtl(t=t0, h_abs=float(h_abs), nfev=nfev)
     c0.kidx[:] = list(range(N_STAGES + 1))
@@ -568,14 +625,27 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
             _E7.ctypes.data_as(ctypes.c_void_p), be.R, be.k, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
             ctypes.c_void_p(stream.cuda_stream))
 
+    w, pobj = ctypes.byref(be.h.w), ctypes.c_void_p(be.pobj.data_ptr())
+
+    def call(n, what, hp):
+        if ex is not None:
+            rc = lib.gp_ode_auto_attempt_global(w, pobj, n, what, *args[:15], rows_total, gb.lo * be.k, gb.rank,
+                                                gb.world, rows_max, ex.fn, None, *args[15:17], hp, args[17])
+            if ex.error is not None:
+                raise RuntimeError("ode_auto_attempt_global: partials exchange failed") from ex.error
+            check(rc, "ode_auto_attempt_global")
+        elif hp is not None:
+            check(lib.gp_ode_auto_attempt_hs(w, pobj, n, what, *args[:-1], hp, args[-1]), "ode_auto_attempt")
+        else:
+            check(lib.gp_ode_auto_attempt(w, pobj, n, what, *args), "ode_auto_attempt")
+
     def launch(n, what):
-        check(lib.gp_ode_auto_attempt(ctypes.byref(be.h.w), ctypes.c_void_p(be.pobj.data_ptr()), n, what, *args),
-              "ode_auto_attempt")
+        call(n, what, None)
 
     lease = _host_status_words(dev) if os.environ.get("GENPOSE2_ODE_ZC", "1")[:1] != "0" else (None, None)
     try:
         if lease[0] is not None:
-            n = _attempts_polled(lib, be, args, stream, lease, max_attempts)
+            n = _attempts_polled(call, be, stream, lease, max_attempts)
         else:
             n = _attempts_evented(launch, ws, rec, stream, side, stat, be, max_attempts)
     finally:

@@ -82,6 +82,8 @@ class EvaluationPipeline:
         if self.energy_agent is not None:
             main.wait_stream(self._side)
             edata["pts_feat"].record_stream(main)
+            if "_energy_pobj" in edata:
+                edata["_energy_pobj"][1].record_stream(main)
             out.energy = self.energy_agent.get_energy(data=edata, pose_samples=pred_pose, T=1e-5, mode="test",
                                                       extract_feature=False)
         energy = out.energy if out.energy is not None else torch.ones(*pred_pose.shape[:2], 2,
@@ -107,9 +109,11 @@ class ShardedEvaluationPipeline:
     batch on every rank, processes the rank's contiguous object block (shard.shard_range) with no
     collective on the sampling path -- each shard is a reference call on its sub-batch -- and gathers
     pred_pose, pts_feat, energy, aggregated and length back in object order on every rank (dst=None)
-    or on ``dst`` only. ``global_batch=True`` (PC sampler) makes the shards one reference call on the
-    whole batch instead: the Langevin grad_norm over every shard's rows (one all-gather of the score-norm
-    partials per step, shard.GlobalBatch) and the prior and device noise drawn for the whole batch."""
+    or on ``dst`` only. ``global_batch=True`` makes the shards one reference call on the whole batch instead
+    (shard.GlobalBatch): the PC sampler's Langevin grad_norm over every shard's rows (one all-gather of the
+    score-norm partials per step) with the prior and device noise drawn for the whole batch; the ODE sampler's
+    select_initial_step norms over the whole batch's state (three one-time all-gathers) and every RK45
+    attempt's error norm over every shard's partials (one all-gather per attempt)."""
 
     def __init__(self, cfg: GenPoseConfig, with_energy: bool = True, with_scale: bool = False, src: int = 0,
                  global_batch: bool = False):

@@ -54,39 +54,74 @@ class GlobalBatch:
 
 
 class PartialsExchange:
-    """gp_pc_sample_global's exchange callback over ``part`` (2 slots of ``n`` floats, ``n / world`` per
-    shard): after each scoring launch, every shard's chunk of the slot the launch wrote reaches every rank
-    before the next launch reads it. RCCL: an all-gather enqueued behind the launch on the current stream
-    (torch orders the next launch after it). gloo: through host copies (tests)."""
+    """The exchange callback of gp_pc_sample_global (``part``: 2 slots of ``n`` fp32 partials, slot
+    ``step & 1``) and of gp_ode_auto_attempt_global (``part``: one slot of ``n`` fp64 partials), ``n / world``
+    entries per shard: after each scoring launch (PC step, RK45 attempt), every shard's chunk of the slot the
+    launch wrote reaches every rank before the next launch reads it. RCCL: an all-gather enqueued behind the
+    launch on the current stream (torch orders the next launch after it). gloo: through host copies (tests)."""
 
     def __init__(self, part: torch.Tensor, n: int, gb: GlobalBatch):
         import torch.distributed as dist
         from . import _lib
         self.part, self.n, self.gb = part, n, gb
+        self.slots = part.numel() // n
+        if self.slots not in (1, 2) or part.numel() != self.slots * n or n % gb.world:
+            raise ValueError(f"partials exchange: {part.numel()} entries for slots of {n} over {gb.world} shards")
         self.per = n // gb.world
         self.nccl = dist.get_backend(gb.group) == "nccl"
-        self.chunk = torch.empty(self.per, dtype=torch.float32, device=part.device)
+        self.chunk = torch.empty(self.per, dtype=part.dtype, device=part.device)
         self.error: Optional[BaseException] = None
         self.fn = _lib.PC_EXCHANGE_FN(self._call)   # kept alive with the object
+
+    def slot(self, step: int) -> torch.Tensor:
+        base = (step & 1) * self.n if self.slots == 2 else 0
+        return self.part[base:base + self.n]
 
     def _call(self, ctx, step, slot_ptr, n, stream) -> int:
         import torch.distributed as dist
         try:
-            base = (step & 1) * self.n
-            slot = self.part[base:base + self.n]
+            slot = self.slot(step)
             assert n == self.n and slot_ptr == slot.data_ptr(), "exchange: unexpected partials slot"
             mine = slot[self.gb.rank * self.per:(self.gb.rank + 1) * self.per]
             if self.nccl:
                 self.chunk.copy_(mine)
                 dist.all_gather_into_tensor(slot, self.chunk, group=self.gb.group)
             else:
-                got = [torch.empty(self.per, dtype=torch.float32) for _ in range(self.gb.world)]
+                got = [torch.empty(self.per, dtype=slot.dtype) for _ in range(self.gb.world)]
                 dist.all_gather(got, mine.cpu(), group=self.gb.group)
                 slot.copy_(torch.cat(got).to(slot.device))
             return 0
         except BaseException as e:   # noqa: BLE001 -- reported through the C return code, re-raised by the caller
             self.error = e
             return -1
+
+
+def gather_shard_rows(local: torch.Tensor, gb: GlobalBatch, k: int) -> torch.Tensor:
+    """The whole batch's (total * k, ...) rows from every rank's (hi - lo) * k rows of ``local``, in object
+    order, on local's device: an all-gather of per_max-object chunks (the last shard zero-padded), then the
+    padding dropped. RCCL on device tensors; gloo through host copies."""
+    import torch.distributed as dist
+    rows = (gb.hi - gb.lo) * k
+    if local.shape[0] != rows:
+        raise ValueError(f"gather_shard_rows: {local.shape[0]} rows for objects [{gb.lo}, {gb.hi}) x {k}")
+    per = gb.per_max * k
+    tail = tuple(local.shape[1:])
+    nccl = dist.get_backend(gb.group) == "nccl"
+    buf = torch.zeros((per,) + tail, dtype=local.dtype, device=local.device if nccl else "cpu")
+    buf[:rows].copy_(local)
+    if nccl:
+        full = torch.empty((gb.world * per,) + tail, dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(full, buf, group=gb.group)
+        chunks = full.view((gb.world, per) + tail)
+    else:
+        got = [torch.empty_like(buf) for _ in range(gb.world)]
+        dist.all_gather(got, buf, group=gb.group)
+        chunks = torch.stack(got)
+    parts = []
+    for r in range(gb.world):
+        lo, hi = shard_range(gb.total, gb.world, r)
+        parts.append(chunks[r, :(hi - lo) * k])
+    return torch.cat(parts).to(local.device)
 
 
 def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0) -> None:

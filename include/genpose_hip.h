@@ -353,6 +353,33 @@ int gp_ode_auto_attempt_hs(const gp_head_weights *w, const float *pobj, int n, i
                            double *const *kslots, const double *tableau_a, const double *b,
                            const double *e, int rows, int k, void *workspace, size_t workspace_bytes,
                            int *host_status, hipStream_t stream);
+/* Global-batch RK45 over shards (SURVEY 8e's optional mode for the ODE; replaces nothing in the reference,
+ * whose single solve_ivp call (samplers.py:226-234) takes one error norm over the whole batch's state per
+ * attempt). Each shard integrates its contiguous rows [row_off, row_off + rows) of rows_total with the
+ * tiling of one call on rows_total rows: its workgroups' error partials go to entries
+ * [shard * per, shard * per + nwg) of the workspace's gp_ode_global_partials(...) partials (per = that
+ * count / shards), and after each attempt's stage launch `exchange(ctx, attempt, part, n, stream)` must
+ * make all n entries hold every shard's partials (an all-gather of `per`-entry fp64 chunks enqueued on
+ * `stream`) before the next control kernel sums them in the fixed order over rows_total * 9 elements.
+ * Every rank then takes the same accept / reject decisions. The caller runs select_initial_step on the
+ * WHOLE batch's y0, f0 and f1 (gp_ode_init_norms over all rows_total rows, e.g. after all-gathering the
+ * shards' vectors). With every shard but the last holding shard_rows_max rows, a multiple of the tile, the
+ * result equals one solve on the whole batch bit for bit. Workspace: gp_ode_global_workspace_size(n)
+ * bytes; host_status as gp_ode_auto_attempt_hs, or NULL. */
+typedef int (*gp_ode_exchange_fn)(void *ctx, int attempt, double *part, int n, hipStream_t stream);
+int gp_ode_global_partials(int rows_total, int shard_rows_max, int shards, int split);
+size_t gp_ode_global_workspace_size(int part_n);
+/* Byte offset of the error partials (fp64) in a device-controlled workspace: a global-batch host zero-fills
+ * the gp_ode_global_partials(...) entries there before the first attempt and all-gathers them in exchange. */
+size_t gp_ode_auto_partials_offset(void);
+int gp_ode_auto_attempt_global(const gp_head_weights *w, const float *pobj, int n, int what,
+                               double t_bound, double direction, double rtol, double atol,
+                               double sig_min, double base, double diff_scale, double *y0, double *y1,
+                               double *const *kslots, const double *tableau_a, const double *b,
+                               const double *e, int rows, int k, int rows_total, int row_off, int shard,
+                               int shards, int shard_rows_max, gp_ode_exchange_fn exchange, void *ctx,
+                               void *workspace, size_t workspace_bytes, int *host_status,
+                               hipStream_t stream);
 /* The whole ODE sampler in one call (cond_ode_sampler, samplers.py:180-258, with scipy solve_ivp
  * RK45, samplers.py:226-234) for hosts without Python: x0 (R,9) fp32 device = the prior sample
  * [+ init_x] at T0; select_initial_step on the host from two RHS norms, then device-controlled

@@ -762,6 +762,23 @@ def _exchange_worker(rank, world, port, out_dir, per):
             want = torch.cat([torch.arange(per, dtype=torch.float32) + 100 * r + step for r in range(world)])
             assert torch.equal(part[base:base + n], want)
         assert ex._call(None, 0, part.data_ptr() + 4, n, None) == -1 and ex.error is not None   # wrong slot
+        # the ODE's form: one slot of fp64 partials, exchanged after every attempt
+        p64 = torch.full((n,), -1.0, dtype=torch.float64)
+        ex64 = shard.PartialsExchange(p64, n, gb)
+        for attempt in range(3):
+            p64[rank * per:(rank + 1) * per] = torch.arange(per, dtype=torch.float64) / 3 + 100 * rank + attempt
+            assert ex64._call(None, attempt, p64.data_ptr(), n, None) == 0, ex64.error
+            want = torch.cat([torch.arange(per, dtype=torch.float64) / 3 + 100 * r + attempt for r in range(world)])
+            assert torch.equal(p64, want)
+        with pytest.raises(ValueError):
+            shard.PartialsExchange(torch.zeros(3 * n), n, gb)
+        # the whole batch's rows from uneven shards (7 objects x 4 rows over `world` ranks), in object order
+        gb7 = shard.GlobalBatch.of(7)
+        full = torch.arange(7 * 4 * 9, dtype=torch.float64).view(7 * 4, 9) * 0.5
+        got = shard.gather_shard_rows(full[gb7.lo * 4:gb7.hi * 4].clone(), gb7, 4)
+        assert torch.equal(got, full)
+        with pytest.raises(ValueError):
+            shard.gather_shard_rows(full[:3], gb7, 4)
         np.save(os.path.join(out_dir, f"ok_{rank}.npy"), np.array(True))
     finally:
         dist.destroy_process_group()
@@ -769,9 +786,11 @@ def _exchange_worker(rank, world, port, out_dir, per):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_global_batch_partials_exchange_gloo(tmp_path, world):
-    """Global-batch PC sampling's host side (shard.GlobalBatch, shard.PartialsExchange) over gloo: every
-    rank's chunk of the slot a scoring launch wrote reaches every rank in shard order, and an unexpected
-    slot pointer is reported as a failure (the C caller turns it into an error) instead of raising into C."""
+    """Global-batch sampling's host side (shard.GlobalBatch, shard.PartialsExchange, shard.gather_shard_rows)
+    over gloo: every rank's chunk of the slot a scoring launch (PC: two fp32 slots) or an RK45 attempt (ODE:
+    one fp64 slot) wrote reaches every rank in shard order, an unexpected slot pointer is reported as a failure
+    (the C caller turns it into an error) instead of raising into C, and the ODE's initial-step vectors are
+    gathered from uneven shards in object order."""
     import torch.multiprocessing as mp
     port = 29700 + (os.getpid() + world) % 1000
     mp.spawn(_exchange_worker, args=(world, port, str(tmp_path), 5), nprocs=world, join=True)

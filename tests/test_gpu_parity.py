@@ -5,6 +5,8 @@ Tolerances (written here, per north_star): indices bit-exact; fp32 features/scor
 relative to max |t| (1e-4 for the ODE T0=1 case, whose adaptive step controller may take a
 different accept/reject path, see tests/test_oracle_golden.py).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -960,3 +962,37 @@ def test_pred_func_with_precomputed_features():
     assert torch.equal(got, ref)
     with pytest.raises(Exception):
         agent.pred_func(dict(data), repeat_num=8, extract_feature=False)   # no pts_feat given
+
+
+def test_global_batch_ode_one_rank_equals_plain_and_exchange_failure(monkeypatch):
+    """The global-batch ODE path (GlobalDeviceRk45, gp_ode_auto_attempt_global) on a one-rank gloo group: the
+    exchange after every attempt has nothing to gather, so the solve equals the plain device-controlled one bit
+    for bit (the same tiling, partials and decisions); an exchange that fails ends the solve with an error."""
+    import torch.distributed as dist
+    from genpose2_amd import shard, synthetic
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    B, K = 6, 24
+    pts, center = synthetic.make_batch(8, B, 1024)
+    data = lambda: {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV)}  # noqa
+    cfg = GenPoseConfig(device=DEV, sampler_mode=["ode"], sampling_steps=None, T0=0.55, seed=3)
+    ref_agent = PoseNet(cfg).eval()
+    ref, _ = ref_agent.pred_func(data(), K, T0=0.55)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{29100 + os.getpid() % 90}", rank=0, world_size=1)
+    try:
+        agent = PoseNet(cfg).eval()
+        agent.global_batch = shard.GlobalBatch.of(B)
+        got, _ = agent.pred_func(data(), K, T0=0.55)
+        assert torch.equal(got, ref) and agent.last_nfev == ref_agent.last_nfev
+
+        def failing(self, ctx, attempt, slot_ptr, n, stream):
+            if attempt == 2:
+                self.error = RuntimeError("injected exchange failure")
+                return -1
+            return 0
+        monkeypatch.setattr(shard.PartialsExchange, "_call", failing)
+        with pytest.raises(RuntimeError, match="exchange failed"):
+            agent.pred_func(data(), K, T0=0.55)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
