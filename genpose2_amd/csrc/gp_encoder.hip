@@ -1363,6 +1363,101 @@ __global__ __launch_bounds__(256) void proj_xyz_kernel(ProjXyzArgs a) {
     st4(a.q + (size_t)p * a.q_stride + qoff + 4 * g, f32x4{v[0], v[1], v[2], v[3]});
 }
 
+// Per-point layer-0 projection with point features (the DINO-pointwise level 0: c_prev = 384 rgb channels + xyz),
+// both branches in one workgroup: Q[p] = W0 [f_p | x_p] + b, exact fp32 MFMA. Each wave owns 16 * CTW consecutive
+// points and every output tile of both branches (NT0 + NT1): a point's row is read once and each A fragment (the
+// packed layer-0 weights, from L2) feeds CTW column tiles; the k-groups of A and of the B operand (the rows, the xyz
+// group last) are kept RING deep in flight. Per
+// accumulator the MFMA sequence is sa_layer's projection pass (k-group g outer, its four k-steps j inner, the same
+// operands): the same bits, where sa_pair_kernel read each row once per branch with one k-group in flight.
+#ifndef PROJ_FEAT_CTW
+#define PROJ_FEAT_CTW 4
+#endif
+#ifndef PROJ_FEAT_RING
+#define PROJ_FEAT_RING 2
+#endif
+struct ProjFeatArgs {
+    const float* feat;     // (npts, c_prev) point-major
+    const float* xyz;      // (npts, 3)
+    int npts, c_prev;      // points over all objects; channels (a multiple of 16)
+    const float* w0[2];    // packed layer-0 fragments of each branch ((c_prev + 16) / 16 k-groups per tile)
+    const float* b0[2];    // biases, padded to 16
+    float* q;              // (npts, q_stride): branch 0's channels, then branch 1's
+    int q_stride;
+};
+template <int NT0, int NT1, int CTW, int RING>
+__global__ __launch_bounds__(256) void proj_feat_kernel(ProjFeatArgs a) {
+    constexpr int NT = NT0 + NT1;
+    const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p0 = (blockIdx.x * 4 + wid) * 16 * CTW;
+    if (p0 >= a.npts) return;   // whole waves leave together
+    const int FG = a.c_prev >> 4, KG = FG + 1;
+    const __amdgpu_buffer_rsrc_t W0 = make_rsrc(a.w0[0], (uint32_t)(NT0 * KG) * 1024u);
+    const __amdgpu_buffer_rsrc_t W1 = make_rsrc(a.w0[1], (uint32_t)(NT1 * KG) * 1024u);
+    const int voff = lane * 16;
+    bool ok[CTW];
+    const float* row[CTW];
+    f32x4 bx[CTW];   // the xyz k-group: raw coordinates in lanes q == 0 (channels c_prev + 0..2)
+#pragma unroll
+    for (int c = 0; c < CTW; ++c) {
+        const int p = p0 + 16 * c + n;
+        ok[c] = p < a.npts;
+        row[c] = a.feat + (size_t)(ok[c] ? p : 0) * a.c_prev + 4 * q;
+        bx[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (ok[c] && q == 0) {
+            const float* px = a.xyz + (size_t)p * 3;
+            bx[c] = f32x4{ld1(px), ld1(px + 1), ld1(px + 2), 0.f};
+        }
+    }
+    f32x4 acc[NT][CTW];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int c = 0; c < CTW; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // every A fragment (weights, L2) feeds CTW column tiles
+    auto fetch = [&](int g, f32x4 (&af)[NT], f32x4 (&bf)[CTW]) {
+#pragma unroll
+        for (int t = 0; t < NT0; ++t) af[t] = ldbuf4(W0, voff, (t * KG + g) * 1024);
+#pragma unroll
+        for (int t = 0; t < NT1; ++t) af[NT0 + t] = ldbuf4(W1, voff, (t * KG + g) * 1024);
+#pragma unroll
+        for (int c = 0; c < CTW; ++c) bf[c] = g < FG ? (ok[c] ? ld4(row[c] + 16 * g) : f32x4{0.f, 0.f, 0.f, 0.f}) : bx[c];
+    };
+    auto compute = [&](const f32x4 (&af)[NT], const f32x4 (&bf)[CTW]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int c = 0; c < CTW; ++c) acc[t][c] = mfma4(af[t][j], bf[c][j], acc[t][c]);
+    };
+    f32x4 ra[RING][NT], rb[RING][CTW];
+#pragma unroll
+    for (int u = 0; u < RING - 1; ++u)
+        if (u < KG) fetch(u, ra[u], rb[u]);
+    for (int g0 = 0; g0 < KG; g0 += RING) {
+#pragma unroll
+        for (int u = 0; u < RING; ++u) {
+            const int g = g0 + u;
+            if (g < KG) {
+                if (g + RING - 1 < KG) fetch(g + RING - 1, ra[(u + RING - 1) % RING], rb[(u + RING - 1) % RING]);
+                __builtin_amdgcn_sched_barrier(0);
+                compute(ra[u], rb[u]);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int br = t < NT0 ? 0 : 1, T = t < NT0 ? t : t - NT0;
+        const f32x4 bias = ld4(a.b0[br] + 16 * T + 4 * q);
+#pragma unroll
+        for (int c = 0; c < CTW; ++c)
+            if (ok[c])
+                st4(a.q + (size_t)(p0 + 16 * c + n) * a.q_stride + 4 * q + (br ? 16 * NT0 : 0) + 16 * T, acc[t][c] + bias);
+    }
+}
+
 // ============================================================================ host side
 static const int kNpoint[4] = {512, 256, 128, 64};
 static const int kNs[2] = {16, 32};
@@ -1677,6 +1772,24 @@ static int run_sa_level(const EncCtx& c, int l, int c_prev, const float* feat_pr
             const size_t threads = (size_t)pa.npts * std::max(pa.ch[0], pa.ch[1]) / 4;   // per branch (grid y)
             hipLaunchKernelGGL(proj_xyz_kernel, dim3((unsigned)((threads + 255) / 256), 2), dim3(256), 0, st, pa);
             rc = gp_check_launch("proj_xyz_kernel");
+        } else if (l == 0 && !split0 && c_prev % 16 == 0 && pad16(kWidths[0][0][1]) == 16 &&
+                   pad16(kWidths[0][1][1]) == 32) {   // point features at level 0 (DINO-pointwise)
+            ProjFeatArgs pa = {};
+            pa.feat = feat_prev;
+            pa.xyz = xyz_prev;
+            pa.npts = B * n_prev;
+            pa.c_prev = c_prev;
+            for (int br = 0; br < 2; ++br) {
+                pa.w0[br] = pp[br].w[0];
+                pa.b0[br] = pp[br].bias[0];
+            }
+            pa.q = qbuf;
+            pa.q_stride = proj_stride(0);
+            GP_REQUIRE(feat_prev && pa.q_stride == 48, "encoder: level-0 feature projection layout");
+            constexpr int CTW = PROJ_FEAT_CTW;   // points per wave / 16
+            hipLaunchKernelGGL((proj_feat_kernel<1, 2, CTW, PROJ_FEAT_RING>), dim3((pa.npts + 64 * CTW - 1) / (64 * CTW)),
+                               dim3(256), 0, st, pa);
+            rc = gp_check_launch("proj_feat_kernel");
         } else {
             rc = split0 ? run_proj_split(c, l, c_prev, feat_prev, xyz_prev, n_prev, qbuf, st)
                         : launch_pair<4>(pp[0], pp[1], B, st);
