@@ -49,6 +49,7 @@ class PoseNet:
         self.noise_feed: Optional[NoiseFeed] = None
         self._calls = 0
         self.after_encode = None                   # optional callable run by pred_func after the encoder
+        self._geom_stream = None                   # encode_geometry's side stream (DINO-pointwise)
         self.ode_host_control = False              # ODE: True runs the RK45 controller on the host
         self.ode_trace: Optional[list] = None      # ODE: a list receives [t, h, error norm] per step attempt
                                                    # (host controller)
@@ -162,8 +163,19 @@ class PoseNet:
         """data["enc_geometry"]: FPS indices, centroids and ball lists of data["pts"] for every level, in
         this agent's encoder workspace. Every agent of the same encoder family (Light or DINO-pointwise) that
         encodes the same points (the ScoreNet and EnergyNet of one batch) then runs only its MLPs; valid until
-        this agent encodes again."""
-        data["enc_geometry"] = self.encoder.geometry(data["pts"])
+        this agent encodes again. The DINO-pointwise geometry runs on a side stream after the current stream's
+        work: the image branches (ImgEncoder, patch gather) do not read it and start beside it, and the fused
+        encoders wait for its event before their first level."""
+        if not self.pointwise:
+            data["enc_geometry"] = self.encoder.geometry(data["pts"])
+            return
+        if self._geom_stream is None:
+            self._geom_stream = torch.cuda.Stream(device=self.device)
+        gs = self._geom_stream
+        gs.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(gs):
+            data["enc_geometry"] = self.encoder.geometry(data["pts"])
+        data["pts"].record_stream(gs)
 
     @torch.no_grad()
     def encode_func(self, data):

@@ -303,6 +303,49 @@ def test_fus_encoder_shared_geometry_bit_exact(fus_sd):
         b.forward(p, rgb, geometry=g)
 
 
+def test_pointwise_agents_geometry_on_side_stream_bit_exact():
+    """PoseNet.encode_geometry with the DINO-pointwise encoders runs the geometry on a side stream (the image
+    branches start beside it): the ScoreNet and EnergyNet agents' encode_func over that geometry -- the EnergyNet
+    one on a third stream, twice in a row with no synchronisation between the steps -- equal each agent's
+    self-contained encode_func bit for bit."""
+    import numpy as np
+    from genpose2_amd import synthetic
+    from genpose2_amd.agent import PoseNet
+    from genpose2_amd.config import GenPoseConfig
+    B, N = 4, 1024
+    cfg = GenPoseConfig(device=DEV, dino="pointwise")
+    score, energy = PoseNet(cfg).eval(), PoseNet(cfg.copy(agent_type="energy")).eval()
+    pts, center = synthetic.make_batch(83, B, N)
+    rng = np.random.Generator(np.random.PCG64(5))
+    d0 = {"pts": torch.from_numpy(pts).to(DEV), "pts_center": torch.from_numpy(center).to(DEV),
+          "dino_layers": [torch.from_numpy(rng.standard_normal((B, 256, 384), dtype=np.float32)).to(DEV)
+                          for _ in range(3)],
+          "roi_xs": torch.from_numpy(rng.integers(0, 224, size=(B, N)).astype(np.int32)).to(DEV),
+          "roi_ys": torch.from_numpy(rng.integers(0, 224, size=(B, N)).astype(np.int32)).to(DEV)}
+    ref = {}
+    for name, agent in (("score", score), ("energy", energy)):
+        d = dict(d0)
+        agent.encode_func(d)
+        ref[name] = d["pts_feat"].clone()
+    side = torch.cuda.Stream(device=DEV)
+    main = torch.cuda.current_stream()
+    got = []
+    for _ in range(2):
+        data, edata = dict(d0), dict(d0)
+        score.encode_geometry(data)
+        assert score._geom_stream is not None and data["enc_geometry"].event is not None
+        edata["enc_geometry"] = data["enc_geometry"]
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            energy.encode_func(edata)
+        score.encode_func(data)
+        main.wait_stream(side)
+        got.append((data["pts_feat"], edata["pts_feat"]))
+    torch.cuda.synchronize()
+    for fs, fe in got:
+        assert torch.equal(fs, ref["score"]) and torch.equal(fe, ref["energy"])
+
+
 # ---------------------------------------------------------------- whole encoder vs the reference
 def test_fus_encoder_vs_reference_golden(fus_model):
     import make_golden_fus as mf
