@@ -172,6 +172,8 @@ class PoseNet:
         if self._geom_stream is None:
             self._geom_stream = torch.cuda.Stream(device=self.device)
         gs = self._geom_stream
+        pts = data["pts"]
+        self.encoder.workspace(pts.shape[0], pts.shape[1])   # allocated (if it grows) on the caller's stream
         gs.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(gs):
             data["enc_geometry"] = self.encoder.geometry(data["pts"])
