@@ -523,6 +523,24 @@ def _host_status_words(dev):
     return (h, dp.value) if rc == 0 and dp.value else (None, None)
 
 
+_CTL_FREE = {}              # device -> free pinned staging buffers of one controller record
+
+
+def _ctl_staging(dev, nbytes: int) -> torch.Tensor:
+    """A pinned host buffer for the initial controller record (its copy to the device is then asynchronous), leased
+    per solve like the status words; return it with _release_ctl_staging once the stream has drained."""
+    with _HSTAT_LOCK:
+        free = _CTL_FREE.setdefault(dev, [])
+        if free:
+            return free.pop()
+    return torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+
+
+def _release_ctl_staging(dev, buf: torch.Tensor) -> None:
+    with _HSTAT_LOCK:
+        _CTL_FREE.setdefault(dev, []).append(buf)
+
+
 def _release_status_words(dev, lease) -> None:
     if lease[0] is not None:
         with _HSTAT_LOCK:
@@ -592,7 +610,8 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
         t_eval = np.asarray(t_eval, dtype=np.float64)
         if np.any(t_eval < min(t0, tf)) or np.any(t_eval > max(t0, tf)):
             raise ValueError("Values in `t_eval` are not within `t_span`.")
-    h_abs, nfev = initial_step(be, t0, tf, direction)
+    # everything that does not depend on the initial step is set up before select_initial_step's two norm reads, so
+    # the host has only h_abs and the controller record to form between the second read and the first attempt
     dev = be.dev
     gb = be.gb if isinstance(be, GlobalDeviceRk45) else None
     ex = None
@@ -611,9 +630,6 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
         part.zero_()
         ex = PartialsExchange(part, part_n, gb)
     rec = ctypes.sizeof(OdeCtl)
-    c0 = OdeCtl(t=t0, h_abs=float(h_abs), nfev=nfev)
-    c0.kidx[:] = list(range(N_STAGES + 1))
-    ws[:rec].copy_(torch.frombuffer(bytearray(c0), dtype=torch.uint8))
     ybuf = [be.y, torch.empty_like(be.y)]
     kbuf = list(be.K)
     karr = _ptr_array(kbuf)
@@ -643,16 +659,23 @@ def rk45_device(be: DeviceRk45, t0: float, t_bound: float, t_eval: Optional[np.n
         call(n, what, None)
 
     lease = _host_status_words(dev) if os.environ.get("GENPOSE2_ODE_ZC", "1")[:1] != "0" else (None, None)
+    stage = _ctl_staging(dev, rec)
     try:
+        h_abs, nfev = initial_step(be, t0, tf, direction)
+        c0 = OdeCtl(t=t0, h_abs=float(h_abs), nfev=nfev)
+        c0.kidx[:] = list(range(N_STAGES + 1))
+        ctypes.memmove(stage.data_ptr(), ctypes.addressof(c0), rec)
+        ws[:rec].copy_(stage, non_blocking=True)   # pinned: enqueued, no host wait
         if lease[0] is not None:
             n = _attempts_polled(call, be, stream, lease, max_attempts)
         else:
             n = _attempts_evented(launch, ws, rec, stream, side, stat, be, max_attempts)
     finally:
-        # the device may still write the words (the speculative next control) until the stream drains
-        if lease[0] is not None:
-            stream.synchronize()
+        # the device may still write the words (the speculative next control) until the stream drains, and the
+        # controller record's copy may still read the staging buffer
+        stream.synchronize()
         _release_status_words(dev, lease)
+        _release_ctl_staging(dev, stage)
     last = ((n + 2) & 1) * rec
 
     ctl = OdeCtl.from_buffer_copy(bytes(ws[last:last + rec].cpu().numpy()))
